@@ -1,0 +1,197 @@
+"""Python side of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Loads ``oracle/build/liboracle.so`` (built from ``mcgraph_oracle.c`` by
+``oracle/Makefile``) and returns the outputs of the reference's graph stages
+in the canonical form of the golden fixtures (``tests/golden/make_golden.py``):
+
+* S2 ``build_point_in_mask_matrix`` — graph/construction.py:22-64
+* S3 ``process_masks``              — graph/construction.py:137-170
+* S4 ``get_observer_num_thresholds``— graph/construction.py:80-96
+* S5 ``init_nodes``                 — graph/construction.py:66-78
+* S6 ``iterative_clustering``       — graph/iterative_clustering.py:36-43
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` may import this module.  The product library never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+_u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_s2.restype = ctypes.c_int
+        L.orc_s2.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i64p, _i32p,
+                             _u8p, _u16p, _u8p, _u8p]
+        L.orc_s3.restype = ctypes.c_int
+        L.orc_s3.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i64p, _i32p,
+                             _u16p, _u8p, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                             _u8p, _i32p, _u8p]
+        L.orc_observer_hist.restype = None
+        L.orc_observer_hist.argtypes = [ctypes.c_int, ctypes.c_int, _u8p, _u64p]
+        L.orc_thresholds.restype = ctypes.c_int
+        L.orc_thresholds.argtypes = [_u64p, ctypes.c_int, _f32p, _i32p]
+        L.orc_cluster.restype = ctypes.c_int
+        L.orc_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p, ctypes.c_int, _f32p,
+                                  ctypes.c_double, _i32p, _i32p, _i32p, _u8p, _u8p]
+        L.orc_num_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def thresholds_from_hist(hist: np.ndarray):
+    """numpy-2 float32 percentile ladder from an observer-count histogram."""
+    hist = np.ascontiguousarray(hist, dtype=np.uint64)
+    F = len(hist) - 1
+    thr = np.zeros(20, np.float32)
+    isint = np.zeros(20, np.int32)
+    n = lib().orc_thresholds(hist, F, thr, isint)
+    if n < 0:
+        return None, None
+    return thr[:n].copy(), isint[:n].astype(bool)
+
+
+def observer_hist(vf: np.ndarray) -> np.ndarray:
+    vf = np.ascontiguousarray(vf, dtype=np.uint8)
+    M, F = vf.shape
+    hist = np.zeros(F + 1, np.uint64)
+    lib().orc_observer_hist(M, F, vf, hist)
+    return hist
+
+
+def cluster(vf0: np.ndarray, cm0: np.ndarray, thr: np.ndarray, ct: float):
+    """S6 on explicit 0/1 node rows (bytes).  Returns (labels per iteration,
+    level sizes, final label of each initial node, final vf, final cm)."""
+    vf0 = np.ascontiguousarray(vf0, dtype=np.uint8)
+    cm0 = np.ascontiguousarray(cm0, dtype=np.uint8)
+    N0, F = vf0.shape
+    M = cm0.shape[1]
+    thr = np.ascontiguousarray(thr, dtype=np.float32)
+    T = len(thr)
+    labels = np.full((max(T, 1), max(N0, 1)), -1, np.int32)
+    sizes = np.zeros(T + 1, np.int32)
+    final = np.zeros(max(N0, 1), np.int32)
+    vf_out = np.zeros((max(N0, 1), F), np.uint8)
+    cm_out = np.zeros((max(N0, 1), M), np.uint8)
+    K = lib().orc_cluster(N0, F, M, vf0, cm0, T, thr, float(ct), labels, sizes, final, vf_out, cm_out)
+    parts = [labels[t, :sizes[t]].copy() for t in range(T)]
+    return parts, sizes, final[:N0], vf_out[:K], cm_out[:K]
+
+
+def run(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
+        mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
+        contained_threshold, timings: dict | None = None):
+    """Whole S2–S6 path on the CPU; returns the golden-fixture dictionary."""
+    L = lib()
+    P, F = int(num_points), int(num_frames)
+    col = np.ascontiguousarray(mask_col, np.int32)
+    label = np.ascontiguousarray(mask_label, np.int32)
+    off = np.ascontiguousarray(mask_off, np.int64)
+    pts = np.ascontiguousarray(mask_pts, np.int32)
+    M_in = len(col)
+    t0 = time.perf_counter()
+    kept = np.zeros(max(M_in, 1), np.uint8)
+    pim = np.zeros((P, F), np.uint16)
+    pfm = np.zeros((P, F), np.uint8)
+    bnd = np.zeros(P, np.uint8)
+    M = L.orc_s2(P, F, M_in, col, label, off, pts, kept, pim, pfm, bnd)
+    keep_idx = np.nonzero(kept[:M_in])[0]
+    gcol, glabel = col[keep_idx], label[keep_idx]
+    lens = (off[1:] - off[:-1])[keep_idx]
+    goff = np.zeros(M + 1, np.int64)
+    np.cumsum(lens, out=goff[1:])
+    gpts = np.concatenate([pts[off[g]:off[g + 1]] for g in keep_idx]).astype(np.int32) if M else np.zeros(0, np.int32)
+    t1 = time.perf_counter()
+    vf = np.zeros((max(M, 1), F), np.uint8)
+    ctgt = np.zeros((max(M, 1), F), np.int32)
+    useg = np.zeros(max(M, 1), np.uint8)
+    L.orc_s3(P, F, M, gcol, glabel, goff, gpts, pim, bnd, float(mask_visible_threshold),
+             float(contained_threshold), float(undersegment_filter_threshold), vf, ctgt, useg)
+    vf, ctgt, useg = vf[:M], ctgt[:M], useg[:M]
+    t2 = time.perf_counter()
+    hist = observer_hist(vf)
+    thr, thr_isint = thresholds_from_hist(hist)
+    t3 = time.perf_counter()
+    if thr is None:
+        raise IndexError("no positive observer count (np.percentile of an empty array)")
+    node0 = np.nonzero(useg == 0)[0].astype(np.int32)
+    cm = np.zeros((len(node0), M), np.uint8)
+    r, c = np.nonzero(ctgt[node0] >= 0)
+    cm[r, ctgt[node0][r, c]] = 1
+    t4 = time.perf_counter()
+    parts, sizes, final, fvf, fcm = cluster(vf[node0], cm, thr, float(view_consensus_threshold))
+    t5 = time.perf_counter()
+    if timings is not None:
+        timings.update(s2=t1 - t0, s3=t2 - t1, s4=t3 - t2, s6=t5 - t4,
+                       pairs=int(sum(int(s) ** 2 for s in sizes[:-1])) if len(thr) else 0,
+                       threads=L.orc_num_threads())
+
+    out = {}
+    out["gl_col"], out["gl_label"] = gcol.copy(), glabel.copy()
+    out["boundary"] = np.nonzero(bnd)[0].astype(np.int32)
+    nzp, nzc = np.nonzero(pim)
+    out["pim_p"], out["pim_c"], out["pim_v"] = nzp.astype(np.int32), nzc.astype(np.int32), pim[nzp, nzc].astype(np.int32)
+    out["pfm_bits"] = np.packbits(pfm.astype(bool), axis=1)
+    out["vf_bits"] = np.packbits(vf.astype(bool), axis=1)
+    rr, cc = np.nonzero(ctgt >= 0)
+    crow, ccol = rr.astype(np.int32), ctgt[rr, cc].astype(np.int32)
+    order = np.lexsort((ccol, crow))
+    out["c_row"], out["c_col"] = crow[order], ccol[order]
+    out["undersegment"] = np.nonzero(useg)[0].astype(np.int32)
+    out["thr_value"], out["thr_is_int"] = thr, thr_isint
+    out["node0_g"] = node0
+    T = len(thr)
+    out["num_iters"] = np.array(T, np.int32)
+    for t in range(T):
+        out[f"part_{t}"] = parts[t]
+    K = len(fvf)
+    members = [[] for _ in range(K)]
+    for i, k in enumerate(final):
+        members[k].append(int(node0[i]))
+    mo, mi, po, pi_, co, ci = [0], [], [0], [], [0], []
+    for k in range(K):
+        gs = sorted(members[k])
+        mi.extend(gs); mo.append(len(mi))
+        u = np.unique(np.concatenate([gpts[goff[g]:goff[g + 1]] for g in gs])) if gs else np.zeros(0, np.int32)
+        pi_.extend(u.tolist()); po.append(len(pi_))
+        cidx = np.nonzero(fcm[k])[0]
+        ci.extend(cidx.tolist()); co.append(len(ci))
+    out["obj_mask_off"], out["obj_mask_idx"] = np.array(mo, np.int64), np.array(mi, np.int32)
+    out["obj_pt_off"], out["obj_pt_idx"] = np.array(po, np.int64), np.array(pi_, np.int32)
+    out["obj_vf_bits"] = np.packbits(fvf.astype(bool), axis=1)
+    out["obj_c_off"], out["obj_c_idx"] = np.array(co, np.int64), np.array(ci, np.int32)
+    out["obj_node_info"] = np.array([(T, k) if T else (0, k) for k in range(K)], np.int32).reshape(-1, 2)
+    if T:
+        last = parts[T - 1]
+        sons = [np.nonzero(last == k)[0].astype(np.int32) for k in range(K)]
+    else:
+        sons = [np.zeros(0, np.int32) for _ in range(K)]
+    so = np.zeros(K + 1, np.int64)
+    so[1:] = np.cumsum([len(s) for s in sons])
+    out["obj_son_off"] = so
+    out["obj_son_idx"] = np.concatenate(sons).astype(np.int32) if K else np.zeros(0, np.int32)
+    return out
