@@ -1,0 +1,314 @@
+"""ctypes binding of libmcgraph.so (the C-ABI in include/mcgraph.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).
+There is no fallback: if the shared object is missing or fails to load, every
+entry point raises, so a GPU run can never silently take another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmcgraph.so")
+
+MC_OK = 0
+MC_ERR_INVALID = 1
+MC_ERR_HIP = 2
+MC_ERR_STATE = 3
+MC_ERR_EMPTY_OBSERVERS = 4
+MC_ERR_UNSUPPORTED = 5
+MC_ERR_NO_NODES = 6
+
+EXPORTED = [
+    "mc_ctx_create", "mc_ctx_destroy", "mc_ctx_set_stream", "mc_ctx_get_stream", "mc_ctx_synchronize",
+    "mc_ctx_last_error", "mc_ctx_set_timing", "mc_ctx_get_kernel_time", "mc_ctx_reset_kernel_times",
+    "mc_scene_set_masks", "mc_graph_build", "mc_graph_get_info", "mc_graph_get_global_masks",
+    "mc_graph_get_boundary", "mc_graph_get_point_in_mask", "mc_graph_get_point_frame_bits",
+    "mc_graph_get_visible_frame_bits", "mc_graph_get_contained", "mc_graph_get_undersegment",
+    "mc_graph_get_nodes0", "mc_graph_get_observer_hist", "mc_graph_get_thresholds", "mc_observer_thresholds",
+    "mc_nodes_set",
+    "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_partition",
+    "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
+]
+
+
+class McError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libmcgraph error {code}: {msg}")
+        self.code = code
+
+
+class GraphParams(ctypes.Structure):
+    _fields_ = [("mask_visible_threshold", ctypes.c_double),
+                ("contained_threshold", ctypes.c_double),
+                ("undersegment_filter_threshold", ctypes.c_double)]
+
+
+class GraphInfo(ctypes.Structure):
+    _fields_ = [("num_points", ctypes.c_int64), ("num_frames", ctypes.c_int32), ("num_masks", ctypes.c_int32),
+                ("num_undersegment", ctypes.c_int32), ("num_nodes0", ctypes.c_int32),
+                ("num_contained", ctypes.c_int64), ("num_boundary", ctypes.c_int64),
+                ("num_thresholds", ctypes.c_int32), ("threshold_status", ctypes.c_int32)]
+
+
+class ClusterInfo(ctypes.Structure):
+    _fields_ = [("num_iterations", ctypes.c_int32), ("num_objects", ctypes.c_int32),
+                ("num_nodes0", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("num_object_points", ctypes.c_int64), ("num_object_contained", ctypes.c_int64),
+                ("num_object_masks", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def load():
+    """Load libmcgraph.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    P = ctypes.POINTER
+    sig = {
+        "mc_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
+        "mc_ctx_destroy": (None, [vp]),
+        "mc_ctx_set_stream": (ctypes.c_int, [vp, vp]),
+        "mc_ctx_get_stream": (vp, [vp]),
+        "mc_ctx_synchronize": (ctypes.c_int, [vp]),
+        "mc_ctx_last_error": (ctypes.c_char_p, [vp]),
+        "mc_ctx_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+        "mc_ctx_get_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
+        "mc_ctx_reset_kernel_times": (ctypes.c_int, [vp]),
+        "mc_scene_set_masks": (ctypes.c_int, [vp, i64, i32, i32, vp, vp, vp, vp, ctypes.c_int]),
+        "mc_graph_build": (ctypes.c_int, [vp, P(GraphParams)]),
+        "mc_graph_get_info": (ctypes.c_int, [vp, P(GraphInfo)]),
+        "mc_graph_get_global_masks": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_boundary": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_point_in_mask": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_point_frame_bits": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_visible_frame_bits": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_contained": (ctypes.c_int, [vp, vp, vp]),
+        "mc_graph_get_undersegment": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_nodes0": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_observer_hist": (ctypes.c_int, [vp, vp]),
+        "mc_graph_get_thresholds": (ctypes.c_int, [vp, vp, vp, P(i32)]),
+        "mc_observer_thresholds": (ctypes.c_int, [vp, i32, i32, vp, vp, vp, P(i32)]),
+        "mc_nodes_set": (ctypes.c_int, [vp, i32, i32, i32, i64, vp, vp, vp, vp, vp]),
+        "mc_cluster_run": (ctypes.c_int, [vp, vp, i32, dbl]),
+        "mc_cluster_get_info": (ctypes.c_int, [vp, P(ClusterInfo)]),
+        "mc_cluster_get_level_sizes": (ctypes.c_int, [vp, vp]),
+        "mc_cluster_get_partition": (ctypes.c_int, [vp, i32, vp]),
+        "mc_cluster_get_edge_counts": (ctypes.c_int, [vp, vp]),
+        "mc_cluster_get_final_labels": (ctypes.c_int, [vp, vp]),
+        "mc_cluster_get_objects": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One libmcgraph context (device memory + stream) — one scene at a time."""
+
+    def __init__(self, device: int = 0):
+        self.L = load()
+        h = ctypes.c_void_p()
+        rc = self.L.mc_ctx_create(int(device), ctypes.byref(h))
+        if rc != MC_OK:
+            raise McError(rc, "mc_ctx_create failed (no HIP device?)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != MC_OK:
+            raise McError(rc, self.L.mc_ctx_last_error(self.h).decode())
+
+    # ---- context ----
+    def set_stream(self, stream_handle):
+        self._check(self.L.mc_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle) if stream_handle else None))
+
+    def stream(self):
+        return self.L.mc_ctx_get_stream(self.h)
+
+    def synchronize(self):
+        self._check(self.L.mc_ctx_synchronize(self.h))
+
+    def set_timing(self, on: bool):
+        self._check(self.L.mc_ctx_set_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self, name: str):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._check(self.L.mc_ctx_get_kernel_time(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def reset_kernel_times(self):
+        self._check(self.L.mc_ctx_reset_kernel_times(self.h))
+
+    # ---- scene ----
+    def set_masks(self, num_points, num_frames, mask_col, mask_label, mask_off, mask_pts=None, pts_device_ptr=None):
+        col = np.ascontiguousarray(mask_col, np.int32)
+        lab = np.ascontiguousarray(mask_label, np.int32)
+        off = np.ascontiguousarray(mask_off, np.int64)
+        if pts_device_ptr is not None:
+            pts_p, on_dev = ctypes.c_void_p(int(pts_device_ptr)), 1
+        else:
+            pts = np.ascontiguousarray(mask_pts, np.int32)
+            self._keep_pts = pts
+            pts_p, on_dev = _ptr(pts), 0
+        self._check(self.L.mc_scene_set_masks(self.h, int(num_points), int(num_frames), len(col), _ptr(col),
+                                               _ptr(lab), _ptr(off), pts_p, on_dev))
+
+    def build(self, mask_visible_threshold, contained_threshold, undersegment_filter_threshold):
+        prm = GraphParams(float(mask_visible_threshold), float(contained_threshold),
+                          float(undersegment_filter_threshold))
+        self._check(self.L.mc_graph_build(self.h, ctypes.byref(prm)))
+
+    def graph_info(self) -> GraphInfo:
+        info = GraphInfo()
+        self._check(self.L.mc_graph_get_info(self.h, ctypes.byref(info)))
+        return info
+
+    def global_masks(self, M):
+        out = np.zeros(max(M, 1), np.int32)
+        self._check(self.L.mc_graph_get_global_masks(self.h, _ptr(out)))
+        return out[:M]
+
+    def boundary(self, P):
+        out = np.zeros(max(P, 1), np.uint8)
+        self._check(self.L.mc_graph_get_boundary(self.h, _ptr(out)))
+        return out[:P]
+
+    def point_in_mask(self, P, F):
+        out = np.zeros((max(P, 1), max(F, 1)), np.uint16)
+        self._check(self.L.mc_graph_get_point_in_mask(self.h, _ptr(out)))
+        return out[:P, :F]
+
+    def point_frame_bits(self, P, F):
+        FW = (F + 63) // 64
+        out = np.zeros((max(P, 1), max(FW, 1)), np.uint64)
+        self._check(self.L.mc_graph_get_point_frame_bits(self.h, _ptr(out)))
+        return out[:P, :FW]
+
+    def visible_frame_bits(self, M, F):
+        FW = (F + 63) // 64
+        out = np.zeros((max(M, 1), max(FW, 1)), np.uint64)
+        self._check(self.L.mc_graph_get_visible_frame_bits(self.h, _ptr(out)))
+        return out[:M, :FW]
+
+    def contained(self, M, nnz):
+        off = np.zeros(M + 1, np.int64)
+        idx = np.zeros(max(nnz, 1), np.int32)
+        self._check(self.L.mc_graph_get_contained(self.h, _ptr(off), _ptr(idx)))
+        return off, idx[:nnz]
+
+    def undersegment(self, n):
+        out = np.zeros(max(n, 1), np.int32)
+        self._check(self.L.mc_graph_get_undersegment(self.h, _ptr(out)))
+        return out[:n]
+
+    def nodes0(self, n):
+        out = np.zeros(max(n, 1), np.int32)
+        self._check(self.L.mc_graph_get_nodes0(self.h, _ptr(out)))
+        return out[:n]
+
+    def observer_hist(self, F):
+        out = np.zeros(F + 1, np.uint64)
+        self._check(self.L.mc_graph_get_observer_hist(self.h, _ptr(out)))
+        return out
+
+    def thresholds(self):
+        thr = np.zeros(20, np.float32)
+        isint = np.zeros(20, np.int32)
+        n = ctypes.c_int32()
+        self._check(self.L.mc_graph_get_thresholds(self.h, _ptr(thr), _ptr(isint), ctypes.byref(n)))
+        return thr[:n.value].copy(), isint[:n.value].astype(bool)
+
+    def observer_thresholds(self, vf_bits, num_frames):
+        """get_observer_num_thresholds (construction.py:80-96) on explicit VF bit rows."""
+        vf = np.ascontiguousarray(vf_bits, np.uint64)
+        thr = np.zeros(20, np.float32)
+        isint = np.zeros(20, np.int32)
+        n = ctypes.c_int32()
+        self._check(self.L.mc_observer_thresholds(self.h, vf.shape[0], int(num_frames), _ptr(vf), _ptr(thr),
+                                                  _ptr(isint), ctypes.byref(n)))
+        return thr[:n.value].copy(), isint[:n.value].astype(bool)
+
+    # ---- nodes / clustering ----
+    def set_nodes(self, num_frames, num_masks, num_points, vf_bits, c_off, c_idx, pt_off, pt_idx):
+        vf = np.ascontiguousarray(vf_bits, np.uint64)
+        c_off = np.ascontiguousarray(c_off, np.int64)
+        c_idx = np.ascontiguousarray(c_idx, np.int32)
+        pt_off = np.ascontiguousarray(pt_off, np.int64)
+        pt_idx = np.ascontiguousarray(pt_idx, np.int32)
+        n = len(c_off) - 1
+        self._check(self.L.mc_nodes_set(self.h, n, int(num_frames), int(num_masks), int(num_points), _ptr(vf),
+                                        _ptr(c_off), _ptr(c_idx), _ptr(pt_off), _ptr(pt_idx)))
+
+    def cluster(self, thresholds, connect_threshold):
+        if thresholds is None:
+            self._check(self.L.mc_cluster_run(self.h, None, 0, float(connect_threshold)))
+        else:
+            thr = np.ascontiguousarray(np.asarray(thresholds, dtype=np.float32))
+            self._check(self.L.mc_cluster_run(self.h, _ptr(thr), len(thr), float(connect_threshold)))
+
+    def cluster_info(self) -> ClusterInfo:
+        info = ClusterInfo()
+        self._check(self.L.mc_cluster_get_info(self.h, ctypes.byref(info)))
+        return info
+
+    def level_sizes(self, n_iter):
+        out = np.zeros(n_iter + 1, np.int32)
+        self._check(self.L.mc_cluster_get_level_sizes(self.h, _ptr(out)))
+        return out
+
+    def partition(self, t, n):
+        out = np.zeros(max(n, 1), np.int32)
+        self._check(self.L.mc_cluster_get_partition(self.h, int(t), _ptr(out)))
+        return out[:n]
+
+    def edge_counts(self, n_iter):
+        out = np.zeros(max(n_iter, 1), np.int64)
+        self._check(self.L.mc_cluster_get_edge_counts(self.h, _ptr(out)))
+        return out[:n_iter]
+
+    def final_labels(self, n0):
+        out = np.zeros(max(n0, 1), np.int32)
+        self._check(self.L.mc_cluster_get_final_labels(self.h, _ptr(out)))
+        return out[:n0]
+
+    def objects(self, info: ClusterInfo, F):
+        K = info.num_objects
+        FW = (F + 63) // 64
+        vf = np.zeros((max(K, 1), max(FW, 1)), np.uint64)
+        c_off = np.zeros(K + 1, np.int64)
+        c_idx = np.zeros(max(info.num_object_contained, 1), np.int32)
+        pt_off = np.zeros(K + 1, np.int64)
+        pt_idx = np.zeros(max(info.num_object_points, 1), np.int32)
+        m_off = np.zeros(K + 1, np.int64)
+        m_idx = np.zeros(max(info.num_object_masks, 1), np.int32)
+        self._check(self.L.mc_cluster_get_objects(self.h, _ptr(vf), _ptr(c_off), _ptr(c_idx), _ptr(pt_off),
+                                                  _ptr(pt_idx), _ptr(m_off), _ptr(m_idx)))
+        return dict(vf_bits=vf[:K, :FW], c_off=c_off, c_idx=c_idx[:c_off[-1]], pt_off=pt_off,
+                    pt_idx=pt_idx[:pt_off[-1]], mask_off=m_off, mask_idx=m_idx[:m_off[-1]])

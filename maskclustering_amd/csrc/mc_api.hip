@@ -1,0 +1,1003 @@
+// mc_api.hip — C-ABI of libmcgraph: context, scene upload, S2–S6 orchestration, getters.
+// Single translation unit: the kernels live in mc_kernels.inl.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "mc_internal.hpp"
+#include "mc_kernels.inl"
+
+using mc::DevBuf;
+using mc::McError;
+using mc::TimedScope;
+using mc::ceil_div;
+
+namespace {
+
+// device-side statistics block (copied to pinned host memory in one transfer)
+enum Stat : int {
+    ST_NBND = 0,      // boundary points
+    ST_NNZC = 1,      // contained entries after undo
+    ST_N0 = 2,        // level-0 nodes
+    ST_NTHR = 3,      // thresholds
+    ST_THR_STATUS = 4,
+    ST_K = 5,         // final objects
+    ST_WORDS = 6,     // point-bitmap words
+    ST_NPTS = 7,      // object points (sum)
+    ST_COUNT = 8,
+};
+
+}  // namespace
+
+struct mc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    mc::KernelTimer timer;
+    int *h_stats = nullptr;  // pinned
+
+    // ---- scene ----
+    bool have_scene = false, have_graph = false, have_nodes = false, have_cluster = false;
+    bool nodes_from_graph = false;
+    int64_t P = 0;
+    int F = 0, FW = 0, M = 0, M_in = 0;
+    int nnz = 0;
+    std::vector<int32_t> h_col, h_label, h_in_index, h_off;
+    DevBuf d_mask_off, d_mask_pts, d_mask_col, d_mask_label, d_frame_start, d_valid;
+    // ---- S2 ----
+    DevBuf d_deg, d_pt_off, d_cursor, d_pt_list, d_boundary, d_pfm, d_scan_tmp;
+    // ---- S3/S5 ----
+    DevBuf d_ctmp, d_crow_len, d_useg, d_keep_cnt, d_node_flag, d_node_pos, d_c_off, d_c_idx, d_vf;
+    // ---- S4 ----
+    DevBuf d_hist, d_thr, d_isint, d_stats;
+    // ---- level-0 nodes ----
+    int N0 = 0;        // host copy (valid after sync_stats or mc_nodes_set)
+    int Mn = 0;        // mask-id space of C rows
+    int64_t n0_pts_total = 0;
+    DevBuf d_node0_g, d_n0_off, d_n0_len, d_n0_ptoff, d_n0_ptlen, d_n0_vf, d_user_cidx, d_user_pts;
+    const int *n0_pool = nullptr;
+    const int *n0_pts = nullptr;
+    int64_t nnzC0 = 0;
+    // ---- S6 ----
+    DevBuf d_parent, d_root, d_isroot, d_rank, d_label, d_levels, d_memcnt, d_memoff, d_ublen, d_newoff;
+    DevBuf d_members, d_colcnt, d_coloff, d_colnodes, d_ovf_list, d_ovf_n, d_scratch, d_touched, d_edges;
+    DevBuf d_Nlev, d_smin, d_final_label;
+    DevBuf d_poolA, d_poolB, d_offA, d_offB, d_lenA, d_lenB, d_vfA, d_vfB;
+    DevBuf d_pmin, d_pmax, d_nwords, d_woff, d_bm, d_ptcnt, d_ptoff_out, d_pts_out;
+    int scratch_n0 = -1;
+    int n_iter = 0;
+    // final object state (device pointers into the pools)
+    const int *fin_off = nullptr, *fin_len = nullptr, *fin_pool = nullptr;
+    const unsigned long long *fin_vf = nullptr;
+    int K = 0;
+    int64_t npts = 0;
+};
+
+namespace {
+
+int fail(mc_ctx *ctx, const McError &e)
+{
+    if (ctx) ctx->err = e.msg;
+    return e.code;
+}
+
+template <typename Fn>
+int guarded(mc_ctx *ctx, Fn &&fn)
+{
+    if (!ctx) return MC_ERR_INVALID;
+    try {
+        MC_HIP(hipSetDevice(ctx->device));
+        fn();
+        return MC_OK;
+    } catch (const McError &e) {
+        return fail(ctx, e);
+    } catch (const std::exception &e) {
+        return fail(ctx, McError{MC_ERR_INVALID, e.what()});
+    }
+}
+
+inline dim3 grid_for(int64_t n, int per_block = 256, int cap = 4096)
+{
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return dim3(static_cast<unsigned>(g));
+}
+
+void sync_stats(mc_ctx *ctx)
+{
+    MC_HIP(hipMemcpyAsync(ctx->h_stats, ctx->d_stats.ptr, ST_COUNT * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    MC_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->timer.collect();
+}
+
+// smin[o] = smallest S with fl32(S / fl32(o + 1e-7f)) >= fl32(ct)  (iterative_clustering.py:23,28);
+// INT_MAX when no S <= max_s qualifies.  Float32 arithmetic like torch on the device.
+std::vector<int> build_smin(int F, double ct, int max_s)
+{
+    std::vector<int> smin(F + 1, std::numeric_limits<int>::max());
+    const float ctf = static_cast<float>(ct);
+    if (std::isnan(ctf)) return smin;
+    for (int o = 0; o <= F; o++) {
+        volatile float den = static_cast<float>(o) + 1e-7f;
+        double est = std::floor(static_cast<double>(ct) * (static_cast<double>(o) + 1e-7)) - 2.0;
+        int64_t s = est < 0 ? 0 : static_cast<int64_t>(est);
+        if (s > static_cast<int64_t>(max_s) + 1) continue;
+        for (; s <= static_cast<int64_t>(max_s) + 1; s++) {
+            volatile float rate = static_cast<float>(s) / den;
+            if (rate >= ctf) {
+                smin[o] = static_cast<int>(s);
+                break;
+            }
+        }
+    }
+    return smin;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_ctx_create(int device, mc_ctx **out)
+{
+    if (!out) return MC_ERR_INVALID;
+    *out = nullptr;
+    mc_ctx *ctx = new mc_ctx();
+    ctx->device = device;
+    int rc = guarded(ctx, [&] {
+        MC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+        MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stats), ST_COUNT * sizeof(int), hipHostMallocDefault));
+        ctx->d_stats.reserve(ST_COUNT * sizeof(int));
+        MC_HIP(hipMemset(ctx->d_stats.ptr, 0, ST_COUNT * sizeof(int)));
+    });
+    if (rc != MC_OK) {
+        mc_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return MC_OK;
+}
+
+void mc_ctx_destroy(mc_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    DevBuf *bufs[] = {&ctx->d_mask_off, &ctx->d_mask_pts, &ctx->d_mask_col, &ctx->d_mask_label, &ctx->d_frame_start,
+                      &ctx->d_valid, &ctx->d_deg, &ctx->d_pt_off, &ctx->d_cursor, &ctx->d_pt_list, &ctx->d_boundary,
+                      &ctx->d_pfm, &ctx->d_scan_tmp, &ctx->d_ctmp, &ctx->d_crow_len, &ctx->d_useg, &ctx->d_keep_cnt,
+                      &ctx->d_node_flag, &ctx->d_node_pos, &ctx->d_c_off, &ctx->d_c_idx, &ctx->d_vf, &ctx->d_hist,
+                      &ctx->d_thr, &ctx->d_isint, &ctx->d_stats, &ctx->d_node0_g, &ctx->d_n0_off, &ctx->d_n0_len,
+                      &ctx->d_n0_ptoff, &ctx->d_n0_ptlen, &ctx->d_n0_vf, &ctx->d_user_cidx, &ctx->d_user_pts,
+                      &ctx->d_parent, &ctx->d_root, &ctx->d_isroot, &ctx->d_rank, &ctx->d_label, &ctx->d_levels,
+                      &ctx->d_memcnt, &ctx->d_memoff, &ctx->d_ublen, &ctx->d_newoff, &ctx->d_members, &ctx->d_colcnt,
+                      &ctx->d_coloff, &ctx->d_colnodes, &ctx->d_ovf_list, &ctx->d_ovf_n, &ctx->d_scratch,
+                      &ctx->d_touched, &ctx->d_edges, &ctx->d_Nlev, &ctx->d_smin, &ctx->d_final_label,
+                      &ctx->d_poolA, &ctx->d_poolB, &ctx->d_offA, &ctx->d_offB, &ctx->d_lenA, &ctx->d_lenB,
+                      &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
+                      &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out};
+    for (DevBuf *b : bufs) b->release();
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int mc_ctx_set_stream(mc_ctx *ctx, void *hip_stream)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->own_stream) MC_HIP(hipStreamDestroy(ctx->stream));
+        if (hip_stream) {
+            ctx->stream = static_cast<hipStream_t>(hip_stream);
+            ctx->own_stream = false;
+        } else {
+            MC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+            ctx->own_stream = true;
+        }
+    });
+}
+
+void *mc_ctx_get_stream(mc_ctx *ctx) { return ctx ? static_cast<void *>(ctx->stream) : nullptr; }
+
+int mc_ctx_synchronize(mc_ctx *ctx)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->timer.collect();
+    });
+}
+
+const char *mc_ctx_last_error(mc_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mc_ctx_set_timing(mc_ctx *ctx, int enable)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->timer.collect();
+        ctx->timer.enabled = enable != 0;
+    });
+}
+
+int mc_ctx_get_kernel_time(mc_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->timer.collect();
+        auto it = ctx->timer.totals.find(kernel ? kernel : "");
+        if (total_ms) *total_ms = it == ctx->timer.totals.end() ? 0.0 : it->second.first;
+        if (launches) *launches = it == ctx->timer.totals.end() ? 0 : it->second.second;
+    });
+}
+
+int mc_ctx_reset_kernel_times(mc_ctx *ctx)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->timer.collect();
+        ctx->timer.totals.clear();
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// scene input
+// ---------------------------------------------------------------------------------------------
+__global__ void k_validate_pts(const int *pts, int nnz, int64_t P, int *bad)
+{
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nnz; i += gridDim.x * 256)
+        if (pts[i] < 0 || pts[i] >= P) atomicOr(bad, 1);
+}
+
+int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int32_t num_masks_in,
+                       const int32_t *mask_col, const int32_t *mask_label, const int64_t *mask_off,
+                       const int32_t *mask_pts, int pts_on_device)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_points >= 0 && num_points < (int64_t(1) << 31) - 1, MC_ERR_UNSUPPORTED, "num_points out of range");
+        MC_REQUIRE(num_frames >= 0 && num_frames <= 16384, MC_ERR_UNSUPPORTED, "num_frames must be <= 16384");
+        MC_REQUIRE(num_masks_in >= 0, MC_ERR_INVALID, "num_masks < 0");
+        MC_REQUIRE(num_masks_in == 0 || (mask_col && mask_label && mask_off), MC_ERR_INVALID, "null mask arrays");
+        MC_REQUIRE(!mask_off || mask_off[0] == 0, MC_ERR_INVALID, "mask_off[0] != 0");
+        const int64_t nnz = num_masks_in ? mask_off[num_masks_in] : 0;
+        MC_REQUIRE(nnz < (int64_t(1) << 31) - 1, MC_ERR_UNSUPPORTED, "more than 2^31 mask points");
+        MC_REQUIRE(nnz == 0 || mask_pts, MC_ERR_INVALID, "null mask_pts");
+        ctx->have_scene = ctx->have_graph = ctx->have_nodes = ctx->have_cluster = false;
+        ctx->P = num_points;
+        ctx->F = num_frames;
+        ctx->FW = (num_frames + 63) / 64;
+        ctx->M_in = num_masks_in;
+        // validation + the frame-skip rule (construction.py:50-51)
+        std::vector<int64_t> frame_pts(std::max(1, num_frames), 0);
+        std::vector<int> frame_masks(std::max(1, num_frames), 0);
+        for (int g = 0; g < num_masks_in; g++) {
+            const int c = mask_col[g];
+            MC_REQUIRE(c >= 0 && c < num_frames, MC_ERR_INVALID, "mask_col out of range");
+            MC_REQUIRE(g == 0 || mask_col[g - 1] <= c, MC_ERR_INVALID, "mask_col must be non-decreasing");
+            MC_REQUIRE(mask_label[g] >= 1 && mask_label[g] <= 65535, MC_ERR_INVALID, "mask label must be in [1, 65535]");
+            MC_REQUIRE(mask_off[g + 1] >= mask_off[g], MC_ERR_INVALID, "mask_off must be non-decreasing");
+            frame_pts[c] += mask_off[g + 1] - mask_off[g];
+            frame_masks[c]++;
+            MC_REQUIRE(frame_masks[c] < mc::kMaxMasksPerFrame, MC_ERR_UNSUPPORTED, "more than 4095 masks in a frame");
+        }
+        {
+            std::vector<int> seen(65536, -1);
+            for (int g = 0; g < num_masks_in; g++) {
+                MC_REQUIRE(seen[mask_label[g]] != mask_col[g], MC_ERR_INVALID, "duplicate mask label within a frame");
+                seen[mask_label[g]] = mask_col[g];
+            }
+        }
+        ctx->h_col.clear();
+        ctx->h_label.clear();
+        ctx->h_in_index.clear();
+        ctx->h_off.assign(1, 0);
+        for (int g = 0; g < num_masks_in; g++) {
+            if (frame_pts[mask_col[g]] == 0) continue;  // masks of a skipped frame have no points
+            ctx->h_in_index.push_back(g);
+            ctx->h_col.push_back(mask_col[g]);
+            ctx->h_label.push_back(mask_label[g]);
+            ctx->h_off.push_back(static_cast<int32_t>(mask_off[g + 1]));
+        }
+        const int M = static_cast<int>(ctx->h_col.size());
+        ctx->M = M;
+        ctx->nnz = static_cast<int>(nnz);
+        MC_REQUIRE(M <= 262144, MC_ERR_UNSUPPORTED, "more than 262144 global masks");
+        std::vector<int32_t> frame_start(num_frames + 1, 0);
+        {
+            int g = 0;
+            for (int c = 0; c <= num_frames; c++) {
+                while (g < M && ctx->h_col[g] < c) g++;
+                frame_start[c] = g;
+            }
+        }
+        const int64_t P = num_points;
+        const int F = num_frames, FW = ctx->FW;
+        hipStream_t s = ctx->stream;
+        ctx->d_mask_off.reserve((M + 1) * sizeof(int));
+        ctx->d_mask_col.reserve((M + 1) * sizeof(int));
+        ctx->d_mask_label.reserve((M + 1) * sizeof(int));
+        ctx->d_frame_start.reserve((F + 2) * sizeof(int));
+        ctx->d_mask_pts.reserve((nnz + 1) * sizeof(int));
+        ctx->d_valid.reserve(sizeof(int));
+        MC_HIP(hipMemcpyAsync(ctx->d_mask_off.ptr, ctx->h_off.data(), (M + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        if (M) {
+            MC_HIP(hipMemcpyAsync(ctx->d_mask_col.ptr, ctx->h_col.data(), M * sizeof(int), hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(ctx->d_mask_label.ptr, ctx->h_label.data(), M * sizeof(int), hipMemcpyHostToDevice, s));
+        }
+        MC_HIP(hipMemcpyAsync(ctx->d_frame_start.ptr, frame_start.data(), (F + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        if (nnz)
+            MC_HIP(hipMemcpyAsync(ctx->d_mask_pts.ptr, mask_pts, nnz * sizeof(int),
+                                  pts_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+        MC_HIP(hipMemsetAsync(ctx->d_valid.ptr, 0, sizeof(int), s));
+        if (nnz)
+            hipLaunchKernelGGL(k_validate_pts, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(),
+                               static_cast<int>(nnz), P, ctx->d_valid.as<int>());
+        int bad = 0;
+        MC_HIP(hipMemcpyAsync(&bad, ctx->d_valid.ptr, sizeof(int), hipMemcpyDeviceToHost, s));
+        MC_HIP(hipStreamSynchronize(s));
+        MC_REQUIRE(bad == 0, MC_ERR_INVALID, "mask point id out of [0, num_points)");
+
+        // S2/S3/S4 buffers (allocated once per scene; nothing is allocated while building)
+        ctx->d_deg.reserve((P + 1) * sizeof(int));
+        ctx->d_pt_off.reserve((P + 2) * sizeof(int));
+        ctx->d_cursor.reserve((P + 1) * sizeof(int));
+        ctx->d_pt_list.reserve((nnz + 1) * sizeof(unsigned));
+        ctx->d_boundary.reserve(P + 1);
+        ctx->d_pfm.reserve((P * FW + 1) * sizeof(unsigned long long));
+        ctx->d_scan_tmp.reserve((2 * (P / 4096 + 4) + 16) * sizeof(int));
+        ctx->d_ctmp.reserve((static_cast<size_t>(M) * F + 1) * sizeof(int));
+        ctx->d_crow_len.reserve((M + 1) * sizeof(int));
+        ctx->d_useg.reserve(M + 1);
+        ctx->d_keep_cnt.reserve((M + 1) * sizeof(int));
+        ctx->d_node_flag.reserve((M + 1) * sizeof(int));
+        ctx->d_node_pos.reserve((M + 2) * sizeof(int));
+        ctx->d_c_off.reserve((M + 2) * sizeof(int));
+        ctx->d_c_idx.reserve((static_cast<size_t>(M) * F + 1) * sizeof(int));
+        ctx->d_vf.reserve((static_cast<size_t>(M) * FW + 1) * sizeof(unsigned long long));
+        ctx->d_hist.reserve((F + 2) * sizeof(unsigned long long));
+        ctx->d_thr.reserve(32 * sizeof(float));
+        ctx->d_isint.reserve(32 * sizeof(int));
+        ctx->d_node0_g.reserve((M + 1) * sizeof(int));
+        ctx->d_n0_off.reserve((M + 1) * sizeof(int));
+        ctx->d_n0_len.reserve((M + 1) * sizeof(int));
+        ctx->d_n0_ptoff.reserve((M + 1) * sizeof(int));
+        ctx->d_n0_ptlen.reserve((M + 1) * sizeof(int));
+        ctx->d_n0_vf.reserve((static_cast<size_t>(M) * FW + 1) * sizeof(unsigned long long));
+        ctx->have_scene = true;
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// S2–S5
+// ---------------------------------------------------------------------------------------------
+int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_scene, MC_ERR_STATE, "mc_graph_build before mc_scene_set_masks");
+        MC_REQUIRE(params, MC_ERR_INVALID, "null params");
+        hipStream_t s = ctx->stream;
+        const int64_t P = ctx->P;
+        const int F = ctx->F, FW = ctx->FW, M = ctx->M, nnz = ctx->nnz;
+        int *stats = ctx->d_stats.as<int>();
+        MC_HIP(hipMemsetAsync(stats, 0, ST_COUNT * sizeof(int), s));
+        ctx->have_cluster = false;
+        {  // S2
+            TimedScope ts(ctx->timer, s, "s2_point_lists");
+            MC_HIP(hipMemsetAsync(ctx->d_deg.ptr, 0, (P + 1) * sizeof(int), s));
+            if (nnz)
+                hipLaunchKernelGGL(mc::k_s2_degree, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(), nnz,
+                                   ctx->d_deg.as<int>());
+            mc::scan_large(s, ctx->d_deg.as<int>(), ctx->d_pt_off.as<int>(), static_cast<int>(P), ctx->d_scan_tmp.as<int>());
+            MC_HIP(hipMemsetAsync(ctx->d_cursor.ptr, 0, (P + 1) * sizeof(int), s));
+            if (M)
+                hipLaunchKernelGGL(mc::k_s2_scatter, dim3(M), dim3(256), 0, s, ctx->d_mask_off.as<int>(),
+                                   ctx->d_mask_pts.as<int>(), ctx->d_mask_col.as<int>(), ctx->d_frame_start.as<int>(),
+                                   ctx->d_pt_off.as<int>(), ctx->d_cursor.as<int>(), ctx->d_pt_list.as<unsigned>());
+            if (P)
+                hipLaunchKernelGGL(mc::k_s2_points, dim3(ceil_div(P, 256)), dim3(256), 0, s, ctx->d_pt_off.as<int>(),
+                                   ctx->d_pt_list.as<unsigned>(), static_cast<int>(P), FW,
+                                   ctx->d_boundary.as<unsigned char>(), ctx->d_pfm.as<unsigned long long>(),
+                                   stats + ST_NBND);
+        }
+        if (M) {  // S3
+            TimedScope ts(ctx->timer, s, "s3_masks");
+            hipLaunchKernelGGL(mc::k_s3_masks, dim3(M), dim3(mc::kS3Threads), 0, s, ctx->d_mask_off.as<int>(),
+                               ctx->d_mask_pts.as<int>(), ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(),
+                               ctx->d_boundary.as<unsigned char>(), ctx->d_frame_start.as<int>(),
+                               ctx->d_mask_label.as<int>(), F, params->mask_visible_threshold,
+                               params->contained_threshold, params->undersegment_filter_threshold,
+                               ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
+        }
+        if (M) {  // S3 undo + S5
+            TimedScope ts(ctx->timer, s, "s3_undo_s5");
+            hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
+                               ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
+                               ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>());
+            mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC);
+            hipLaunchKernelGGL(mc::k_s3_undo_write, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
+                               ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), ctx->d_mask_col.as<int>(), M,
+                               F, FW, ctx->d_c_off.as<int>(), ctx->d_c_idx.as<int>(),
+                               ctx->d_vf.as<unsigned long long>());
+            mc::scan_device_n(s, ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), nullptr, M, stats + ST_N0);
+            hipLaunchKernelGGL(mc::k_s5_nodes, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_node_pos.as<int>(),
+                               ctx->d_useg.as<unsigned char>(), ctx->d_c_off.as<int>(), ctx->d_mask_off.as<int>(),
+                               ctx->d_vf.as<unsigned long long>(), M, FW, ctx->d_node0_g.as<int>(),
+                               ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
+                               ctx->d_n0_ptlen.as<int>(), ctx->d_n0_vf.as<unsigned long long>());
+        }
+        {  // S4
+            TimedScope ts(ctx->timer, s, "s4_observer_hist");
+            MC_HIP(hipMemsetAsync(ctx->d_hist.ptr, 0, (F + 1) * sizeof(unsigned long long), s));
+            if (M && F) {
+                const int nblk = ceil_div(M, mc::kHistTile);
+                const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + (F + 1) * sizeof(unsigned);
+                const int64_t nb = static_cast<int64_t>(nblk) * (nblk + 1) / 2;
+                hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(nb)), dim3(256), lds, s,
+                                   ctx->d_vf.as<unsigned long long>(), M, FW, F, nblk,
+                                   ctx->d_hist.as<unsigned long long>());
+            }
+            hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(64), 0, s, ctx->d_hist.as<unsigned long long>(), F,
+                               ctx->d_thr.as<float>(), ctx->d_isint.as<int>(), stats + ST_NTHR, stats + ST_THR_STATUS);
+        }
+        MC_HIP(hipGetLastError());
+        // level-0 nodes live in the graph's buffers
+        ctx->n0_pool = ctx->d_c_idx.as<int>();
+        ctx->n0_pts = ctx->d_mask_pts.as<int>();
+        ctx->Mn = M;
+        ctx->n0_pts_total = nnz;
+        ctx->nodes_from_graph = true;
+        ctx->have_graph = true;
+        ctx->have_nodes = true;
+    });
+}
+
+int mc_graph_get_info(mc_ctx *ctx, mc_graph_info *info)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph && info, MC_ERR_STATE, "no graph");
+        sync_stats(ctx);
+        const int *h = ctx->h_stats;
+        info->num_points = ctx->P;
+        info->num_frames = ctx->F;
+        info->num_masks = ctx->M;
+        info->num_nodes0 = h[ST_N0];
+        info->num_undersegment = ctx->M - h[ST_N0];
+        info->num_contained = h[ST_NNZC];
+        info->num_boundary = h[ST_NBND];
+        info->num_thresholds = h[ST_NTHR];
+        info->threshold_status = h[ST_THR_STATUS];
+    });
+}
+
+int mc_graph_get_global_masks(mc_ctx *ctx, int32_t *input_index)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_scene, MC_ERR_STATE, "no scene");
+        std::copy(ctx->h_in_index.begin(), ctx->h_in_index.end(), input_index);
+    });
+}
+
+int mc_graph_get_boundary(mc_ctx *ctx, uint8_t *flags)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        if (ctx->P) MC_HIP(hipMemcpyAsync(flags, ctx->d_boundary.ptr, ctx->P, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_graph_get_point_in_mask(mc_ctx *ctx, uint16_t *pim)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        const size_t bytes = static_cast<size_t>(ctx->P) * ctx->F * sizeof(uint16_t);
+        if (!bytes) return;
+        DevBuf tmp;
+        tmp.reserve(bytes);
+        MC_HIP(hipMemsetAsync(tmp.ptr, 0, bytes, ctx->stream));
+        hipLaunchKernelGGL(mc::k_s2_dense_pim, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, ctx->stream,
+                           ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_mask_label.as<int>(),
+                           ctx->d_frame_start.as<int>(), static_cast<int>(ctx->P), ctx->F, tmp.as<unsigned short>());
+        MC_HIP(hipMemcpyAsync(pim, tmp.ptr, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        tmp.release();
+    });
+}
+
+int mc_graph_get_point_frame_bits(mc_ctx *ctx, uint64_t *bits)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        const size_t bytes = static_cast<size_t>(ctx->P) * ctx->FW * 8;
+        if (bytes) MC_HIP(hipMemcpyAsync(bits, ctx->d_pfm.ptr, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_graph_get_visible_frame_bits(mc_ctx *ctx, uint64_t *bits)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        const size_t bytes = static_cast<size_t>(ctx->M) * ctx->FW * 8;
+        if (bytes) MC_HIP(hipMemcpyAsync(bits, ctx->d_vf.ptr, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_graph_get_contained(mc_ctx *ctx, int64_t *row_off, int32_t *col_idx)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        sync_stats(ctx);
+        std::vector<int32_t> off(ctx->M + 1);
+        MC_HIP(hipMemcpyAsync(off.data(), ctx->d_c_off.ptr, (ctx->M + 1) * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        const int nnzc = ctx->h_stats[ST_NNZC];
+        if (nnzc) MC_HIP(hipMemcpyAsync(col_idx, ctx->d_c_idx.ptr, nnzc * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i <= ctx->M; i++) row_off[i] = ctx->M ? off[i] : 0;
+    });
+}
+
+int mc_graph_get_undersegment(mc_ctx *ctx, int32_t *ids)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        std::vector<uint8_t> u(ctx->M);
+        if (ctx->M) MC_HIP(hipMemcpyAsync(u.data(), ctx->d_useg.ptr, ctx->M, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        int k = 0;
+        for (int g = 0; g < ctx->M; g++)
+            if (u[g]) ids[k++] = g;
+    });
+}
+
+int mc_graph_get_nodes0(mc_ctx *ctx, int32_t *mask_index)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        sync_stats(ctx);
+        const int n0 = ctx->h_stats[ST_N0];
+        if (n0) MC_HIP(hipMemcpyAsync(mask_index, ctx->d_node0_g.ptr, n0 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_graph_get_observer_hist(mc_ctx *ctx, uint64_t *hist)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        MC_HIP(hipMemcpyAsync(hist, ctx->d_hist.ptr, (ctx->F + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_graph_get_thresholds(mc_ctx *ctx, float *thr, int32_t *is_int, int32_t *n)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_graph, MC_ERR_STATE, "no graph");
+        sync_stats(ctx);
+        MC_HIP(hipMemcpyAsync(thr, ctx->d_thr.ptr, mc::kMaxThresholds * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipMemcpyAsync(is_int, ctx->d_isint.ptr, mc::kMaxThresholds * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        *n = ctx->h_stats[ST_NTHR];
+        if (ctx->h_stats[ST_THR_STATUS] != MC_OK)
+            throw McError{ctx->h_stats[ST_THR_STATUS], "no positive observer count (np.percentile of an empty array)"};
+    });
+}
+
+int mc_observer_thresholds(mc_ctx *ctx, int32_t num_rows, int32_t num_frames, const uint64_t *vf_bits, float *thr,
+                           int32_t *is_int, int32_t *n)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_rows >= 0 && num_frames >= 0 && num_frames <= 16384, MC_ERR_INVALID, "bad sizes");
+        MC_REQUIRE(thr && is_int && n && (num_rows == 0 || num_frames == 0 || vf_bits), MC_ERR_INVALID, "null argument");
+        hipStream_t s = ctx->stream;
+        const int M = num_rows, F = num_frames, FW = (F + 63) / 64;
+        DevBuf vf, hist, dthr, disint, st;
+        vf.reserve(static_cast<size_t>(M) * FW * 8 + 8);
+        hist.reserve((F + 2) * 8);
+        dthr.reserve(32 * 4);
+        disint.reserve(32 * 4);
+        st.reserve(2 * 4);
+        if (M && FW) MC_HIP(hipMemcpyAsync(vf.ptr, vf_bits, static_cast<size_t>(M) * FW * 8, hipMemcpyHostToDevice, s));
+        MC_HIP(hipMemsetAsync(hist.ptr, 0, (F + 1) * 8, s));
+        if (M && F) {
+            const int nblk = ceil_div(M, mc::kHistTile);
+            const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + (F + 1) * sizeof(unsigned);
+            const int64_t nb = static_cast<int64_t>(nblk) * (nblk + 1) / 2;
+            hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(nb)), dim3(256), lds, s,
+                               vf.as<unsigned long long>(), M, FW, F, nblk, hist.as<unsigned long long>());
+        }
+        hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(64), 0, s, hist.as<unsigned long long>(), F,
+                           dthr.as<float>(), disint.as<int>(), st.as<int>(), st.as<int>() + 1);
+        int hs[2];
+        MC_HIP(hipMemcpyAsync(hs, st.ptr, 8, hipMemcpyDeviceToHost, s));
+        MC_HIP(hipMemcpyAsync(thr, dthr.ptr, mc::kMaxThresholds * 4, hipMemcpyDeviceToHost, s));
+        MC_HIP(hipMemcpyAsync(is_int, disint.ptr, mc::kMaxThresholds * 4, hipMemcpyDeviceToHost, s));
+        MC_HIP(hipStreamSynchronize(s));
+        *n = hs[0];
+        if (hs[1] != MC_OK) throw McError{hs[1], "no positive observer count (np.percentile of an empty array)"};
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// arbitrary level-0 nodes
+// ---------------------------------------------------------------------------------------------
+__global__ void k_nodes_from_csr(int n, const int64_t *c_off, const int64_t *pt_off, int *n_off, int *n_len, int *n_ptoff,
+                                 int *n_ptlen)
+{
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        n_off[i] = static_cast<int>(c_off[i]);
+        n_len[i] = static_cast<int>(c_off[i + 1] - c_off[i]);
+        n_ptoff[i] = static_cast<int>(pt_off[i]);
+        n_ptlen[i] = static_cast<int>(pt_off[i + 1] - pt_off[i]);
+    }
+}
+
+int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num_masks, int64_t num_points,
+                 const uint64_t *vf_bits, const int64_t *c_off, const int32_t *c_idx, const int64_t *pt_off,
+                 const int32_t *pt_idx)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_nodes >= 0 && num_frames >= 0 && num_masks >= 0 && num_points >= 0, MC_ERR_INVALID, "negative size");
+        MC_REQUIRE(num_frames <= 16384, MC_ERR_UNSUPPORTED, "num_frames must be <= 16384");
+        MC_REQUIRE(num_masks <= 262144, MC_ERR_UNSUPPORTED, "num_masks must be <= 262144");
+        MC_REQUIRE(num_nodes == 0 || (vf_bits && c_off && pt_off), MC_ERR_INVALID, "null node arrays");
+        const int64_t nc = num_nodes ? c_off[num_nodes] : 0, np = num_nodes ? pt_off[num_nodes] : 0;
+        MC_REQUIRE(nc < (int64_t(1) << 31) && np < (int64_t(1) << 31), MC_ERR_UNSUPPORTED, "node arrays too large");
+        for (int64_t i = 0; i < nc; i++) MC_REQUIRE(c_idx[i] >= 0 && c_idx[i] < num_masks, MC_ERR_INVALID, "contained id out of range");
+        for (int64_t i = 0; i < np; i++) MC_REQUIRE(pt_idx[i] >= 0 && pt_idx[i] < num_points, MC_ERR_INVALID, "point id out of range");
+        for (int i = 0; i < num_nodes; i++)
+            for (int64_t k = c_off[i] + 1; k < c_off[i + 1]; k++)
+                MC_REQUIRE(c_idx[k - 1] < c_idx[k], MC_ERR_INVALID, "contained ids must be ascending and unique per node");
+        hipStream_t s = ctx->stream;
+        ctx->have_graph = false;
+        ctx->have_cluster = false;
+        ctx->nodes_from_graph = false;
+        ctx->F = num_frames;
+        ctx->FW = (num_frames + 63) / 64;
+        ctx->P = num_points;
+        ctx->Mn = num_masks;
+        ctx->N0 = num_nodes;
+        ctx->nnzC0 = nc;
+        ctx->n0_pts_total = np;
+        const int n = num_nodes, FW = ctx->FW;
+        ctx->d_n0_off.reserve((n + 1) * sizeof(int));
+        ctx->d_n0_len.reserve((n + 1) * sizeof(int));
+        ctx->d_n0_ptoff.reserve((n + 1) * sizeof(int));
+        ctx->d_n0_ptlen.reserve((n + 1) * sizeof(int));
+        ctx->d_n0_vf.reserve((static_cast<size_t>(n) * FW + 1) * 8);
+        ctx->d_user_cidx.reserve((nc + 1) * sizeof(int));
+        ctx->d_user_pts.reserve((np + 1) * sizeof(int));
+        DevBuf t1, t2;
+        t1.reserve((n + 1) * 8);
+        t2.reserve((n + 1) * 8);
+        if (n) {
+            MC_HIP(hipMemcpyAsync(t1.ptr, c_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(t2.ptr, pt_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+            if (FW) MC_HIP(hipMemcpyAsync(ctx->d_n0_vf.ptr, vf_bits, static_cast<size_t>(n) * FW * 8, hipMemcpyHostToDevice, s));
+            if (nc) MC_HIP(hipMemcpyAsync(ctx->d_user_cidx.ptr, c_idx, nc * sizeof(int), hipMemcpyHostToDevice, s));
+            if (np) MC_HIP(hipMemcpyAsync(ctx->d_user_pts.ptr, pt_idx, np * sizeof(int), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_nodes_from_csr, grid_for(n), dim3(256), 0, s, n, t1.as<int64_t>(), t2.as<int64_t>(),
+                               ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
+                               ctx->d_n0_ptlen.as<int>());
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        t1.release();
+        t2.release();
+        ctx->n0_pool = ctx->d_user_cidx.as<int>();
+        ctx->n0_pts = ctx->d_user_pts.as<int>();
+        ctx->have_nodes = true;
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// S6
+// ---------------------------------------------------------------------------------------------
+int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double connect_threshold)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_nodes, MC_ERR_STATE, "mc_cluster_run before mc_graph_build / mc_nodes_set");
+        hipStream_t s = ctx->stream;
+        int *stats = ctx->d_stats.as<int>();
+        if (ctx->nodes_from_graph) {
+            sync_stats(ctx);  // the one host round trip between S4 and S6
+            ctx->N0 = ctx->h_stats[ST_N0];
+            ctx->nnzC0 = ctx->h_stats[ST_NNZC];
+        }
+        int nthr;
+        if (thresholds) {
+            MC_REQUIRE(n >= 0 && n <= 4096, MC_ERR_INVALID, "bad threshold count");
+            nthr = n;
+            ctx->d_thr.reserve((n + 1) * sizeof(float));
+            if (n) MC_HIP(hipMemcpyAsync(ctx->d_thr.ptr, thresholds, n * sizeof(float), hipMemcpyHostToDevice, s));
+        } else {
+            MC_REQUIRE(ctx->nodes_from_graph, MC_ERR_STATE, "device thresholds need mc_graph_build");
+            if (ctx->h_stats[ST_THR_STATUS] != MC_OK)
+                throw McError{ctx->h_stats[ST_THR_STATUS], "no positive observer count (np.percentile of an empty array)"};
+            nthr = ctx->h_stats[ST_NTHR];
+        }
+        const int N0 = ctx->N0, F = ctx->F, FW = ctx->FW, Mn = ctx->Mn;
+        MC_REQUIRE(!(N0 == 0 && nthr > 0), MC_ERR_NO_NODES, "no nodes to cluster (torch.stack of an empty list)");
+        const bool dense = !(connect_threshold > 0.0);  // ct <= 0: every pair with O >= thr connects
+        const bool ct_nan = std::isnan(connect_threshold);
+        std::vector<int> smin = build_smin(F, ct_nan ? std::nan("") : connect_threshold, std::max(Mn, 1));
+        const size_t n0 = static_cast<size_t>(std::max(N0, 1));
+        const size_t cap = static_cast<size_t>(std::max<int64_t>(ctx->nnzC0, 1));
+        ctx->d_smin.reserve((F + 1) * sizeof(int));
+        MC_HIP(hipMemcpyAsync(ctx->d_smin.ptr, smin.data(), (F + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+        ctx->d_parent.reserve(n0 * 4);
+        ctx->d_root.reserve(n0 * 4);
+        ctx->d_isroot.reserve(n0 * 4);
+        ctx->d_rank.reserve((n0 + 1) * 4);
+        ctx->d_label.reserve(n0 * 4);
+        ctx->d_levels.reserve(std::max<size_t>(1, static_cast<size_t>(nthr)) * n0 * 4);
+        ctx->d_memcnt.reserve(n0 * 4);
+        ctx->d_memoff.reserve((n0 + 1) * 4);
+        ctx->d_ublen.reserve(n0 * 4);
+        ctx->d_newoff.reserve((n0 + 1) * 4);
+        ctx->d_members.reserve(n0 * 4);
+        ctx->d_colcnt.reserve((Mn + 1) * 4);
+        ctx->d_coloff.reserve((Mn + 2) * 4);
+        ctx->d_colnodes.reserve(cap * 4);
+        ctx->d_ovf_list.reserve(n0 * 4);
+        ctx->d_ovf_n.reserve(4);
+        constexpr int kOvfBlocks = 64;
+        if (ctx->scratch_n0 < N0) {
+            ctx->d_scratch.reserve(static_cast<size_t>(kOvfBlocks) * n0 * 4);
+            ctx->d_touched.reserve(static_cast<size_t>(kOvfBlocks) * n0 * 4);
+            MC_HIP(hipMemsetAsync(ctx->d_scratch.ptr, 0, static_cast<size_t>(kOvfBlocks) * n0 * 4, s));
+            ctx->scratch_n0 = N0;
+        }
+        ctx->d_edges.reserve(std::max(nthr, 1) * 8);
+        ctx->d_Nlev.reserve((nthr + 2) * 4);
+        ctx->d_final_label.reserve(n0 * 4);
+        ctx->d_poolA.reserve(cap * 4);
+        ctx->d_poolB.reserve(cap * 4);
+        ctx->d_offA.reserve(n0 * 4);
+        ctx->d_offB.reserve(n0 * 4);
+        ctx->d_lenA.reserve(n0 * 4);
+        ctx->d_lenB.reserve(n0 * 4);
+        ctx->d_vfA.reserve(n0 * FW * 8 + 8);
+        ctx->d_vfB.reserve(n0 * FW * 8 + 8);
+        ctx->d_pmin.reserve(n0 * 4);
+        ctx->d_pmax.reserve(n0 * 4);
+        ctx->d_nwords.reserve(n0 * 4);
+        ctx->d_woff.reserve((n0 + 1) * 4);
+        ctx->d_ptcnt.reserve(n0 * 4);
+        ctx->d_ptoff_out.reserve((n0 + 1) * 4);
+        ctx->d_pts_out.reserve((ctx->n0_pts_total + 1) * 4);
+
+        int *Nlev = ctx->d_Nlev.as<int>();
+        if (ctx->nodes_from_graph) {
+            hipLaunchKernelGGL(mc::k_copy_i32, dim3(1), dim3(1), 0, s, stats + ST_N0, Nlev);
+        } else {
+            MC_HIP(hipMemcpyAsync(Nlev, &ctx->N0, sizeof(int), hipMemcpyHostToDevice, s));
+        }
+        MC_HIP(hipMemsetAsync(ctx->d_edges.ptr, 0, std::max(nthr, 1) * 8, s));
+        hipLaunchKernelGGL(mc::k6_iota, grid_for(N0), dim3(256), 0, s, N0, ctx->d_final_label.as<int>());
+
+        const int *cur_off = ctx->d_n0_off.as<int>(), *cur_len = ctx->d_n0_len.as<int>(), *cur_pool = ctx->n0_pool;
+        const unsigned long long *cur_vf = ctx->d_n0_vf.as<unsigned long long>();
+        const dim3 gN = grid_for(N0), gW = grid_for(N0, mc::kPairWaves, 8192), gK = grid_for(N0, 1, 4096);
+        for (int t = 0; t < nthr; t++) {
+            const int *dN = Nlev + t;
+            int *dNn = Nlev + t + 1;
+            const bool toA = (t % 2) == 0;
+            int *nx_off = toA ? ctx->d_offA.as<int>() : ctx->d_offB.as<int>();
+            int *nx_len = toA ? ctx->d_lenA.as<int>() : ctx->d_lenB.as<int>();
+            int *nx_pool = toA ? ctx->d_poolA.as<int>() : ctx->d_poolB.as<int>();
+            unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
+            {
+                TimedScope ts(ctx->timer, s, "s6_columns");
+                if (!dense) MC_HIP(hipMemsetAsync(ctx->d_colcnt.ptr, 0, (Mn + 1) * 4, s));
+                hipLaunchKernelGGL(mc::k6_prep, gN, dim3(256), 0, s, dN, cur_off, dense ? ctx->d_n0_len.as<int>() : cur_len,
+                                   cur_pool, ctx->d_parent.as<int>(), ctx->d_colcnt.as<int>());
+                if (!dense) {
+                    mc::scan_device_n(s, ctx->d_colcnt.as<int>(), ctx->d_coloff.as<int>(), nullptr, Mn, nullptr);
+                    hipLaunchKernelGGL(mc::k6_colscatter, gN, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
+                                       ctx->d_coloff.as<int>(), ctx->d_colcnt.as<int>(), ctx->d_colnodes.as<int>());
+                }
+            }
+            if (!dense) {
+                TimedScope ts(ctx->timer, s, "s6_pairs");
+                MC_HIP(hipMemsetAsync(ctx->d_ovf_n.ptr, 0, 4, s));
+                hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
+                                   ctx->d_coloff.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
+                                   ctx->d_thr.as<float>(), t, ctx->d_smin.as<int>(), ctx->d_parent.as<int>(),
+                                   ctx->d_edges.as<unsigned long long>(), ctx->d_ovf_list.as<int>(),
+                                   ctx->d_ovf_n.as<int>());
+                hipLaunchKernelGGL(mc::k6_pairs_overflow, dim3(kOvfBlocks), dim3(256), 0, s, ctx->d_ovf_list.as<int>(),
+                                   ctx->d_ovf_n.as<int>(), cur_off, cur_len, cur_pool, ctx->d_coloff.as<int>(),
+                                   ctx->d_colnodes.as<int>(), cur_vf, FW, ctx->d_thr.as<float>(), t,
+                                   ctx->d_smin.as<int>(), ctx->d_parent.as<int>(),
+                                   ctx->d_edges.as<unsigned long long>(), ctx->d_scratch.as<int>(),
+                                   ctx->d_touched.as<int>(), N0);
+            } else {
+                TimedScope ts(ctx->timer, s, "s6_pairs");
+                hipLaunchKernelGGL(mc::k6_pairs_dense, dim3(4096), dim3(256), 0, s, dN, cur_vf, FW,
+                                   ctx->d_thr.as<float>(), t, ctx->d_parent.as<int>(),
+                                   ctx->d_edges.as<unsigned long long>());
+            }
+            {
+                TimedScope ts(ctx->timer, s, "s6_components");
+                hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
+                                   ctx->d_root.as<int>(), ctx->d_isroot.as<int>());
+                mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
+                MC_HIP(hipMemsetAsync(ctx->d_memcnt.ptr, 0, n0 * 4, s));
+                MC_HIP(hipMemsetAsync(ctx->d_ublen.ptr, 0, n0 * 4, s));
+                hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(), ctx->d_rank.as<int>(),
+                                   cur_len, ctx->d_label.as<int>(), ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0,
+                                   ctx->d_memcnt.as<int>(), ctx->d_ublen.as<int>());
+                mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr);
+                mc::scan_device_n(s, ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dNn, 0, nullptr);
+                hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, ctx->d_label.as<int>(),
+                                   ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>());
+            }
+            {
+                TimedScope ts(ctx->timer, s, "s6_merge");
+                hipLaunchKernelGGL(mc::k6_merge, gK, dim3(256), 0, s, dNn, ctx->d_memoff.as<int>(),
+                                   ctx->d_members.as<int>(), cur_off, cur_len, cur_pool, cur_vf, FW,
+                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_vf);
+                hipLaunchKernelGGL(mc::k6_maplevel, gN, dim3(256), 0, s, N0, ctx->d_label.as<int>(),
+                                   ctx->d_final_label.as<int>());
+            }
+            cur_off = nx_off;
+            cur_len = nx_len;
+            cur_pool = nx_pool;
+            cur_vf = nx_vf;
+        }
+        ctx->fin_off = cur_off;
+        ctx->fin_len = cur_len;
+        ctx->fin_pool = cur_pool;
+        ctx->fin_vf = cur_vf;
+        ctx->n_iter = nthr;
+        // ---- final point sets (node.py:35), per-object range bitmaps ----
+        const int *dK = Nlev + nthr;
+        {
+            TimedScope ts(ctx->timer, s, "s7_points");
+            hipLaunchKernelGGL(mc::k_fill_i32, gN, dim3(256), 0, s, ctx->d_pmin.as<int>(), N0, INT_MAX);
+            hipLaunchKernelGGL(mc::k_fill_i32, gN, dim3(256), 0, s, ctx->d_pmax.as<int>(), N0, -1);
+            hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts, ctx->d_pmin.as<int>(),
+                               ctx->d_pmax.as<int>());
+            hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                               ctx->d_nwords.as<int>());
+            mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
+            hipLaunchKernelGGL(mc::k_copy_i32, dim3(1), dim3(1), 0, s, dK, stats + ST_K);
+        }
+        sync_stats(ctx);  // bitmap capacity
+        ctx->K = ctx->h_stats[ST_K];
+        const size_t words = static_cast<size_t>(std::max(ctx->h_stats[ST_WORDS], 1));
+        ctx->d_bm.reserve(words * 8);
+        {
+            TimedScope ts(ctx->timer, s, "s7_points");
+            MC_HIP(hipMemsetAsync(ctx->d_bm.ptr, 0, words * 8, s));
+            hipLaunchKernelGGL(mc::k7_setbits, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts, ctx->d_pmin.as<int>(),
+                               ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>());
+            hipLaunchKernelGGL(mc::k7_count, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
+                               ctx->d_bm.as<unsigned long long>(), ctx->d_ptcnt.as<int>());
+            mc::scan_device_n(s, ctx->d_ptcnt.as<int>(), ctx->d_ptoff_out.as<int>(), dK, 0, stats + ST_NPTS);
+            hipLaunchKernelGGL(mc::k7_extract, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
+                               ctx->d_bm.as<unsigned long long>(), ctx->d_pmin.as<int>(), ctx->d_ptoff_out.as<int>(),
+                               ctx->d_pts_out.as<int>());
+        }
+        MC_HIP(hipGetLastError());
+        MC_HIP(hipMemcpyAsync(ctx->h_stats, ctx->d_stats.ptr, ST_COUNT * sizeof(int), hipMemcpyDeviceToHost, s));
+        ctx->have_cluster = true;
+    });
+}
+
+int mc_cluster_get_info(mc_ctx *ctx, mc_cluster_info *info)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster && info, MC_ERR_STATE, "no clustering result");
+        sync_stats(ctx);
+        info->num_iterations = ctx->n_iter;
+        info->num_objects = ctx->h_stats[ST_K];
+        info->num_nodes0 = ctx->N0;
+        info->reserved = 0;
+        info->num_object_points = ctx->h_stats[ST_NPTS];
+        std::vector<int> len(std::max(ctx->K, 1));
+        if (ctx->K) MC_HIP(hipMemcpyAsync(len.data(), ctx->fin_len, ctx->K * 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        int64_t tot = 0;
+        for (int k = 0; k < ctx->K; k++) tot += len[k];
+        info->num_object_contained = tot;
+        info->num_object_masks = ctx->N0;
+    });
+}
+
+int mc_cluster_get_level_sizes(mc_ctx *ctx, int32_t *sizes)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        MC_HIP(hipMemcpyAsync(sizes, ctx->d_Nlev.ptr, (ctx->n_iter + 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_cluster_get_partition(mc_ctx *ctx, int32_t iteration, int32_t *labels)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        MC_REQUIRE(iteration >= 0 && iteration < ctx->n_iter, MC_ERR_INVALID, "iteration out of range");
+        int nt = 0;
+        MC_HIP(hipMemcpyAsync(&nt, ctx->d_Nlev.as<int>() + iteration, 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        const size_t n0 = static_cast<size_t>(std::max(ctx->N0, 1));
+        if (nt)
+            MC_HIP(hipMemcpyAsync(labels, ctx->d_levels.as<int>() + static_cast<size_t>(iteration) * n0, nt * 4,
+                                  hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_cluster_get_edge_counts(mc_ctx *ctx, int64_t *edges)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        if (ctx->n_iter)
+            MC_HIP(hipMemcpyAsync(edges, ctx->d_edges.ptr, ctx->n_iter * 8, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_cluster_get_final_labels(mc_ctx *ctx, int32_t *labels)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        if (ctx->N0) MC_HIP(hipMemcpyAsync(labels, ctx->d_final_label.ptr, ctx->N0 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_cluster_get_objects(mc_ctx *ctx, uint64_t *vf_bits, int64_t *c_off, int32_t *c_idx, int64_t *pt_off,
+                           int32_t *pt_idx, int64_t *mask_off, int32_t *mask_idx)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        sync_stats(ctx);
+        const int K = ctx->K, FW = ctx->FW;
+        hipStream_t s = ctx->stream;
+        std::vector<int> off(std::max(K, 1)), len(std::max(K, 1)), poff(K + 1);
+        if (K) {
+            MC_HIP(hipMemcpyAsync(off.data(), ctx->fin_off, K * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(len.data(), ctx->fin_len, K * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(poff.data(), ctx->d_ptoff_out.ptr, (K + 1) * 4, hipMemcpyDeviceToHost, s));
+            if (vf_bits && FW) MC_HIP(hipMemcpyAsync(vf_bits, ctx->fin_vf, static_cast<size_t>(K) * FW * 8, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        if (c_off) {
+            c_off[0] = 0;
+            for (int k = 0; k < K; k++) {
+                c_off[k + 1] = c_off[k] + len[k];
+                if (c_idx && len[k])
+                    MC_HIP(hipMemcpyAsync(c_idx + c_off[k], ctx->fin_pool + off[k], len[k] * 4, hipMemcpyDeviceToHost, s));
+            }
+        }
+        if (pt_off) {
+            for (int k = 0; k <= K; k++) pt_off[k] = K ? poff[k] : 0;
+            const int np = K ? poff[K] : 0;
+            if (pt_idx && np) MC_HIP(hipMemcpyAsync(pt_idx, ctx->d_pts_out.ptr, static_cast<size_t>(np) * 4, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        if (mask_off) {
+            // members of each object as ascending level-0 node ids (stable counting sort)
+            std::vector<int> fl(std::max(ctx->N0, 1));
+            if (ctx->N0) MC_HIP(hipMemcpy(fl.data(), ctx->d_final_label.ptr, ctx->N0 * 4, hipMemcpyDeviceToHost));
+            std::vector<int64_t> cnt(K + 1, 0);
+            for (int i = 0; i < ctx->N0; i++) cnt[fl[i] + 1]++;
+            for (int k = 0; k < K; k++) cnt[k + 1] += cnt[k];
+            for (int k = 0; k <= K; k++) mask_off[k] = cnt[k];
+            if (mask_idx)
+                for (int i = 0; i < ctx->N0; i++) mask_idx[cnt[fl[i]]++] = i;
+        }
+    });
+}
+
+}  // extern "C"
