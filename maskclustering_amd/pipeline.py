@@ -73,10 +73,11 @@ class GraphRun:
         else:
             thr, isint = np.zeros(0, np.float32), np.zeros(0, bool)
         out["thr_value"], out["thr_is_int"] = thr, isint
-        out.update(self.canonical_cluster(F))
+        out.update(self.canonical_cluster(F, node0=out["node0_g"]))
         return out
 
-    def canonical_cluster(self, F) -> dict:
+    def canonical_cluster(self, F, node0=None) -> dict:
+        """S6 results; ``node0`` maps level-0 node ids to global mask ids."""
         c = self.ctx
         ci = c.cluster_info()
         T = ci.num_iterations
@@ -88,7 +89,6 @@ class GraphRun:
         out["edge_counts"] = c.edge_counts(T)
         obj = c.objects(ci, F)
         K = ci.num_objects
-        node0 = out.get("node0_g")
         out["obj_mask_off"] = obj["mask_off"]
         out["obj_mask_idx"] = obj["mask_idx"]  # level-0 node ids; callers map to masks
         out["obj_pt_off"], out["obj_pt_idx"] = obj["pt_off"], obj["pt_idx"]
