@@ -126,8 +126,10 @@ def main():
     dominant = max((g for g in calib if g in work), key=lambda g: calib[g])
     log("calibration (ms):", json.dumps({k: round(v, 4) for k, v in calib.items()}), "dominant:", dominant)
 
-    # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant group
+    # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant
+    # group only (one event pair per step)
     run.ctx.reset_kernel_times()
+    run.ctx.set_timing_filter(dominant)
     run.ctx.set_timing(True)
     if world > 1:
         dist.barrier()

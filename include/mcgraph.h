@@ -84,6 +84,7 @@ int mc_ctx_synchronize(mc_ctx *ctx);
 const char *mc_ctx_last_error(mc_ctx *ctx);
 /* live per-kernel timing with HIP events on the context stream (bench/profiling) */
 int mc_ctx_set_timing(mc_ctx *ctx, int enable);
+int mc_ctx_set_timing_filter(mc_ctx *ctx, const char *kernel);  /* NULL/"" = every kernel group */
 int mc_ctx_get_kernel_time(mc_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int mc_ctx_reset_kernel_times(mc_ctx *ctx);
 

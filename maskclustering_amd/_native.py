@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmcgraph.so")
+LIB_PATH = os.environ.get("MCGRAPH_LIB") or os.path.join(HERE, "libmcgraph.so")  # override: profiling variants
 
 MC_OK = 0
 MC_ERR_INVALID = 1
@@ -24,7 +24,7 @@ MC_ERR_NO_NODES = 6
 
 EXPORTED = [
     "mc_ctx_create", "mc_ctx_destroy", "mc_ctx_set_stream", "mc_ctx_get_stream", "mc_ctx_synchronize",
-    "mc_ctx_last_error", "mc_ctx_set_timing", "mc_ctx_get_kernel_time", "mc_ctx_reset_kernel_times",
+    "mc_ctx_last_error", "mc_ctx_set_timing", "mc_ctx_set_timing_filter", "mc_ctx_get_kernel_time", "mc_ctx_reset_kernel_times",
     "mc_scene_set_masks", "mc_graph_build", "mc_graph_get_info", "mc_graph_get_global_masks",
     "mc_graph_get_boundary", "mc_graph_get_point_in_mask", "mc_graph_get_point_frame_bits",
     "mc_graph_get_visible_frame_bits", "mc_graph_get_contained", "mc_graph_get_undersegment",
@@ -82,6 +82,7 @@ def load():
         "mc_ctx_synchronize": (ctypes.c_int, [vp]),
         "mc_ctx_last_error": (ctypes.c_char_p, [vp]),
         "mc_ctx_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+        "mc_ctx_set_timing_filter": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "mc_ctx_get_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
         "mc_ctx_reset_kernel_times": (ctypes.c_int, [vp]),
         "mc_scene_set_masks": (ctypes.c_int, [vp, i64, i32, i32, vp, vp, vp, vp, ctypes.c_int]),
@@ -157,6 +158,9 @@ class Context:
 
     def set_timing(self, on: bool):
         self._check(self.L.mc_ctx_set_timing(self.h, 1 if on else 0))
+
+    def set_timing_filter(self, name):
+        self._check(self.L.mc_ctx_set_timing_filter(self.h, name.encode() if name else None))
 
     def kernel_time(self, name: str):
         ms, n = ctypes.c_double(), ctypes.c_int64()

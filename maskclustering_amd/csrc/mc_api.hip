@@ -27,7 +27,8 @@ enum Stat : int {
     ST_K = 5,         // final objects
     ST_WORDS = 6,     // point-bitmap words
     ST_NPTS = 7,      // object points (sum)
-    ST_COUNT = 8,
+    ST_OBJOVF = 8,    // a point in more objects than the per-point fast path holds
+    ST_COUNT = 9,
 };
 
 }  // namespace
@@ -49,7 +50,7 @@ struct mc_ctx {
     std::vector<int32_t> h_col, h_label, h_in_index, h_off;
     DevBuf d_mask_off, d_mask_pts, d_mask_col, d_mask_label, d_frame_start, d_valid;
     // ---- S2 ----
-    DevBuf d_deg, d_pt_off, d_cursor, d_pt_list, d_boundary, d_pfm, d_scan_tmp;
+    DevBuf d_deg, d_pt_off, d_pt_list, d_boundary, d_pfm, d_scan_tmp;
     // ---- S3/S5 ----
     DevBuf d_ctmp, d_crow_len, d_useg, d_keep_cnt, d_node_flag, d_node_pos, d_c_off, d_c_idx, d_vf;
     // ---- S4 ----
@@ -59,14 +60,16 @@ struct mc_ctx {
     int Mn = 0;        // mask-id space of C rows
     int64_t n0_pts_total = 0;
     DevBuf d_node0_g, d_n0_off, d_n0_len, d_n0_ptoff, d_n0_ptlen, d_n0_vf, d_user_cidx, d_user_pts;
+    DevBuf d_owner0, d_node_of_mask, d_obj_of_mask, d_s3_small, d_s3_big, d_collen;
+    int n_s3_small = 0, n_s3_big = 0;
     const int *n0_pool = nullptr;
     const int *n0_pts = nullptr;
     int64_t nnzC0 = 0;
     // ---- S6 ----
     DevBuf d_parent, d_root, d_isroot, d_rank, d_label, d_levels, d_memcnt, d_memoff, d_ublen, d_newoff;
     DevBuf d_members, d_colcnt, d_coloff, d_colnodes, d_ovf_list, d_ovf_n, d_scratch, d_touched, d_edges;
-    DevBuf d_Nlev, d_smin, d_final_label;
-    DevBuf d_poolA, d_poolB, d_offA, d_offB, d_lenA, d_lenB, d_vfA, d_vfB;
+    DevBuf d_Nlev, d_final_label;
+    DevBuf d_poolA, d_poolB, d_offA, d_offB, d_lenA, d_lenB, d_vfA, d_vfB, d_ownA, d_ownB, d_cap;
     DevBuf d_pmin, d_pmax, d_nwords, d_woff, d_bm, d_ptcnt, d_ptoff_out, d_pts_out;
     int scratch_n0 = -1;
     int n_iter = 0;
@@ -115,27 +118,21 @@ void sync_stats(mc_ctx *ctx)
     ctx->timer.collect();
 }
 
-// smin[o] = smallest S with fl32(S / fl32(o + 1e-7f)) >= fl32(ct)  (iterative_clustering.py:23,28);
-// INT_MAX when no S <= max_s qualifies.  Float32 arithmetic like torch on the device.
-std::vector<int> build_smin(int F, double ct, int max_s)
+
+// S4 histogram launch: persistent blocks, R lane-indexed LDS replicas (odd stride)
+void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsigned long long *hist)
 {
-    std::vector<int> smin(F + 1, std::numeric_limits<int>::max());
-    const float ctf = static_cast<float>(ct);
-    if (std::isnan(ctf)) return smin;
-    for (int o = 0; o <= F; o++) {
-        volatile float den = static_cast<float>(o) + 1e-7f;
-        double est = std::floor(static_cast<double>(ct) * (static_cast<double>(o) + 1e-7)) - 2.0;
-        int64_t s = est < 0 ? 0 : static_cast<int64_t>(est);
-        if (s > static_cast<int64_t>(max_s) + 1) continue;
-        for (; s <= static_cast<int64_t>(max_s) + 1; s++) {
-            volatile float rate = static_cast<float>(s) / den;
-            if (rate >= ctf) {
-                smin[o] = static_cast<int>(s);
-                break;
-            }
-        }
-    }
-    return smin;
+    if (!M || !F) return;
+    const int FW = (F + 63) / 64;
+    const int nblk = ceil_div(M, mc::kHistTile);
+    const long long ntiles = static_cast<long long>(nblk) * (nblk + 1) / 2;
+    const int HS = (F + 1) | 1;
+    int R = 32;
+    while (R > 1 && static_cast<size_t>(R) * HS * 4 > 40 * 1024) R >>= 1;
+    const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + static_cast<size_t>(R) * HS * 4;
+    const long long grid = std::min<long long>(ntiles, 1024);
+    hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(grid)), dim3(256), lds, s, vf, M, FW, F, nblk, ntiles, R,
+                       HS, hist);
 }
 
 }  // namespace
@@ -169,7 +166,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     DevBuf *bufs[] = {&ctx->d_mask_off, &ctx->d_mask_pts, &ctx->d_mask_col, &ctx->d_mask_label, &ctx->d_frame_start,
-                      &ctx->d_valid, &ctx->d_deg, &ctx->d_pt_off, &ctx->d_cursor, &ctx->d_pt_list, &ctx->d_boundary,
+                      &ctx->d_valid, &ctx->d_deg, &ctx->d_pt_off, &ctx->d_pt_list, &ctx->d_boundary,
                       &ctx->d_pfm, &ctx->d_scan_tmp, &ctx->d_ctmp, &ctx->d_crow_len, &ctx->d_useg, &ctx->d_keep_cnt,
                       &ctx->d_node_flag, &ctx->d_node_pos, &ctx->d_c_off, &ctx->d_c_idx, &ctx->d_vf, &ctx->d_hist,
                       &ctx->d_thr, &ctx->d_isint, &ctx->d_stats, &ctx->d_node0_g, &ctx->d_n0_off, &ctx->d_n0_len,
@@ -177,10 +174,12 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_parent, &ctx->d_root, &ctx->d_isroot, &ctx->d_rank, &ctx->d_label, &ctx->d_levels,
                       &ctx->d_memcnt, &ctx->d_memoff, &ctx->d_ublen, &ctx->d_newoff, &ctx->d_members, &ctx->d_colcnt,
                       &ctx->d_coloff, &ctx->d_colnodes, &ctx->d_ovf_list, &ctx->d_ovf_n, &ctx->d_scratch,
-                      &ctx->d_touched, &ctx->d_edges, &ctx->d_Nlev, &ctx->d_smin, &ctx->d_final_label,
+                      &ctx->d_touched, &ctx->d_edges, &ctx->d_Nlev, &ctx->d_final_label,
                       &ctx->d_poolA, &ctx->d_poolB, &ctx->d_offA, &ctx->d_offB, &ctx->d_lenA, &ctx->d_lenB,
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
-                      &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out};
+                      &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out, &ctx->d_owner0,
+                      &ctx->d_node_of_mask, &ctx->d_ownA, &ctx->d_ownB, &ctx->d_cap, &ctx->d_obj_of_mask,
+                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -220,6 +219,15 @@ int mc_ctx_set_timing(mc_ctx *ctx, int enable)
         MC_HIP(hipStreamSynchronize(ctx->stream));
         ctx->timer.collect();
         ctx->timer.enabled = enable != 0;
+    });
+}
+
+int mc_ctx_set_timing_filter(mc_ctx *ctx, const char *kernel)
+{
+    return guarded(ctx, [&] {
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->timer.collect();
+        ctx->timer.filter = kernel ? kernel : "";
     });
 }
 
@@ -281,7 +289,7 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
             MC_REQUIRE(mask_off[g + 1] >= mask_off[g], MC_ERR_INVALID, "mask_off must be non-decreasing");
             frame_pts[c] += mask_off[g + 1] - mask_off[g];
             frame_masks[c]++;
-            MC_REQUIRE(frame_masks[c] < mc::kMaxMasksPerFrame, MC_ERR_UNSUPPORTED, "more than 4095 masks in a frame");
+            MC_REQUIRE(frame_masks[c] < 2048, MC_ERR_UNSUPPORTED, "more than 2047 masks in a frame");
         }
         {
             std::vector<int> seen(65536, -1);
@@ -342,8 +350,8 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
 
         // S2/S3/S4 buffers (allocated once per scene; nothing is allocated while building)
         ctx->d_deg.reserve((P + 1) * sizeof(int));
+        MC_HIP(hipMemsetAsync(ctx->d_deg.ptr, 0, (P + 1) * sizeof(int), s));  // kept zero by the S2 scatter
         ctx->d_pt_off.reserve((P + 2) * sizeof(int));
-        ctx->d_cursor.reserve((P + 1) * sizeof(int));
         ctx->d_pt_list.reserve((nnz + 1) * sizeof(unsigned));
         ctx->d_boundary.reserve(P + 1);
         ctx->d_pfm.reserve((P * FW + 1) * sizeof(unsigned long long));
@@ -366,6 +374,29 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
         ctx->d_n0_ptoff.reserve((M + 1) * sizeof(int));
         ctx->d_n0_ptlen.reserve((M + 1) * sizeof(int));
         ctx->d_n0_vf.reserve((static_cast<size_t>(M) * FW + 1) * sizeof(unsigned long long));
+        ctx->d_owner0.reserve((static_cast<size_t>(M) * F + 1) * sizeof(int));
+        ctx->d_node_of_mask.reserve((M + 1) * sizeof(int));
+        ctx->d_obj_of_mask.reserve((M + 1) * sizeof(int));
+        // S3 work lists: wave-per-mask for the bulk, workgroup-per-mask for large masks
+        {
+            int max_per_frame = 0;
+            for (int c = 0; c < F; c++) max_per_frame = std::max(max_per_frame, frame_start[c + 1] - frame_start[c]);
+            const bool wave_ok = F <= 64 * mc::kS3wFrameWords64 && max_per_frame < mc::kS3wCounters;
+            std::vector<int> small, big;
+            for (int g = 0; g < M; g++) {
+                const int sz = ctx->h_off[g + 1] - ctx->h_off[g];
+                (wave_ok && sz <= mc::kS3SmallPts ? small : big).push_back(g);
+            }
+            ctx->n_s3_small = static_cast<int>(small.size());
+            ctx->n_s3_big = static_cast<int>(big.size());
+            ctx->d_s3_small.reserve((small.size() + 1) * sizeof(int));
+            ctx->d_s3_big.reserve((big.size() + 1) * sizeof(int));
+            if (!small.empty())
+                MC_HIP(hipMemcpyAsync(ctx->d_s3_small.ptr, small.data(), small.size() * sizeof(int), hipMemcpyHostToDevice, s));
+            if (!big.empty())
+                MC_HIP(hipMemcpyAsync(ctx->d_s3_big.ptr, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice, s));
+            MC_HIP(hipStreamSynchronize(s));
+        }
         ctx->have_scene = true;
     });
 }
@@ -382,20 +413,16 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         const int64_t P = ctx->P;
         const int F = ctx->F, FW = ctx->FW, M = ctx->M, nnz = ctx->nnz;
         int *stats = ctx->d_stats.as<int>();
-        MC_HIP(hipMemsetAsync(stats, 0, ST_COUNT * sizeof(int), s));
         ctx->have_cluster = false;
         {  // S2
             TimedScope ts(ctx->timer, s, "s2_point_lists");
-            MC_HIP(hipMemsetAsync(ctx->d_deg.ptr, 0, (P + 1) * sizeof(int), s));
-            if (nnz)
-                hipLaunchKernelGGL(mc::k_s2_degree, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(), nnz,
-                                   ctx->d_deg.as<int>());
+            hipLaunchKernelGGL(mc::k_s2_degree, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(), nnz,
+                               ctx->d_deg.as<int>(), stats, static_cast<int>(ST_COUNT));
             mc::scan_large(s, ctx->d_deg.as<int>(), ctx->d_pt_off.as<int>(), static_cast<int>(P), ctx->d_scan_tmp.as<int>());
-            MC_HIP(hipMemsetAsync(ctx->d_cursor.ptr, 0, (P + 1) * sizeof(int), s));
             if (M)
                 hipLaunchKernelGGL(mc::k_s2_scatter, dim3(M), dim3(256), 0, s, ctx->d_mask_off.as<int>(),
                                    ctx->d_mask_pts.as<int>(), ctx->d_mask_col.as<int>(), ctx->d_frame_start.as<int>(),
-                                   ctx->d_pt_off.as<int>(), ctx->d_cursor.as<int>(), ctx->d_pt_list.as<unsigned>());
+                                   ctx->d_pt_off.as<int>(), ctx->d_deg.as<int>(), ctx->d_pt_list.as<unsigned>());
             if (P)
                 hipLaunchKernelGGL(mc::k_s2_points, dim3(ceil_div(P, 256)), dim3(256), 0, s, ctx->d_pt_off.as<int>(),
                                    ctx->d_pt_list.as<unsigned>(), static_cast<int>(P), FW,
@@ -404,43 +431,52 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         }
         if (M) {  // S3
             TimedScope ts(ctx->timer, s, "s3_masks");
-            hipLaunchKernelGGL(mc::k_s3_masks, dim3(M), dim3(mc::kS3Threads), 0, s, ctx->d_mask_off.as<int>(),
-                               ctx->d_mask_pts.as<int>(), ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(),
-                               ctx->d_boundary.as<unsigned char>(), ctx->d_frame_start.as<int>(),
-                               ctx->d_mask_label.as<int>(), F, params->mask_visible_threshold,
-                               params->contained_threshold, params->undersegment_filter_threshold,
-                               ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
+            if (ctx->n_s3_big)
+                hipLaunchKernelGGL(mc::k_s3_masks<4>, grid_for(ctx->n_s3_big, 1, 8192), dim3(256), 0, s,
+                                   ctx->d_s3_big.as<int>(), ctx->n_s3_big, ctx->d_mask_off.as<int>(),
+                                   ctx->d_mask_pts.as<int>(), ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(),
+                                   ctx->d_boundary.as<unsigned char>(), ctx->d_pfm.as<unsigned long long>(), FW,
+                                   ctx->d_frame_start.as<int>(), ctx->d_mask_label.as<int>(), F,
+                                   params->mask_visible_threshold, params->contained_threshold,
+                                   params->undersegment_filter_threshold, ctx->d_ctmp.as<int>(),
+                                   ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
+            if (ctx->n_s3_small)
+                hipLaunchKernelGGL(mc::k_s3_masks<1>, grid_for(ctx->n_s3_small, 4, 16384), dim3(256), 0, s,
+                                   ctx->d_s3_small.as<int>(), ctx->n_s3_small, ctx->d_mask_off.as<int>(),
+                                   ctx->d_mask_pts.as<int>(), ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(),
+                                   ctx->d_boundary.as<unsigned char>(), ctx->d_pfm.as<unsigned long long>(), FW,
+                                   ctx->d_frame_start.as<int>(), ctx->d_mask_label.as<int>(), F,
+                                   params->mask_visible_threshold, params->contained_threshold,
+                                   params->undersegment_filter_threshold, ctx->d_ctmp.as<int>(),
+                                   ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
         }
         if (M) {  // S3 undo + S5
             TimedScope ts(ctx->timer, s, "s3_undo_s5");
-            hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
-                               ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
-                               ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>());
-            mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC);
+            hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(std::max(M, F + 1), 256)), dim3(256), 0, s,
+                               ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
+                               ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>(),
+                               ctx->d_hist.as<unsigned long long>());
+            mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC,
+                              ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), stats + ST_N0);
             hipLaunchKernelGGL(mc::k_s3_undo_write, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
                                ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), ctx->d_mask_col.as<int>(), M,
                                F, FW, ctx->d_c_off.as<int>(), ctx->d_c_idx.as<int>(),
                                ctx->d_vf.as<unsigned long long>());
-            mc::scan_device_n(s, ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), nullptr, M, stats + ST_N0);
             hipLaunchKernelGGL(mc::k_s5_nodes, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_node_pos.as<int>(),
                                ctx->d_useg.as<unsigned char>(), ctx->d_c_off.as<int>(), ctx->d_mask_off.as<int>(),
                                ctx->d_vf.as<unsigned long long>(), M, FW, ctx->d_node0_g.as<int>(),
                                ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
-                               ctx->d_n0_ptlen.as<int>(), ctx->d_n0_vf.as<unsigned long long>());
+                               ctx->d_n0_ptlen.as<int>(), ctx->d_n0_vf.as<unsigned long long>(),
+                               ctx->d_owner0.as<int>(), ctx->d_node_of_mask.as<int>());
+        } else {
+            MC_HIP(hipMemsetAsync(ctx->d_hist.ptr, 0, (F + 1) * sizeof(unsigned long long), s));
         }
         {  // S4
             TimedScope ts(ctx->timer, s, "s4_observer_hist");
-            MC_HIP(hipMemsetAsync(ctx->d_hist.ptr, 0, (F + 1) * sizeof(unsigned long long), s));
-            if (M && F) {
-                const int nblk = ceil_div(M, mc::kHistTile);
-                const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + (F + 1) * sizeof(unsigned);
-                const int64_t nb = static_cast<int64_t>(nblk) * (nblk + 1) / 2;
-                hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(nb)), dim3(256), lds, s,
-                                   ctx->d_vf.as<unsigned long long>(), M, FW, F, nblk,
-                                   ctx->d_hist.as<unsigned long long>());
-            }
-            hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(64), 0, s, ctx->d_hist.as<unsigned long long>(), F,
-                               ctx->d_thr.as<float>(), ctx->d_isint.as<int>(), stats + ST_NTHR, stats + ST_THR_STATUS);
+            launch_hist(s, ctx->d_vf.as<unsigned long long>(), M, F, ctx->d_hist.as<unsigned long long>());
+            hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
+                               ctx->d_hist.as<unsigned long long>(), F, ctx->d_thr.as<float>(), ctx->d_isint.as<int>(),
+                               stats + ST_NTHR, stats + ST_THR_STATUS);
         }
         MC_HIP(hipGetLastError());
         // level-0 nodes live in the graph's buffers
@@ -604,14 +640,9 @@ int mc_observer_thresholds(mc_ctx *ctx, int32_t num_rows, int32_t num_frames, co
         st.reserve(2 * 4);
         if (M && FW) MC_HIP(hipMemcpyAsync(vf.ptr, vf_bits, static_cast<size_t>(M) * FW * 8, hipMemcpyHostToDevice, s));
         MC_HIP(hipMemsetAsync(hist.ptr, 0, (F + 1) * 8, s));
-        if (M && F) {
-            const int nblk = ceil_div(M, mc::kHistTile);
-            const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + (F + 1) * sizeof(unsigned);
-            const int64_t nb = static_cast<int64_t>(nblk) * (nblk + 1) / 2;
-            hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(nb)), dim3(256), lds, s,
-                               vf.as<unsigned long long>(), M, FW, F, nblk, hist.as<unsigned long long>());
-        }
-        hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(64), 0, s, hist.as<unsigned long long>(), F,
+        launch_hist(s, vf.as<unsigned long long>(), M, F, hist.as<unsigned long long>());
+        hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
+                           hist.as<unsigned long long>(), F,
                            dthr.as<float>(), disint.as<int>(), st.as<int>(), st.as<int>() + 1);
         int hs[2];
         MC_HIP(hipMemcpyAsync(hs, st.ptr, 8, hipMemcpyDeviceToHost, s));
@@ -627,13 +658,14 @@ int mc_observer_thresholds(mc_ctx *ctx, int32_t num_rows, int32_t num_frames, co
 // arbitrary level-0 nodes
 // ---------------------------------------------------------------------------------------------
 __global__ void k_nodes_from_csr(int n, const int64_t *c_off, const int64_t *pt_off, int *n_off, int *n_len, int *n_ptoff,
-                                 int *n_ptlen)
+                                 int *n_ptlen, int *owner)
 {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         n_off[i] = static_cast<int>(c_off[i]);
         n_len[i] = static_cast<int>(c_off[i + 1] - c_off[i]);
         n_ptoff[i] = static_cast<int>(pt_off[i]);
         n_ptlen[i] = static_cast<int>(pt_off[i + 1] - pt_off[i]);
+        for (int64_t e = c_off[i]; e < c_off[i + 1]; e++) owner[e] = i;
     }
 }
 
@@ -672,6 +704,7 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
         ctx->d_n0_vf.reserve((static_cast<size_t>(n) * FW + 1) * 8);
         ctx->d_user_cidx.reserve((nc + 1) * sizeof(int));
         ctx->d_user_pts.reserve((np + 1) * sizeof(int));
+        ctx->d_owner0.reserve((nc + 1) * sizeof(int));
         DevBuf t1, t2;
         t1.reserve((n + 1) * 8);
         t2.reserve((n + 1) * 8);
@@ -683,7 +716,7 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
             if (np) MC_HIP(hipMemcpyAsync(ctx->d_user_pts.ptr, pt_idx, np * sizeof(int), hipMemcpyHostToDevice, s));
             hipLaunchKernelGGL(k_nodes_from_csr, grid_for(n), dim3(256), 0, s, n, t1.as<int64_t>(), t2.as<int64_t>(),
                                ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
-                               ctx->d_n0_ptlen.as<int>());
+                               ctx->d_n0_ptlen.as<int>(), ctx->d_owner0.as<int>());
         }
         MC_HIP(hipStreamSynchronize(s));
         t1.release();
@@ -704,7 +737,7 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         hipStream_t s = ctx->stream;
         int *stats = ctx->d_stats.as<int>();
         if (ctx->nodes_from_graph) {
-            sync_stats(ctx);  // the one host round trip between S4 and S6
+            sync_stats(ctx);  // the one host round trip between S4 and S6 (sizes for the S6 buffers)
             ctx->N0 = ctx->h_stats[ST_N0];
             ctx->nnzC0 = ctx->h_stats[ST_NNZC];
         }
@@ -720,31 +753,38 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
                 throw McError{ctx->h_stats[ST_THR_STATUS], "no positive observer count (np.percentile of an empty array)"};
             nthr = ctx->h_stats[ST_NTHR];
         }
-        const int N0 = ctx->N0, F = ctx->F, FW = ctx->FW, Mn = ctx->Mn;
+        const int N0 = ctx->N0, FW = ctx->FW, Mn = ctx->Mn;
         MC_REQUIRE(!(N0 == 0 && nthr > 0), MC_ERR_NO_NODES, "no nodes to cluster (torch.stack of an empty list)");
-        const bool dense = !(connect_threshold > 0.0);  // ct <= 0: every pair with O >= thr connects
+        const bool dense = !(connect_threshold > 0.0);  // ct <= 0: all pairs with O >= thr (NaN: no edge)
         const bool ct_nan = std::isnan(connect_threshold);
-        std::vector<int> smin = build_smin(F, ct_nan ? std::nan("") : connect_threshold, std::max(Mn, 1));
+        const bool dense_obs = dense && !ct_nan;
+        const float ctf = static_cast<float>(connect_threshold);  // torch compares in float32
         const size_t n0 = static_cast<size_t>(std::max(N0, 1));
         const size_t cap = static_cast<size_t>(std::max<int64_t>(ctx->nnzC0, 1));
-        ctx->d_smin.reserve((F + 1) * sizeof(int));
-        MC_HIP(hipMemcpyAsync(ctx->d_smin.ptr, smin.data(), (F + 1) * sizeof(int), hipMemcpyHostToDevice, s));
         ctx->d_parent.reserve(n0 * 4);
         ctx->d_root.reserve(n0 * 4);
         ctx->d_isroot.reserve(n0 * 4);
         ctx->d_rank.reserve((n0 + 1) * 4);
         ctx->d_label.reserve(n0 * 4);
         ctx->d_levels.reserve(std::max<size_t>(1, static_cast<size_t>(nthr)) * n0 * 4);
+        const bool fresh_memcnt = ctx->d_memcnt.bytes < n0 * 4;
         ctx->d_memcnt.reserve(n0 * 4);
+        if (fresh_memcnt) MC_HIP(hipMemsetAsync(ctx->d_memcnt.ptr, 0, ctx->d_memcnt.bytes, s));  // kept zero by K9
         ctx->d_memoff.reserve((n0 + 1) * 4);
         ctx->d_ublen.reserve(n0 * 4);
         ctx->d_newoff.reserve((n0 + 1) * 4);
         ctx->d_members.reserve(n0 * 4);
+        const bool fresh_colcnt = ctx->d_colcnt.bytes < static_cast<size_t>(Mn + 1) * 4;
         ctx->d_colcnt.reserve((Mn + 1) * 4);
+        if (fresh_colcnt) MC_HIP(hipMemsetAsync(ctx->d_colcnt.ptr, 0, ctx->d_colcnt.bytes, s));  // kept zero by K3
         ctx->d_coloff.reserve((Mn + 2) * 4);
+        ctx->d_collen.reserve((Mn + 1) * 4);
         ctx->d_colnodes.reserve(cap * 4);
         ctx->d_ovf_list.reserve(n0 * 4);
-        ctx->d_ovf_n.reserve(4);
+        if (!ctx->d_ovf_n.ptr) {
+            ctx->d_ovf_n.reserve(4);
+            MC_HIP(hipMemsetAsync(ctx->d_ovf_n.ptr, 0, 4, s));  // kept zero by K5
+        }
         constexpr int kOvfBlocks = 64;
         if (ctx->scratch_n0 < N0) {
             ctx->d_scratch.reserve(static_cast<size_t>(kOvfBlocks) * n0 * 4);
@@ -754,9 +794,12 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         }
         ctx->d_edges.reserve(std::max(nthr, 1) * 8);
         ctx->d_Nlev.reserve((nthr + 2) * 4);
+        ctx->d_cap.reserve((nthr + 2) * 4);
         ctx->d_final_label.reserve(n0 * 4);
         ctx->d_poolA.reserve(cap * 4);
         ctx->d_poolB.reserve(cap * 4);
+        ctx->d_ownA.reserve(cap * 4);
+        ctx->d_ownB.reserve(cap * 4);
         ctx->d_offA.reserve(n0 * 4);
         ctx->d_offB.reserve(n0 * 4);
         ctx->d_lenA.reserve(n0 * 4);
@@ -772,17 +815,28 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         ctx->d_pts_out.reserve((ctx->n0_pts_total + 1) * 4);
 
         int *Nlev = ctx->d_Nlev.as<int>();
-        if (ctx->nodes_from_graph) {
-            hipLaunchKernelGGL(mc::k_copy_i32, dim3(1), dim3(1), 0, s, stats + ST_N0, Nlev);
-        } else {
-            MC_HIP(hipMemcpyAsync(Nlev, &ctx->N0, sizeof(int), hipMemcpyHostToDevice, s));
-        }
-        MC_HIP(hipMemsetAsync(ctx->d_edges.ptr, 0, std::max(nthr, 1) * 8, s));
-        hipLaunchKernelGGL(mc::k6_iota, grid_for(N0), dim3(256), 0, s, N0, ctx->d_final_label.as<int>());
+        int *dcap = ctx->d_cap.as<int>();
+        hipLaunchKernelGGL(mc::k6_init, grid_for(std::max<int64_t>(N0, nthr)), dim3(256), 0, s, N0,
+                           ctx->d_final_label.as<int>(), ctx->nodes_from_graph ? stats + ST_N0 : nullptr, N0, Nlev,
+                           dcap, ctx->nodes_from_graph ? stats + ST_NNZC : nullptr, static_cast<int>(ctx->nnzC0),
+                           ctx->d_edges.as<unsigned long long>(), nthr);
 
         const int *cur_off = ctx->d_n0_off.as<int>(), *cur_len = ctx->d_n0_len.as<int>(), *cur_pool = ctx->n0_pool;
+        const int *cur_own = ctx->d_owner0.as<int>();
         const unsigned long long *cur_vf = ctx->d_n0_vf.as<unsigned long long>();
-        const dim3 gN = grid_for(N0), gW = grid_for(N0, mc::kPairWaves, 8192), gK = grid_for(N0, 1, 4096);
+        const dim3 gN = grid_for(N0), gE = grid_for(std::max<int64_t>(N0, ctx->nnzC0)),
+                   gW = grid_for(N0, mc::kPairWaves, 2048), gK = grid_for(N0, 1, 2048),
+                   gC = grid_for(std::max(N0, Mn), 64, 8192);
+        if (!dense_obs && nthr > 0) {  // level-0 column lists (nodes contained by each mask)
+            TimedScope ts(ctx->timer, s, "s6_columns");
+            hipLaunchKernelGGL(mc::k6_colcount, gE, dim3(256), 0, s, Nlev, dcap, cur_pool, cur_own,
+                               ctx->d_parent.as<int>(), ctx->d_colcnt.as<int>());
+            mc::scan_device_n(s, ctx->d_colcnt.as<int>(), ctx->d_coloff.as<int>(), nullptr, Mn, nullptr);
+            hipLaunchKernelGGL(mc::k6_colscatter, gE, dim3(256), 0, s, dcap, cur_pool, cur_own,
+                               ctx->d_coloff.as<int>(), ctx->d_colcnt.as<int>(), ctx->d_colnodes.as<int>());
+            hipLaunchKernelGGL(mc::k6_colupdate, gC, dim3(64), 0, s, Mn, Nlev, ctx->d_coloff.as<int>(),
+                               ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), nullptr, ctx->d_parent.as<int>());
+        }
         for (int t = 0; t < nthr; t++) {
             const int *dN = Nlev + t;
             int *dNn = Nlev + t + 1;
@@ -790,34 +844,30 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             int *nx_off = toA ? ctx->d_offA.as<int>() : ctx->d_offB.as<int>();
             int *nx_len = toA ? ctx->d_lenA.as<int>() : ctx->d_lenB.as<int>();
             int *nx_pool = toA ? ctx->d_poolA.as<int>() : ctx->d_poolB.as<int>();
+            int *nx_own = toA ? ctx->d_ownA.as<int>() : ctx->d_ownB.as<int>();
             unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
-            {
-                TimedScope ts(ctx->timer, s, "s6_columns");
-                if (!dense) MC_HIP(hipMemsetAsync(ctx->d_colcnt.ptr, 0, (Mn + 1) * 4, s));
-                hipLaunchKernelGGL(mc::k6_prep, gN, dim3(256), 0, s, dN, cur_off, dense ? ctx->d_n0_len.as<int>() : cur_len,
-                                   cur_pool, ctx->d_parent.as<int>(), ctx->d_colcnt.as<int>());
-                if (!dense) {
-                    mc::scan_device_n(s, ctx->d_colcnt.as<int>(), ctx->d_coloff.as<int>(), nullptr, Mn, nullptr);
-                    hipLaunchKernelGGL(mc::k6_colscatter, gN, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
-                                       ctx->d_coloff.as<int>(), ctx->d_colcnt.as<int>(), ctx->d_colnodes.as<int>());
+            if (!dense_obs) {
+                if (t > 0) {
+                    TimedScope ts(ctx->timer, s, "s6_columns");
+                    hipLaunchKernelGGL(mc::k6_colupdate, gC, dim3(64), 0, s, Mn, dN, ctx->d_coloff.as<int>(),
+                                       ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), ctx->d_label.as<int>(),
+                                       ctx->d_parent.as<int>());
                 }
-            }
-            if (!dense) {
                 TimedScope ts(ctx->timer, s, "s6_pairs");
-                MC_HIP(hipMemsetAsync(ctx->d_ovf_n.ptr, 0, 4, s));
                 hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
-                                   ctx->d_coloff.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
-                                   ctx->d_thr.as<float>(), t, ctx->d_smin.as<int>(), ctx->d_parent.as<int>(),
+                                   ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
+                                   ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
                                    ctx->d_edges.as<unsigned long long>(), ctx->d_ovf_list.as<int>(),
                                    ctx->d_ovf_n.as<int>());
                 hipLaunchKernelGGL(mc::k6_pairs_overflow, dim3(kOvfBlocks), dim3(256), 0, s, ctx->d_ovf_list.as<int>(),
                                    ctx->d_ovf_n.as<int>(), cur_off, cur_len, cur_pool, ctx->d_coloff.as<int>(),
-                                   ctx->d_colnodes.as<int>(), cur_vf, FW, ctx->d_thr.as<float>(), t,
-                                   ctx->d_smin.as<int>(), ctx->d_parent.as<int>(),
+                                   ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
+                                   ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
                                    ctx->d_edges.as<unsigned long long>(), ctx->d_scratch.as<int>(),
                                    ctx->d_touched.as<int>(), N0);
             } else {
                 TimedScope ts(ctx->timer, s, "s6_pairs");
+                hipLaunchKernelGGL(mc::k6_parent_init, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>());
                 hipLaunchKernelGGL(mc::k6_pairs_dense, dim3(4096), dim3(256), 0, s, dN, cur_vf, FW,
                                    ctx->d_thr.as<float>(), t, ctx->d_parent.as<int>(),
                                    ctx->d_edges.as<unsigned long long>());
@@ -825,29 +875,28 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             {
                 TimedScope ts(ctx->timer, s, "s6_components");
                 hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
-                                   ctx->d_root.as<int>(), ctx->d_isroot.as<int>());
+                                   ctx->d_root.as<int>(), ctx->d_isroot.as<int>(), ctx->d_ublen.as<int>(),
+                                   ctx->d_ovf_n.as<int>());
                 mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
-                MC_HIP(hipMemsetAsync(ctx->d_memcnt.ptr, 0, n0 * 4, s));
-                MC_HIP(hipMemsetAsync(ctx->d_ublen.ptr, 0, n0 * 4, s));
                 hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(), ctx->d_rank.as<int>(),
                                    cur_len, ctx->d_label.as<int>(), ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0,
                                    ctx->d_memcnt.as<int>(), ctx->d_ublen.as<int>());
-                mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr);
-                mc::scan_device_n(s, ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dNn, 0, nullptr);
-                hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, ctx->d_label.as<int>(),
-                                   ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>());
+                mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr,
+                                  ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dcap + t + 1);
+                hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, N0, ctx->d_label.as<int>(),
+                                   ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>(),
+                                   ctx->d_final_label.as<int>());
             }
             {
                 TimedScope ts(ctx->timer, s, "s6_merge");
                 hipLaunchKernelGGL(mc::k6_merge, gK, dim3(256), 0, s, dNn, ctx->d_memoff.as<int>(),
                                    ctx->d_members.as<int>(), cur_off, cur_len, cur_pool, cur_vf, FW,
-                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_vf);
-                hipLaunchKernelGGL(mc::k6_maplevel, gN, dim3(256), 0, s, N0, ctx->d_label.as<int>(),
-                                   ctx->d_final_label.as<int>());
+                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_own, nx_vf);
             }
             cur_off = nx_off;
             cur_len = nx_len;
             cur_pool = nx_pool;
+            cur_own = nx_own;
             cur_vf = nx_vf;
         }
         ctx->fin_off = cur_off;
@@ -857,28 +906,54 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         ctx->n_iter = nthr;
         // ---- final point sets (node.py:35), per-object range bitmaps ----
         const int *dK = Nlev + nthr;
+        const bool point_path = ctx->nodes_from_graph;
         {
             TimedScope ts(ctx->timer, s, "s7_points");
-            hipLaunchKernelGGL(mc::k_fill_i32, gN, dim3(256), 0, s, ctx->d_pmin.as<int>(), N0, INT_MAX);
-            hipLaunchKernelGGL(mc::k_fill_i32, gN, dim3(256), 0, s, ctx->d_pmax.as<int>(), N0, -1);
-            hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
-                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts, ctx->d_pmin.as<int>(),
-                               ctx->d_pmax.as<int>());
+            hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+            if (point_path) {
+                hipLaunchKernelGGL(mc::k7_obj_of_mask, grid_for(ctx->M), dim3(256), 0, s, ctx->M,
+                                   ctx->d_node_of_mask.as<int>(), ctx->d_final_label.as<int>(),
+                                   ctx->d_obj_of_mask.as<int>());
+                hipLaunchKernelGGL(mc::k7p_points<0>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
+                                   ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
+                                   ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(), nullptr,
+                                   nullptr, stats + ST_OBJOVF);
+            }
+            else
+                hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                                   ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                                   ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
             hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
-                               ctx->d_nwords.as<int>());
+                               ctx->d_nwords.as<int>(), stats + ST_K);
             mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
-            hipLaunchKernelGGL(mc::k_copy_i32, dim3(1), dim3(1), 0, s, dK, stats + ST_K);
         }
         sync_stats(ctx);  // bitmap capacity
         ctx->K = ctx->h_stats[ST_K];
+        const bool use_points = point_path && ctx->h_stats[ST_OBJOVF] == 0;
+        if (point_path && !use_points) {  // a point in > 8 objects: redo the ranges per node
+            hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+            hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                               ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+            hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                               ctx->d_nwords.as<int>(), stats + ST_K);
+            mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
+            sync_stats(ctx);
+        }
         const size_t words = static_cast<size_t>(std::max(ctx->h_stats[ST_WORDS], 1));
         ctx->d_bm.reserve(words * 8);
         {
             TimedScope ts(ctx->timer, s, "s7_points");
             MC_HIP(hipMemsetAsync(ctx->d_bm.ptr, 0, words * 8, s));
-            hipLaunchKernelGGL(mc::k7_setbits, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
-                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts, ctx->d_pmin.as<int>(),
-                               ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>());
+            if (use_points)
+                hipLaunchKernelGGL(mc::k7p_points<1>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
+                                   ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
+                                   ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                                   ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>(), stats + ST_OBJOVF);
+            else
+                hipLaunchKernelGGL(mc::k7_setbits, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                                   ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                                   ctx->d_pmin.as<int>(), ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>());
             hipLaunchKernelGGL(mc::k7_count, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
                                ctx->d_bm.as<unsigned long long>(), ctx->d_ptcnt.as<int>());
             mc::scan_device_n(s, ctx->d_ptcnt.as<int>(), ctx->d_ptoff_out.as<int>(), dK, 0, stats + ST_NPTS);

@@ -62,6 +62,7 @@ inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) 
 // Kernel timing with events (enabled only by bench/profiling runs).
 struct KernelTimer {
     bool enabled = false;
+    std::string filter;  // empty = every scope
     struct Rec {
         hipEvent_t a, b;
         std::string name;
@@ -107,15 +108,17 @@ struct TimedScope {
     hipStream_t s;
     hipEvent_t a{}, b{};
     const char *name;
-    TimedScope(KernelTimer &t_, hipStream_t s_, const char *n) : t(t_), s(s_), name(n) {
-        if (t.enabled) {
+    bool on;
+    TimedScope(KernelTimer &t_, hipStream_t s_, const char *n)
+        : t(t_), s(s_), name(n), on(t_.enabled && (t_.filter.empty() || t_.filter == n)) {
+        if (on) {
             a = t.get();
             b = t.get();
             MC_HIP(hipEventRecord(a, s));
         }
     }
     ~TimedScope() {
-        if (t.enabled) {
+        if (on) {
             (void)hipEventRecord(b, s);
             t.pending.push_back({a, b, name});
         }

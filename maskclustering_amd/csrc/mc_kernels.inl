@@ -1,15 +1,16 @@
-// mc_kernels.hip — gfx950 kernels of the view-consensus graph path.
+// mc_kernels.inl — gfx950 kernels of the view-consensus graph path (included by mc_api.hip).
 //
-// Data layout in HBM (see DESIGN.md §3):
+// Data layout in HBM (DESIGN.md §3):
 //   mask CSR      mask_off[M+1] (i32), mask_pts[nnz] (i32)      S1 output, read-only
 //   point lists   pt_off[P+1], pt_list[nnz] (u32 = frame<<12 | mask-in-frame), sorted per point
 //   boundary[P]   u8;  pfm[P][FW] u64 point-frame bits (FW = ceil(F/64))
 //   C rows        c_off[M+1], c_idx[nnzC] (global mask ids, ascending) — contained_masks after undo
 //   VF            vf[M][FW] u64 — visible_frames after undo (== frames of the C row)
-//   nodes (S6)    (off,len) into a C pool + vf[N][FW]; double-buffered pools per iteration
+//   nodes (S6)    (off,len) into a C pool + slot owner per pool slot + vf[N][FW]; pools ping-pong
 //
 // Every kernel that works on a data-dependent count reads it from device memory
-// (no host round trip inside the S6 loop).
+// (no host round trip inside the S6 loop).  Counters that kernels accumulate into
+// are restored to zero by the kernel that consumes them (no per-iteration memsets).
 #include "mc_internal.hpp"
 
 #include <climits>
@@ -84,40 +85,59 @@ __device__ __forceinline__ void st_agent(int *p, int v)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
 // ---------------------------------------------------------------------------------------------
 // scans
 // ---------------------------------------------------------------------------------------------
 // Exclusive scan of n ints (n read from *dn when dn != nullptr) by ONE 1024-thread workgroup.
-// out[0..n] gets n+1 entries (out[n] = total); *dtotal = total when given.
-// Used for every device-sized scan (N <= M): one launch, no host round trip.
-__global__ __launch_bounds__(1024) void k_scan1(const int *__restrict__ in, int *__restrict__ out,
-                                                const int *dn, int n_host, int *dtotal)
+// out[0..n] gets n+1 entries (out[n] = total); *dtotal = total when given.  Up to two
+// independent arrays per launch (in2/out2 may be null).  Tiles of 8192 ints are staged
+// through LDS so global loads and stores are coalesced; LDS index padded (i + i/32).
+constexpr int kScan1Tile = 8192;
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 5); }
+
+__global__ __launch_bounds__(1024) void k_scan1(const int *__restrict__ in, int *__restrict__ out, const int *dn,
+                                                int n_host, int *dtotal, const int *__restrict__ in2,
+                                                int *__restrict__ out2, int *dtotal2)
 {
+    __shared__ int buf[kScan1Tile + kScan1Tile / 32];
     __shared__ int ws[16];
     const int n = dn ? *dn : n_host;
-    constexpr int IT = 4;
-    int carry = 0;
-    for (int base = 0; base < n; base += 1024 * IT) {
-        int v[IT];
-        int s = 0;
-        const int i0 = base + threadIdx.x * IT;
+    constexpr int IT = kScan1Tile / 1024;
+    for (int arr = 0; arr < 2; arr++) {
+        const int *src = arr == 0 ? in : in2;
+        int *dst = arr == 0 ? out : out2;
+        int *tot_out = arr == 0 ? dtotal : dtotal2;
+        if (!src) break;
+        int carry = 0;
+        for (int base = 0; base < n; base += kScan1Tile) {
+            const int cnt = min(kScan1Tile, n - base);
+            for (int i = threadIdx.x; i < kScan1Tile; i += 1024) buf[scan_pad(i)] = i < cnt ? src[base + i] : 0;
+            __syncthreads();
+            int v[IT];
+            int s = 0;
 #pragma unroll
-        for (int k = 0; k < IT; k++) {
-            v[k] = (i0 + k < n) ? in[i0 + k] : 0;
-            s += v[k];
-        }
-        int tot;
-        int ex = block_excl_scan<1024>(s, ws, tot) + carry;
+            for (int k = 0; k < IT; k++) {
+                v[k] = buf[scan_pad(threadIdx.x * IT + k)];
+                s += v[k];
+            }
+            int tot;
+            int ex = block_excl_scan<1024>(s, ws, tot) + carry;
 #pragma unroll
-        for (int k = 0; k < IT; k++) {
-            if (i0 + k < n) out[i0 + k] = ex;
-            ex += v[k];
+            for (int k = 0; k < IT; k++) {
+                buf[scan_pad(threadIdx.x * IT + k)] = ex;
+                ex += v[k];
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i < cnt; i += 1024) dst[base + i] = buf[scan_pad(i)];
+            carry += tot;
+            __syncthreads();
         }
-        carry += tot;
-    }
-    if (threadIdx.x == 0) {
-        out[n] = carry;
-        if (dtotal) *dtotal = carry;
+        if (threadIdx.x == 0) {
+            dst[n] = carry;
+            if (tot_out) *tot_out = carry;
+        }
     }
 }
 
@@ -159,9 +179,10 @@ __global__ __launch_bounds__(256) void k_scan_down(const int *__restrict__ in, i
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = pscan[gridDim.x];
 }
 
-void scan_device_n(hipStream_t s, const int *in, int *out, const int *dn, int n_host, int *dtotal)
+void scan_device_n(hipStream_t s, const int *in, int *out, const int *dn, int n_host, int *dtotal,
+                   const int *in2 = nullptr, int *out2 = nullptr, int *dtotal2 = nullptr)
 {
-    hipLaunchKernelGGL(k_scan1, dim3(1), dim3(1024), 0, s, in, out, dn, n_host, dtotal);
+    hipLaunchKernelGGL(k_scan1, dim3(1), dim3(1024), 0, s, in, out, dn, n_host, dtotal, in2, out2, dtotal2);
 }
 
 void scan_large(hipStream_t s, const int *in, int *out, int n, int *tmp /* >= 2*(n/tile+2) */)
@@ -179,17 +200,20 @@ void scan_large(hipStream_t s, const int *in, int *out, int n, int *tmp /* >= 2*
 // ---------------------------------------------------------------------------------------------
 // S2  point-in-mask structure (graph/construction.py:22-64)
 // ---------------------------------------------------------------------------------------------
-// deg[p] += 1 for every (mask, point) entry
-__global__ __launch_bounds__(256) void k_s2_degree(const int *__restrict__ pts, int nnz, int *__restrict__ deg)
+// deg[p] += 1 for every (mask, point) entry.  Block 0 also clears the statistics block.
+__global__ __launch_bounds__(256) void k_s2_degree(const int *__restrict__ pts, int nnz, int *__restrict__ deg,
+                                                   int *__restrict__ stats, int nstats)
 {
+    if (blockIdx.x == 0 && threadIdx.x < nstats) stats[threadIdx.x] = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nnz; i += gridDim.x * 256) atomicAdd(&deg[pts[i]], 1);
 }
 
 // One workgroup per mask: append (frame << 12 | mask-in-frame) to each point's list.
+// deg[] counts down to zero again (ready for the next build, no memset).
 __global__ __launch_bounds__(256) void k_s2_scatter(const int *__restrict__ mask_off, const int *__restrict__ pts,
                                                     const int *__restrict__ mask_col,
                                                     const int *__restrict__ frame_start,
-                                                    const int *__restrict__ pt_off, int *__restrict__ cursor,
+                                                    const int *__restrict__ pt_off, int *__restrict__ deg,
                                                     unsigned *__restrict__ pt_list)
 {
     const int g = blockIdx.x;
@@ -197,51 +221,75 @@ __global__ __launch_bounds__(256) void k_s2_scatter(const int *__restrict__ mask
     const unsigned e = (static_cast<unsigned>(c) << kLocalBits) | static_cast<unsigned>(g - frame_start[c]);
     const int b = mask_off[g], en = mask_off[g + 1];
     for (int k = b + threadIdx.x; k < en; k += 256) {
-        int p = pts[k];
-        int pos = pt_off[p] + atomicAdd(&cursor[p], 1);
+        const int p = pts[k];
+        const int pos = pt_off[p] + atomicSub(&deg[p], 1) - 1;
         pt_list[pos] = e;
     }
 }
 
-// One thread per point: sort its list (frame-major), flag boundary points
-// (>= 2 masks in one frame: construction.py:56,61-62) and write the point-frame
-// bits (construction.py:52).
+// Sort one point's list (in LDS or global), flag the point as boundary if one frame
+// appears twice (>= 2 masks in one frame: construction.py:56,61-62) and write its
+// point-frame bits (construction.py:52).
+__device__ __forceinline__ int s2_point_row(unsigned *lst, int n, int FW, unsigned long long *pfm_row)
+{
+    for (int i = 1; i < n; i++) {
+        const unsigned x = lst[i];
+        int j = i - 1;
+        while (j >= 0 && lst[j] > x) {
+            lst[j + 1] = lst[j];
+            j--;
+        }
+        lst[j + 1] = x;
+    }
+    int isb = 0;
+    unsigned prevc = 0xffffffffu;
+    int q = 0;
+    for (int w = 0; w < FW; w++) {
+        unsigned long long word = 0;
+        while (q < n) {
+            const unsigned c = lst[q] >> kLocalBits;
+            if (static_cast<int>(c >> 6) != w) break;
+            if (c == prevc) isb = 1;
+            prevc = c;
+            word |= 1ull << (c & 63);
+            q++;
+        }
+        pfm_row[w] = word;
+    }
+    return isb;
+}
+
+// 256 consecutive points per workgroup; their lists are one contiguous range of pt_list,
+// staged through LDS when it fits (coalesced load, LDS sort, coalesced store).
+constexpr int kS2Stage = 8192;
+
 __global__ __launch_bounds__(256) void k_s2_points(const int *__restrict__ pt_off, unsigned *__restrict__ pt_list,
                                                    int P, int FW, unsigned char *__restrict__ boundary,
                                                    unsigned long long *__restrict__ pfm, int *__restrict__ nbnd)
 {
-    const int p = blockIdx.x * 256 + threadIdx.x;
+    __shared__ unsigned stage[kS2Stage];
+    const int p0 = blockIdx.x * 256;
+    const int p = p0 + threadIdx.x;
+    const int pend = min(P, p0 + 256);
+    const int eb = pt_off[p0], ee = pt_off[pend];
+    const bool staged = (ee - eb) <= kS2Stage;
     int isb = 0;
-    if (p < P) {
+    if (staged) {
+        for (int i = threadIdx.x; i < ee - eb; i += 256) stage[i] = pt_list[eb + i];
+        __syncthreads();
+        if (p < P) {
+            const int b = pt_off[p] - eb, e = pt_off[p + 1] - eb;
+            isb = s2_point_row(stage + b, e - b, FW, pfm + static_cast<size_t>(p) * FW);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < ee - eb; i += 256) pt_list[eb + i] = stage[i];
+    } else if (p < P) {
         const int b = pt_off[p], e = pt_off[p + 1];
-        for (int i = b + 1; i < e; i++) {
-            unsigned x = pt_list[i];
-            int j = i - 1;
-            while (j >= b && pt_list[j] > x) {
-                pt_list[j + 1] = pt_list[j];
-                j--;
-            }
-            pt_list[j + 1] = x;
-        }
-        unsigned prevc = 0xffffffffu;
-        int q = b;
-        for (int w = 0; w < FW; w++) {
-            unsigned long long word = 0;
-            while (q < e) {
-                unsigned c = pt_list[q] >> kLocalBits;
-                if (static_cast<int>(c >> 6) != w) break;
-                if (c == prevc) isb = 1;
-                prevc = c;
-                word |= 1ull << (c & 63);
-                q++;
-            }
-            pfm[static_cast<size_t>(p) * FW + w] = word;
-        }
-        boundary[p] = static_cast<unsigned char>(isb);
+        isb = s2_point_row(pt_list + b, e - b, FW, pfm + static_cast<size_t>(p) * FW);
     }
-    // wave-aggregated boundary count
-    unsigned long long bal = __ballot(isb);
-    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(nbnd, __popcll(bal));
+    if (p < P) boundary[p] = static_cast<unsigned char>(isb);
+    const unsigned long long bal = __ballot(isb);
+    if (lane_id() == 0 && bal) atomicAdd(nbnd, __popcll(bal));
 }
 
 // Dense point_in_mask_matrix (uint16 P×F) for the getter only (construction.py:39,58,61).
@@ -264,190 +312,241 @@ __global__ __launch_bounds__(256) void k_s2_dense_pim(const int *__restrict__ pt
 // ---------------------------------------------------------------------------------------------
 // S3  process_one_mask / process_masks (graph/construction.py:98-170)
 // ---------------------------------------------------------------------------------------------
-// One workgroup per mask g.  V = S_g \ boundary, T = |V| (construction.py:105).
-// Pass 1 marks the frames in which some point of V lies in a mask ("possibly visible",
-// :110).  Touched frames are ranked; each gets a slot range of one LDS counter per mask
-// of that frame.  Pass 2 counts, per (frame, mask), the points of V in that mask (the
-// per-frame bincount, :116).  Pass 3 applies the reference's rules in float64:
-//   skip if (1 - c0/T) < mvt and nz < 500                          (:117-120)
-//   visible; argmax mask (smallest id on ties); contained if cmax/nz > ct  (:121-128)
-//   otherwise split                                                 (:130)
-// Touched frames are processed in windows when their masks exceed the LDS counters.
-constexpr int kS3Threads = 256;
-constexpr int kS3Counters = 4096;
-constexpr int kS3Window = 512;
-constexpr int kS3MaxFrameWords = 512;  // F <= 16384
+// S3 kernel, W waves per mask (W = 1: four masks per workgroup, wave-private LDS;
+// W = 4: one mask per workgroup, for large masks).  V = S_g \ boundary, T = |V|
+// (construction.py:105).
+//  pass 1: the frames in which some point of V lies in a mask ("possibly visible",
+//          :110) = OR of the point-frame bit rows of V (no pass over list entries);
+//          touched frames are ranked by a popcount prefix over that bitmap.
+//  pass 2: per (touched frame, mask of the frame) LDS counters count the points of V in
+//          that mask (the per-frame bincount, :116); list entries are read by 16-lane
+//          groups (one point per group), so loads are coalesced.
+//  pass 3: one lane per touched frame applies the reference's rules in float64:
+//          skip if (1 - c0/T) < mvt and nz < 500                          (:117-120)
+//          visible; argmax mask (smallest id on ties); contained if cmax/nz > ct (:121-128)
+//          otherwise split                                                 (:130)
+// Touched frames are processed in windows of 64·W frames / CNT counters.
+template <int W> struct S3Cfg;
+template <> struct S3Cfg<1> { static constexpr int FWMAX = 32, CNT = 1024; };   // F <= 2048
+template <> struct S3Cfg<4> { static constexpr int FWMAX = 256, CNT = 4096; };  // F <= 16384
+constexpr int kS3SmallPts = 1024;  // masks up to this size go to the W = 1 kernel
+constexpr int kS3Batch = 8;        // list entries gathered per lane before use
+constexpr int kS3wCounters = S3Cfg<1>::CNT;
+constexpr int kS3wFrameWords64 = S3Cfg<1>::FWMAX;
 
-__global__ __launch_bounds__(kS3Threads) void k_s3_masks(
-    const int *__restrict__ mask_off, const int *__restrict__ pts, const int *__restrict__ pt_off,
-    const unsigned *__restrict__ pt_list, const unsigned char *__restrict__ boundary,
-    const int *__restrict__ frame_start, const int *__restrict__ mask_label, int F, double mvt, double ctn,
-    double ust, int *__restrict__ ctmp, int *__restrict__ crow_len, unsigned char *__restrict__ useg)
+template <int W>
+__device__ __forceinline__ void s3_sync()
 {
-    __shared__ unsigned fbits[kS3MaxFrameWords];
-    __shared__ int wpre[kS3MaxFrameWords];
-    __shared__ int tf_frame[kS3Window];
-    __shared__ int tf_slot[kS3Window + 1];
-    __shared__ int tf_dec[kS3Window];
-    __shared__ int tf_tgt[kS3Window];
-    __shared__ int cnt[kS3Counters];
-    __shared__ int ws[kS3Threads / 64];
-    __shared__ int s_jn, s_slots;
+    if (W == 1) wave_sync();
+    else __syncthreads();
+}
 
-    const int g = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int FB = (F + 31) >> 5;
-    const int b = mask_off[g], en = mask_off[g + 1];
-    int *crow = ctmp + static_cast<size_t>(g) * F;
-
-    for (int w = tid; w < FB; w += kS3Threads) fbits[w] = 0u;
-    __syncthreads();
-    // pass 1
-    int myT = 0;
-    for (int k = b + tid; k < en; k += kS3Threads) {
-        const int p = pts[k];
-        if (boundary[p]) continue;
-        myT++;
-        const int pb = pt_off[p], pe = pt_off[p + 1];
-        for (int i = pb; i < pe; i++) {
-            const unsigned c = pt_list[i] >> kLocalBits;
-            atomicOr(&fbits[c >> 5], 1u << (c & 31));
-        }
+// exclusive scan / sum over the 64·W threads of one mask
+template <int W>
+__device__ __forceinline__ int s3_excl_scan(int v, int *ws, int &total)
+{
+    if (W == 1) {
+        const int inc = wave_incl_scan(v);
+        total = __shfl(inc, 63, 64);
+        return inc - v;
     }
-    const int T = block_sum<kS3Threads>(myT, ws);
-    // rank of touched frames: prefix popcount over bitmap words
-    int ntf = 0;
-    {
-        int carry = 0;
-        for (int w0 = 0; w0 < FB; w0 += kS3Threads) {
-            const int w = w0 + tid;
-            const int v = w < FB ? __popc(fbits[w]) : 0;
+    return block_excl_scan<64 * W>(v, ws, total);
+}
+
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, 64);
+    return v;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_s3_masks(
+    const int *__restrict__ list, int nlist, const int *__restrict__ mask_off, const int *__restrict__ pts,
+    const int *__restrict__ pt_off, const unsigned *__restrict__ pt_list, const unsigned char *__restrict__ boundary,
+    const unsigned long long *__restrict__ pfm, int FW, const int *__restrict__ frame_start,
+    const int *__restrict__ mask_label, int F, double mvt, double ctn, double ust, int *__restrict__ ctmp,
+    int *__restrict__ crow_len, unsigned char *__restrict__ useg)
+{
+    constexpr int SLOTS = 4 / W, FWMAX = S3Cfg<W>::FWMAX, CNT = S3Cfg<W>::CNT, WIN = 64 * W;
+    __shared__ unsigned long long fb_s[SLOTS][FWMAX];
+    __shared__ int wpre_s[SLOTS][FWMAX];
+    __shared__ int tfr_s[SLOTS][WIN];
+    __shared__ int tsl_s[SLOTS][WIN + 1];
+    __shared__ int cnt_s[SLOTS][CNT];
+    __shared__ int spre_s[4][64];
+    __shared__ int spb_s[4][64];
+    __shared__ int ws[4];
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int slot = wv / W, wl = wv % W, tl = wl * 64 + lane;
+    unsigned long long *fb = fb_s[slot];
+    int *wpre = wpre_s[slot], *tf_frame = tfr_s[slot], *tf_slot = tsl_s[slot], *cnt = cnt_s[slot];
+    const int FB = (F + 63) >> 6;  // == FW
+
+    for (int q = blockIdx.x * SLOTS + slot; q < nlist; q += gridDim.x * SLOTS) {
+        const int g = list[q];
+        const int b = mask_off[g], en = mask_off[g + 1];
+        int *crow = ctmp + static_cast<size_t>(g) * F;
+        for (int w = tl; w < FB; w += 64 * W) fb[w] = 0ull;
+        s3_sync<W>();
+        // pass 1: touched frames = OR of pfm rows of V; T = |V|
+        int myT = 0;
+        for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
+            const int k = k0 + lane;
+            const int p = k < en ? pts[k] : 0;
+            const bool nb = k < en && !boundary[p];
+            myT += nb ? 1 : 0;
+            for (int w = 0; w < FW; w++) {
+                unsigned long long v = nb ? pfm[static_cast<size_t>(p) * FW + w] : 0ull;
+                v = wave_or64(v);
+                if (lane == 0 && v) atomicOr(&fb[w], v);
+            }
+        }
+        int T;
+        if (W == 1) T = wave_sum(myT);
+        else T = block_sum<64 * W>(myT, ws);
+        s3_sync<W>();
+        int ntf = 0;
+        for (int w0 = 0; w0 < FB; w0 += 64 * W) {  // rank prefix over bitmap words
+            const int w = w0 + tl;
+            const int pc = w < FB ? __popcll(fb[w]) : 0;
             int tot;
-            const int ex = block_excl_scan<kS3Threads>(v, ws, tot);
-            if (w < FB) wpre[w] = ex + carry;
-            carry += tot;
+            const int ex = s3_excl_scan<W>(pc, ws, tot);
+            if (w < FB) wpre[w] = ex + ntf;
+            ntf += tot;
         }
-        ntf = carry;
-    }
-    __syncthreads();
-
-    int vis = 0, split = 0, ncont = 0;  // uniform across the block
-    for (int j0 = 0; j0 < ntf;) {
-        // frames of rank [j0, j0 + window)
-        for (int w = tid; w < FB; w += kS3Threads) {
-            unsigned bits = fbits[w];
-            int r = wpre[w];
-            while (bits) {
-                const int bt = __ffs(bits) - 1;
-                bits &= bits - 1;
-                if (r >= j0 && r < j0 + kS3Window) tf_frame[r - j0] = (w << 5) + bt;
-                r++;
-            }
-        }
-        __syncthreads();
-        const int jmax = min(kS3Window, ntf - j0);
-        // slot bases (exclusive scan of masks-per-frame), cut the window at the counter capacity
-        {
-            int carry = 0;
-            for (int i0 = 0; i0 < jmax; i0 += kS3Threads) {
-                const int i = i0 + tid;
-                const int nm = i < jmax ? frame_start[tf_frame[i] + 1] - frame_start[tf_frame[i]] : 0;
-                int tot;
-                const int ex = block_excl_scan<kS3Threads>(nm, ws, tot);
-                if (i < jmax) tf_slot[i] = ex + carry;
-                carry += tot;
-            }
-            if (tid == 0) tf_slot[jmax] = carry;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int jn = jmax;
-            if (tf_slot[jmax] > kS3Counters) {
-                // largest jn with tf_slot[jn] <= capacity (every frame has < 4096 masks)
-                int lo = 1, hi = jmax;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (tf_slot[mid] <= kS3Counters) lo = mid;
-                    else hi = mid - 1;
+        s3_sync<W>();
+        int vis = 0, split = 0, ncont = 0;
+        for (int j0 = 0; j0 < ntf;) {
+            for (int w = tl; w < FB; w += 64 * W) {  // frames of rank [j0, j0 + WIN)
+                unsigned long long bits = fb[w];
+                int r = wpre[w];
+                while (bits) {
+                    const int bt = __ffsll(static_cast<long long>(bits)) - 1;
+                    bits &= bits - 1;
+                    if (r >= j0 && r < j0 + WIN) tf_frame[r - j0] = (w << 6) + bt;
+                    r++;
                 }
-                jn = lo;
             }
-            s_jn = jn;
-            s_slots = tf_slot[jn];
-        }
-        __syncthreads();
-        const int jn = s_jn, nslots = s_slots;
-        for (int i = tid; i < nslots; i += kS3Threads) cnt[i] = 0;
-        __syncthreads();
-        // pass 2: per (frame, mask) counts of V
-        for (int k = b + tid; k < en; k += kS3Threads) {
-            const int p = pts[k];
-            if (boundary[p]) continue;
-            const int pb = pt_off[p], pe = pt_off[p + 1];
-            for (int i = pb; i < pe; i++) {
-                const unsigned e = pt_list[i];
-                const unsigned c = e >> kLocalBits;
-                const int r = wpre[c >> 5] + __popc(fbits[c >> 5] & ((1u << (c & 31)) - 1u)) - j0;
-                if (r >= 0 && r < jn) atomicAdd(&cnt[tf_slot[r] + static_cast<int>(e & (kMaxMasksPerFrame - 1))], 1);
+            s3_sync<W>();
+            const int jmax = min(WIN, ntf - j0);
+            const int fr = tl < jmax ? tf_frame[tl] : 0;
+            const int fs_l = tl < jmax ? frame_start[fr] : 0;
+            const int nm = tl < jmax ? frame_start[fr + 1] - fs_l : 0;
+            int tot;
+            const int ex = s3_excl_scan<W>(nm, ws, tot);
+            // window = longest prefix of frames whose counters fit (at least one frame)
+            int jn;
+            {
+                const int fits = (tl < jmax && ex + nm <= CNT) ? 1 : 0;
+                int nf;
+                s3_excl_scan<W>(fits, ws, nf);
+                jn = max(1, nf);
             }
-        }
-        __syncthreads();
-        // pass 3: the reference's per-frame decision
-        for (int i = tid; i < jn; i += kS3Threads) {
-            const int c = tf_frame[i];
-            const int fs = frame_start[c];
-            const int nm = frame_start[c + 1] - fs;
-            const int base = tf_slot[i];
-            int nz = 0, bc = 0, bl = 0, best = -1;
-            for (int l = 0; l < nm; l++) {
-                const int v = cnt[base + l];
-                nz += v;
-                if (v > 0) {
-                    const int lab = mask_label[fs + l];
-                    if (v > bc || (v == bc && lab < bl)) {
+            if (tl < jn) tf_slot[tl] = ex;
+            if (tl == jn - 1) tf_slot[jn] = ex + nm;
+            s3_sync<W>();
+            const int nslots = tf_slot[jn];
+            for (int x = tl; x < nslots; x += 64 * W) cnt[x] = 0;
+            s3_sync<W>();
+            // pass 2: counts.  Per chunk of 64 points the list entries are flattened and
+            // gathered kS3Batch per lane before any is consumed (independent loads in flight).
+            {
+                int *spre = spre_s[wv], *spb = spb_s[wv];
+                for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
+                    const int k = k0 + lane;
+                    int pb = 0, d = 0;
+                    if (k < en) {
+                        const int p = pts[k];
+                        if (!boundary[p]) {
+                            pb = pt_off[p];
+                            d = pt_off[p + 1] - pb;
+                        }
+                    }
+                    const int inc = wave_incl_scan(d);
+                    const int E = __shfl(inc, 63, 64);
+                    spre[lane] = inc - d;
+                    spb[lane] = pb;
+                    wave_sync();
+                    for (int base = 0; base < E; base += 64 * kS3Batch) {
+                        unsigned ent[kS3Batch];
+#pragma unroll
+                        for (int r = 0; r < kS3Batch; r++) {
+                            const int kk = base + r * 64 + lane;
+                            ent[r] = 0xffffffffu;
+                            if (kk < E) {
+                                int lo = 0;
+#pragma unroll
+                                for (int st = 32; st >= 1; st >>= 1)
+                                    if (spre[lo + st] <= kk) lo += st;
+                                ent[r] = pt_list[spb[lo] + kk - spre[lo]];
+                            }
+                        }
+#pragma unroll
+                        for (int r = 0; r < kS3Batch; r++) {
+                            const unsigned e = ent[r];
+                            if (e == 0xffffffffu) continue;
+                            const unsigned c = e >> kLocalBits;
+                            const int rr = wpre[c >> 6] + __popcll(fb[c >> 6] & ((1ull << (c & 63)) - 1ull)) - j0;
+                            if (rr >= 0 && rr < jn) atomicAdd(&cnt[tf_slot[rr] + static_cast<int>(e & (kMaxMasksPerFrame - 1))], 1);
+                        }
+                    }
+                    wave_sync();
+                }
+            }
+            s3_sync<W>();
+            // pass 3: the reference's per-frame decision
+            int dec = 0, tgt = 0;
+            if (tl < jn) {
+                const int base = tf_slot[tl];
+                int nz = 0, bc = 0, best = -1;
+                for (int l = 0; l < nm; l++) {
+                    const int v = cnt[base + l];
+                    nz += v;
+                    if (v > bc) {
                         bc = v;
-                        bl = lab;
                         best = l;
+                    } else if (v == bc && v > 0 && mask_label[fs_l + l] < mask_label[fs_l + best]) {
+                        best = l;  // np.argmax: smallest id on ties
                     }
                 }
+                const int c0 = T - nz;
+                if (1.0 - static_cast<double>(c0) / static_cast<double>(T) < mvt && nz < 500) dec = 0;
+                else if (static_cast<double>(bc) / static_cast<double>(nz) > ctn) dec = 2;
+                else dec = 1;
+                tgt = fs_l + best;
             }
-            const int c0 = T - nz;
-            int dec;
-            if (1.0 - static_cast<double>(c0) / static_cast<double>(T) < mvt && nz < 500) dec = 0;
-            else if (static_cast<double>(bc) / static_cast<double>(nz) > ctn) dec = 2;
-            else dec = 1;
-            tf_dec[i] = dec;
-            tf_tgt[i] = fs + best;
+            // ordered compaction of contained frames -> C row entries (frame order)
+            int ncw;
+            const int pos = s3_excl_scan<W>(dec == 2 ? 1 : 0, ws, ncw);
+            if (dec == 2) crow[ncont + pos] = tgt;
+            ncont += ncw;
+            int nv, ns;
+            s3_excl_scan<W>(dec >= 1 ? 1 : 0, ws, nv);
+            s3_excl_scan<W>(dec == 1 ? 1 : 0, ws, ns);
+            vis += nv;
+            split += ns;
+            j0 += jn;
+            s3_sync<W>();
         }
-        __syncthreads();
-        // ordered compaction of contained frames -> C row entries (frame order)
-        for (int i0 = 0; i0 < jn; i0 += kS3Threads) {
-            const int i = i0 + tid;
-            const int d = i < jn ? tf_dec[i] : 0;
-            int tot;
-            const int ex = block_excl_scan<kS3Threads>(d == 2 ? 1 : 0, ws, tot);
-            if (d == 2) crow[ncont + ex] = tf_tgt[i];
-            ncont += tot;
-            vis += block_sum<kS3Threads>(d >= 1 ? 1 : 0, ws);
-            split += block_sum<kS3Threads>(d == 1 ? 1 : 0, ws);
+        if (tl == 0) {
+            crow_len[g] = ncont;
+            // construction.py:132
+            useg[g] = (vis == 0 || static_cast<double>(split) / static_cast<double>(vis) > ust) ? 1 : 0;
         }
-        j0 += jn;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        crow_len[g] = ncont;
-        // construction.py:132
-        useg[g] = (vis == 0 || static_cast<double>(split) / static_cast<double>(vis) > ust) ? 1 : 0;
     }
 }
 
 // Under-segmentation undo (construction.py:164-169): drop C entries that point to an
 // under-segmented mask; VF is then exactly the frames of the remaining C entries.
+// Also clears the observer histogram for S4 (replaces a memset).
 __global__ __launch_bounds__(256) void k_s3_undo_count(const int *__restrict__ ctmp, const int *__restrict__ crow_len,
                                                        const unsigned char *__restrict__ useg, int M, int F,
-                                                       int *__restrict__ keep_cnt, int *__restrict__ node_flag)
+                                                       int *__restrict__ keep_cnt, int *__restrict__ node_flag,
+                                                       unsigned long long *__restrict__ hist)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
+    for (int v = g; v <= F; v += gridDim.x * 256) hist[v] = 0ull;
     if (g >= M) return;
     const int *row = ctmp + static_cast<size_t>(g) * F;
     int k = 0;
@@ -465,36 +564,58 @@ __global__ __launch_bounds__(256) void k_s3_undo_write(const int *__restrict__ c
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= M) return;
     const int *row = ctmp + static_cast<size_t>(g) * F;
+    unsigned long long *vrow = vf + static_cast<size_t>(g) * FW;
     int o = c_off[g];
     const int n = crow_len[g];
-    int i = 0;
-    for (int w = 0; w < FW; w++) {
-        unsigned long long word = 0;
-        while (i < n) {
-            const int t = row[i];
-            const int c = mask_col[t];
-            if ((c >> 6) != w) break;
-            if (!useg[t]) {
-                c_idx[o++] = t;
-                word |= 1ull << (c & 63);
-            }
-            i++;
+    int wcur = 0;
+    unsigned long long word = 0;
+    constexpr int B = 8;
+    for (int i0 = 0; i0 < n; i0 += B) {
+        int t[B], c[B];
+        bool keep[B];
+#pragma unroll
+        for (int j = 0; j < B; j++) t[j] = i0 + j < n ? row[i0 + j] : -1;
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            keep[j] = t[j] >= 0 && !useg[t[j] < 0 ? 0 : t[j]];
+            c[j] = t[j] >= 0 ? mask_col[t[j]] : 0;
         }
-        vf[static_cast<size_t>(g) * FW + w] = word;
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            if (!keep[j]) continue;
+            c_idx[o++] = t[j];
+            const int w = c[j] >> 6;
+            while (wcur < w) {
+                vrow[wcur++] = word;
+                word = 0;
+            }
+            word |= 1ull << (c[j] & 63);
+        }
+    }
+    while (wcur < FW) {
+        vrow[wcur++] = word;
+        word = 0;
     }
 }
 
 // S5 init_nodes (construction.py:66-78): node i = i-th non-under-segmented mask.
+// Writes the level-0 node view (rows alias the C CSR; every C slot gets its owner node,
+// -1 for rows of under-segmented masks) and the mask -> node map.
 __global__ __launch_bounds__(256) void k_s5_nodes(const int *__restrict__ node_pos, const unsigned char *__restrict__ useg,
                                                   const int *__restrict__ c_off, const int *__restrict__ mask_off,
                                                   const unsigned long long *__restrict__ vf, int M, int FW,
                                                   int *__restrict__ node0_g, int *__restrict__ n_off,
                                                   int *__restrict__ n_len, int *__restrict__ n_ptoff,
-                                                  int *__restrict__ n_ptlen, unsigned long long *__restrict__ n_vf)
+                                                  int *__restrict__ n_ptlen, unsigned long long *__restrict__ n_vf,
+                                                  int *__restrict__ slot_owner, int *__restrict__ node_of_mask)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= M || useg[g]) return;
-    const int i = node_pos[g];
+    if (g >= M) return;
+    const int owner = useg[g] ? -1 : node_pos[g];
+    node_of_mask[g] = owner;
+    for (int e = c_off[g]; e < c_off[g + 1]; e++) slot_owner[e] = owner;
+    if (owner < 0) return;
+    const int i = owner;
     node0_g[i] = g;
     n_off[i] = c_off[g];
     n_len[i] = c_off[g + 1] - c_off[g];
@@ -506,95 +627,124 @@ __global__ __launch_bounds__(256) void k_s5_nodes(const int *__restrict__ node_p
 // ---------------------------------------------------------------------------------------------
 // S4  observer-count histogram over ALL M masks (construction.py:84-86) + percentiles (:88-95)
 // ---------------------------------------------------------------------------------------------
-// Tiles of 64×64 (i, j) pairs, upper triangle; O = popcount(VF_i & VF_j); histogram of
-// positive O values with weight 2 off the diagonal (O is symmetric), 1 on it.
+// Persistent blocks walk 64×64 (i, j) tiles of the upper triangle; O = popcount(VF_i & VF_j);
+// positive O values are histogrammed with weight 2 off the diagonal (O is symmetric), 1 on it.
+// Each block keeps R lane-indexed replicas of the histogram in LDS (no same-address
+// atomics inside a wave) and reduces them once at the end.
 constexpr int kHistTile = 64, kHistKW = 8;
 
 __global__ __launch_bounds__(256) void k_s4_hist(const unsigned long long *__restrict__ vf, int M, int FW, int F,
-                                                 int nblk, unsigned long long *__restrict__ hist_g)
+                                                 int nblk, long long ntiles, int R, int HS,
+                                                 unsigned long long *__restrict__ hist_g)
 {
     extern __shared__ unsigned char smem_raw[];
     unsigned long long *A = reinterpret_cast<unsigned long long *>(smem_raw);
     unsigned long long *B = A + kHistTile * kHistKW;
-    unsigned *hist = reinterpret_cast<unsigned *>(B + kHistTile * kHistKW);
+    unsigned *hist = reinterpret_cast<unsigned *>(B + kHistTile * kHistKW);  // R replicas of HS (odd) bins
 
-    // triangular decode: bid -> (bi, bj), bi <= bj
-    int bid = blockIdx.x;
-    int bi = 0;
-    {
-        // rows have nblk, nblk-1, ... blocks
-        double nn = nblk;
-        int guess = static_cast<int>(floor((2.0 * nn + 1.0 - sqrt((2.0 * nn + 1.0) * (2.0 * nn + 1.0) - 8.0 * bid)) / 2.0));
-        if (guess < 0) guess = 0;
-        auto start = [&](int r) { return r * nblk - (r * (r - 1)) / 2; };
-        while (guess > 0 && start(guess) > bid) guess--;
-        while (guess + 1 < nblk && start(guess + 1) <= bid) guess++;
-        bi = guess;
-        bid -= start(bi);
-    }
-    const int bj = bi + bid;
-
-    for (int v = threadIdx.x; v <= F; v += 256) hist[v] = 0u;
+    for (int v = threadIdx.x; v < R * HS; v += 256) hist[v] = 0u;
+    unsigned *myh = hist + (lane_id() & (R - 1)) * HS;
     const int ti = threadIdx.x >> 2;          // row in tile
     const int tj0 = (threadIdx.x & 3) * 16;   // 16 columns
-    int acc[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) acc[k] = 0;
 
-    for (int w0 = 0; w0 < FW; w0 += kHistKW) {
-        __syncthreads();
-        for (int x = threadIdx.x; x < kHistTile * kHistKW; x += 256) {
-            const int r = x / kHistKW, w = x % kHistKW;
-            const int gi = bi * kHistTile + r, gj = bj * kHistTile + r;
-            A[x] = (gi < M && w0 + w < FW) ? vf[static_cast<size_t>(gi) * FW + w0 + w] : 0ull;
-            B[x] = (gj < M && w0 + w < FW) ? vf[static_cast<size_t>(gj) * FW + w0 + w] : 0ull;
+    auto row_start = [&](long long r) { return r * nblk - (r * (r - 1)) / 2; };
+    for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // triangular decode: tile -> (bi, bj), bi <= bj
+        const double nn = nblk;
+        long long bi = static_cast<long long>(floor((2.0 * nn + 1.0 - sqrt((2.0 * nn + 1.0) * (2.0 * nn + 1.0) - 8.0 * static_cast<double>(tile))) / 2.0));
+        if (bi < 0) bi = 0;
+        while (bi > 0 && row_start(bi) > tile) bi--;
+        while (bi + 1 < nblk && row_start(bi + 1) <= tile) bi++;
+        const long long bj = bi + (tile - row_start(bi));
+
+        int acc[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[k] = 0;
+        for (int w0 = 0; w0 < FW; w0 += kHistKW) {
+            __syncthreads();
+            for (int x = threadIdx.x; x < kHistTile * kHistKW; x += 256) {
+                const int r = x / kHistKW, w = x % kHistKW;
+                const long long gi = bi * kHistTile + r, gj = bj * kHistTile + r;
+                A[x] = (gi < M && w0 + w < FW) ? vf[static_cast<size_t>(gi) * FW + w0 + w] : 0ull;
+                B[x] = (gj < M && w0 + w < FW) ? vf[static_cast<size_t>(gj) * FW + w0 + w] : 0ull;
+            }
+            __syncthreads();
+            const int kw = min(kHistKW, FW - w0);
+            for (int w = 0; w < kw; w++) {
+                const unsigned long long a = A[ti * kHistKW + w];
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc[k] += __popcll(a & B[(tj0 + k) * kHistKW + w]);
+            }
         }
-        __syncthreads();
+        const long long gi = bi * kHistTile + ti;
 #pragma unroll
-        for (int w = 0; w < kHistKW; w++) {
-            const unsigned long long a = A[ti * kHistKW + w];
-#pragma unroll
-            for (int k = 0; k < 16; k++) acc[k] += __popcll(a & B[(tj0 + k) * kHistKW + w]);
+        for (int k = 0; k < 16; k++) {
+            const long long gj = bj * kHistTile + tj0 + k;
+            if (gi < M && gj < M && acc[k] > 0 && (bi != bj || gi <= gj)) atomicAdd(&myh[acc[k]], gi == gj ? 1u : 2u);
         }
-    }
-    const int gi = bi * kHistTile + ti;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int gj = bj * kHistTile + tj0 + k;
-        if (gi < M && gj < M && acc[k] > 0 && (bi != bj || gi <= gj)) atomicAdd(&hist[acc[k]], gi == gj ? 1u : 2u);
     }
     __syncthreads();
-    for (int v = threadIdx.x; v <= F; v += 256)
-        if (hist[v]) atomicAdd(&hist_g[v], static_cast<unsigned long long>(hist[v]));
+    for (int v = threadIdx.x; v <= F; v += 256) {
+        unsigned long long s = 0;
+        for (int r = 0; r < R; r++) s += hist[r * HS + v];
+        if (s) atomicAdd(&hist_g[v], s);
+    }
 }
 
 // numpy 2.x np.percentile(float32 array, p), "linear" (see oracle/mcgraph_oracle.c and
-// SURVEY.md App. A.4): every float op rounded explicitly (no contraction).
-__device__ float hist_order_stat(const unsigned long long *hist, int F, unsigned long long k)
+// SURVEY.md App. A.4): every float op rounded explicitly (no contraction).  The
+// histogram's cumulative counts are built in LDS; order statistics by binary search.
+__device__ float cum_order_stat(const unsigned long long *cum, int F, unsigned long long k)
 {
-    unsigned long long acc = 0;
-    for (int v = 1; v <= F; v++) {
-        acc += hist[v];
-        if (k < acc) return static_cast<float>(v);
+    // smallest v in [1, F] with cum[v] > k   (cum[v] = #values <= v)
+    int lo = 1, hi = F;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cum[mid] > k) hi = mid;
+        else lo = mid + 1;
     }
-    return static_cast<float>(F);
+    return static_cast<float>(lo);
 }
 
-__global__ void k_s4_thresholds(const unsigned long long *__restrict__ hist, int F, float *__restrict__ thr,
-                                int *__restrict__ is_int, int *__restrict__ nthr, int *__restrict__ status)
+// dynamic LDS: cum[F+1] (u64)
+__global__ __launch_bounds__(256) void k_s4_thresholds(const unsigned long long *__restrict__ hist, int F,
+                                                       float *__restrict__ thr, int *__restrict__ is_int,
+                                                       int *__restrict__ nthr, int *__restrict__ status)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    unsigned long long n = 0;
-    for (int v = 1; v <= F; v++) n += hist[v];
-    if (n == 0) {
-        *nthr = 0;
-        *status = MC_ERR_EMPTY_OBSERVERS;
-        return;
+    extern __shared__ unsigned long long cum[];
+    __shared__ unsigned long long part[256];
+    __shared__ float pval[20];
+    // cumulative histogram over v = 1..F (cum[0] = 0): per-thread chunks + serial fix-up
+    const int per = (F + 256) / 256;
+    const int v0 = threadIdx.x * per;
+    unsigned long long s = 0;
+    for (int v = v0; v < min(F + 1, v0 + per); v++) {
+        s += v == 0 ? 0ull : hist[v];
+        cum[v] = s;
     }
-    *status = MC_OK;
-    int k = 0;
-    const float nm1 = static_cast<float>(n - 1);
-    for (int p = 95; p > -5; p -= 5) {
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the 256 chunk sums by one wave
+        unsigned long long a0 = part[4 * threadIdx.x], a1 = part[4 * threadIdx.x + 1], a2 = part[4 * threadIdx.x + 2],
+                           a3 = part[4 * threadIdx.x + 3];
+        unsigned long long t = a0 + a1 + a2 + a3, x = t;
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_up(x, d, 64);
+            if (static_cast<int>(threadIdx.x) >= d) x += y;
+        }
+        unsigned long long ex = x - t;
+        part[4 * threadIdx.x] = ex;
+        part[4 * threadIdx.x + 1] = ex + a0;
+        part[4 * threadIdx.x + 2] = ex + a0 + a1;
+        part[4 * threadIdx.x + 3] = ex + a0 + a1 + a2;
+    }
+    __syncthreads();
+    for (int v = v0; v < min(F + 1, v0 + per); v++) cum[v] += part[threadIdx.x];
+    __syncthreads();
+    const unsigned long long n = cum[F];
+    if (threadIdx.x < 20 && n > 0) {  // one percentile per lane: p = 95, 90, ..., 0
+        const int p = 95 - 5 * static_cast<int>(threadIdx.x);
+        const float nm1 = static_cast<float>(n - 1);
         const float q = __fdiv_rn(static_cast<float>(p), 100.0f);
         const float vi = __fmul_rn(nm1, q);
         long long prev, next;
@@ -609,11 +759,25 @@ __global__ void k_s4_thresholds(const unsigned long long *__restrict__ hist, int
         const unsigned long long ip = prev < 0 ? n - 1 : static_cast<unsigned long long>(prev);
         const unsigned long long in = next < 0 ? n - 1 : static_cast<unsigned long long>(next);
         const float gamma = static_cast<float>(static_cast<double>(vi) - static_cast<double>(prev));
-        const float a = hist_order_stat(hist, F, ip);
-        const float bb = hist_order_stat(hist, F, in);
+        const float a = cum_order_stat(cum, F, ip);
+        const float bb = cum_order_stat(cum, F, in);
         const float diff = __fsub_rn(bb, a);
         float r = __fadd_rn(a, __fmul_rn(diff, gamma));
         if (gamma >= 0.5f) r = __fsub_rn(bb, __fmul_rn(diff, __fsub_rn(1.0f, gamma)));
+        pval[threadIdx.x] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (n == 0) {
+        *nthr = 0;
+        *status = MC_ERR_EMPTY_OBSERVERS;
+        return;
+    }
+    *status = MC_OK;
+    int k = 0;
+    for (int j = 0; j < 20; j++) {  // construction.py:88-95
+        const int p = 95 - 5 * j;
+        float r = pval[j];
         int isint = 0;
         if (r <= 1.0f) {
             if (p < 50) break;
@@ -658,89 +822,160 @@ __device__ __forceinline__ void uf_unite(int *parent, int a, int b)
     }
 }
 
-// K1: parent init + column counts (nodes that contain mask m)
-__global__ __launch_bounds__(256) void k6_prep(const int *__restrict__ dN, const int *__restrict__ n_off,
-                                               const int *__restrict__ n_len, const int *__restrict__ pool,
-                                               int *__restrict__ parent, int *__restrict__ colcnt)
+// K1: parent init + column counts (nodes that contain mask m), one thread per pool slot.
+__global__ __launch_bounds__(256) void k6_colcount(const int *__restrict__ dN, const int *__restrict__ dcap,
+                                                   const int *__restrict__ pool, const int *__restrict__ owner,
+                                                   int *__restrict__ parent, int *__restrict__ colcnt)
 {
-    const int N = *dN;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
-        parent[i] = i;
-        const int o = n_off[i], l = n_len[i];
-        for (int k = 0; k < l; k++) atomicAdd(&colcnt[pool[o + k]], 1);
+    const int N = *dN, cap = *dcap;
+    const int lim = max(N, cap);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < lim; e += gridDim.x * 256) {
+        if (e < N) parent[e] = e;
+        if (e < cap && owner[e] >= 0) atomicAdd(&colcnt[pool[e]], 1);
     }
 }
 
-// K3: column lists (transpose of the node-mask incidence); colcnt returns to zero.
-__global__ __launch_bounds__(256) void k6_colscatter(const int *__restrict__ dN, const int *__restrict__ n_off,
-                                                     const int *__restrict__ n_len, const int *__restrict__ pool,
-                                                     const int *__restrict__ coloff, int *__restrict__ colcnt,
-                                                     int *__restrict__ colnodes)
+__global__ __launch_bounds__(256) void k6_parent_init(const int *__restrict__ dN, int *__restrict__ parent)
 {
     const int N = *dN;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
-        const int o = n_off[i], l = n_len[i];
-        for (int k = 0; k < l; k++) {
-            const int m = pool[o + k];
-            const int pos = coloff[m] + atomicSub(&colcnt[m], 1) - 1;
-            colnodes[pos] = i;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) parent[i] = i;
+}
+
+// K3: column lists (transpose of the node-mask incidence); colcnt returns to zero.
+__global__ __launch_bounds__(256) void k6_colscatter(const int *__restrict__ dcap, const int *__restrict__ pool,
+                                                     const int *__restrict__ owner, const int *__restrict__ coloff,
+                                                     int *__restrict__ colcnt, int *__restrict__ colnodes)
+{
+    const int cap = *dcap;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < cap; e += gridDim.x * 256) {
+        const int a = owner[e];
+        if (a < 0) continue;
+        const int m = pool[e];
+        colnodes[coloff[m] + atomicSub(&colcnt[m], 1) - 1] = a;
+    }
+}
+
+// Column lists of the next level in place (iteration t >= 1): every column m keeps its
+// level-0 slot range [coloff[m], coloff[m+1]) and a current length collen[m]; its node
+// ids are mapped through the previous iteration's labels, sorted and deduplicated
+// (a column is the set of nodes contained by mask m).  label == nullptr: initialise
+// the lengths after the level-0 transpose.  Also resets the union-find parents.
+constexpr int kColStage = 2048;
+__device__ __forceinline__ int col_sort_unique(int *c, int n)
+{
+    for (int i = 1; i < n; i++) {
+        const int x = c[i];
+        int j = i - 1;
+        while (j >= 0 && c[j] > x) {
+            c[j + 1] = c[j];
+            j--;
+        }
+        c[j + 1] = x;
+    }
+    int u = 0;
+    for (int j = 0; j < n; j++)
+        if (u == 0 || c[j] != c[u - 1]) c[u++] = c[j];
+    return u;
+}
+
+// one wave per 64 columns
+__global__ __launch_bounds__(64) void k6_colupdate(int Mn, const int *__restrict__ dN, const int *__restrict__ coloff,
+                                                   int *__restrict__ collen, int *__restrict__ colnodes,
+                                                   const int *__restrict__ label, int *__restrict__ parent)
+{
+    __shared__ int stage[kColStage];
+    const int N = *dN;
+    const int nblk_cols = (Mn + 63) / 64;
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < N; i += gridDim.x * 64) parent[i] = i;
+    for (int blk = blockIdx.x; blk < nblk_cols; blk += gridDim.x) {
+        const int m0 = blk * 64, m1 = min(Mn, m0 + 64);
+        const int m = m0 + threadIdx.x;
+        if (!label) {
+            if (m < m1) collen[m] = coloff[m + 1] - coloff[m];
+            continue;
+        }
+        const int eb = coloff[m0], ee = coloff[m1];
+        if (ee - eb <= kColStage) {
+            for (int x = threadIdx.x; x < ee - eb; x += 64) stage[x] = colnodes[eb + x];
+            wave_sync();
+            if (m < m1) {
+                int *c = stage + coloff[m] - eb;
+                const int n = collen[m];
+                for (int j = 0; j < n; j++) c[j] = label[c[j]];
+                collen[m] = col_sort_unique(c, n);
+            }
+            wave_sync();
+            for (int x = threadIdx.x; x < ee - eb; x += 64) colnodes[eb + x] = stage[x];
+            wave_sync();
+        } else if (m < m1) {
+            int *c = colnodes + coloff[m];
+            const int n = collen[m];
+            for (int j = 0; j < n; j++) c[j] = label[c[j]];
+            collen[m] = col_sort_unique(c, n);
         }
     }
 }
 
+// Edge rule of update_graph (iterative_clustering.py:20-29) in float32, as torch evaluates
+// it: disconnect if O < thr; connect if fl32(S / fl32(O + 1e-7f)) >= fl32(ct); i != j.
 struct EdgeRule {
-    int thr_ceil;          // observer threshold as integer: O >= thr_ceil  <=>  !(fl32(O) < thr)
-    const int *smin;       // smin[o] = min S with fl32(S / fl32(o + 1e-7f)) >= fl32(ct)   (o in [0, F])
+    float thr;  // observer_num_threshold (np.float32 or the int 1) as float32
+    float ct;   // connect_threshold as float32
 };
 
-__device__ __forceinline__ bool edge_ok(int o, int s, const int *smin, int thr_ceil)
+__device__ __forceinline__ bool edge_ok(int o, int s, EdgeRule er)
 {
-    return o >= thr_ceil && s >= smin[o];
-}
-
-__device__ __forceinline__ int thr_to_ceil(float t)
-{
-    if (t != t) return INT_MIN;  // NaN: (O < NaN) is false, never disconnects
-    if (t <= -2147483648.0f) return INT_MIN;
-    if (t >= 2147483647.0f) return INT_MAX;
-    return static_cast<int>(ceilf(t));
+    const float of = static_cast<float>(o);
+    if (of < er.thr) return false;
+    const float rate = __fdiv_rn(static_cast<float>(s), __fadd_rn(of, 1e-7f));
+    return rate >= er.ct;
 }
 
 // K4: supporter counts by sparse expansion (Gustavson row-by-row C·Cᵀ), one wave per node a:
 //   S[a,b] = |C_a ∩ C_b| = #{m in C_a : b in col(m)}, accumulated in an LDS hash for b > a.
-// Only pairs with S >= 1 can pass the rate test when ct > 0 (smin[o] >= 1), so every
-// candidate edge is enumerated.  Then O[a,b] = popcount(VF_a & VF_b) and the edge rule
-// (iterative_clustering.py:20-29) decide; edges are merged with union-find at once.
-constexpr int kHashBits = 10, kHashSize = 1 << kHashBits, kHashMaxFill = (kHashSize * 3) / 4;
-constexpr int kPairWaves = 4;
+// Only pairs with S >= 1 can pass the rate test when ct > 0, so every candidate edge is
+// enumerated.  Then O[a,b] = popcount(VF_a & VF_b) and the edge rule decide; edges are
+// merged with union-find at once.  Loads are batched (independent gathers in flight
+// before use); only the hash slots actually used are scanned and reset.
+constexpr int kHashBits = 9, kHashSize = 1 << kHashBits, kHashMaxFill = (kHashSize * 3) / 4;
+constexpr int kPairWaves = 4, kPairBatch = 8, kTestBatch = 4;
+// Profiling ablations (timing-only builds, results wrong): 1 = no union-find,
+// 2 = no hash insert (expansion loads only), 3 = no partner test phase.
+#ifndef MC_ABLATE_PAIRS
+#define MC_ABLATE_PAIRS 0
+#endif
 
 __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, const int *__restrict__ n_off,
                                                 const int *__restrict__ n_len, const int *__restrict__ pool,
-                                                const int *__restrict__ coloff, const int *__restrict__ colnodes,
+                                                const int *__restrict__ coloff, const int *__restrict__ collen,
+                                                const int *__restrict__ colnodes,
                                                 const unsigned long long *__restrict__ nvf, int FW,
-                                                const float *__restrict__ thr, int t, const int *__restrict__ smin,
+                                                const float *__restrict__ thr, int t, float ctf,
                                                 int *__restrict__ parent, unsigned long long *__restrict__ edges,
                                                 int *__restrict__ ovf_list, int *__restrict__ ovf_n)
 {
     __shared__ int hkey[kPairWaves][kHashSize];
     __shared__ int hcnt[kPairWaves][kHashSize];
+    __shared__ short hused[kPairWaves][kHashMaxFill + 64];
     __shared__ int epre[kPairWaves][65];
     __shared__ int ebeg[kPairWaves][64];
     __shared__ int hfill[kPairWaves];
     __shared__ int hovf[kPairWaves];
 
     const int N = *dN;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int thr_ceil = thr_to_ceil(thr[t]);
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const EdgeRule er{thr[t], ctf};
     int *keys = hkey[wv];
     int *cnts = hcnt[wv];
+    short *used = hused[wv];
     unsigned long long nedges = 0;
 
+    if (blockIdx.x * kPairWaves >= N) return;  // uniform: nothing for this block
+    for (int s = lane; s < kHashSize; s += 64) {
+        keys[s] = -1;
+        cnts[s] = 0;
+    }
     for (int a = blockIdx.x * kPairWaves + wv; a < N; a += gridDim.x * kPairWaves) {
-        for (int s = lane; s < kHashSize; s += 64) {
-            keys[s] = -1;
-            cnts[s] = 0;
-        }
         if (lane == 0) {
             hfill[wv] = 0;
             hovf[wv] = 0;
@@ -753,7 +988,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
             if (e < L) {
                 const int m = pool[o + e];
                 beg = coloff[m];
-                len = coloff[m + 1] - beg;
+                len = collen[m];
             }
             const int incl = wave_incl_scan(len);
             epre[wv][lane + 1] = incl;
@@ -761,51 +996,97 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
             if (lane == 0) epre[wv][0] = 0;
             wave_sync();
             const int total = __shfl(incl, 63, 64);
-            for (int k = lane; k < total; k += 64) {
-                // entry holding expansion element k
-                int lo = 0, hi = 63;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (epre[wv][mid] <= k) lo = mid;
-                    else hi = mid - 1;
+            for (int k0 = 0; k0 < total; k0 += 64 * kPairBatch) {
+                int bn[kPairBatch];
+#pragma unroll
+                for (int r = 0; r < kPairBatch; r++) {
+                    const int k = k0 + r * 64 + lane;
+                    bn[r] = -1;
+                    if (k < total) {
+                        int lo = 0;  // largest entry with epre[lo] <= k
+#pragma unroll
+                        for (int st = 32; st >= 1; st >>= 1)
+                            if (epre[wv][lo + st] <= k) lo += st;
+                        bn[r] = colnodes[ebeg[wv][lo] + (k - epre[wv][lo])];
+                    }
                 }
-                const int bnode = colnodes[ebeg[wv][lo] + (k - epre[wv][lo])];
-                if (bnode <= a || hovf[wv]) continue;
-                unsigned h = (static_cast<unsigned>(bnode) * 2654435761u) >> (32 - kHashBits);
-                for (int probe = 0; probe < kHashSize; probe++) {
-                    int cur = keys[h];
-                    if (cur == -1) {
-                        cur = atomicCAS(&keys[h], -1, bnode);
+#pragma unroll
+                for (int r = 0; r < kPairBatch; r++) {
+                    const int bnode = bn[r];
+                    if (bnode <= a || hovf[wv]) continue;
+                    if (MC_ABLATE_PAIRS == 2) {
+                        asm volatile("" ::"v"(bnode));
+                        continue;
+                    }
+                    unsigned h = (static_cast<unsigned>(bnode) * 2654435761u) >> (32 - kHashBits);
+                    for (int probe = 0; probe < kHashSize; probe++) {
+                        int cur = keys[h];
                         if (cur == -1) {
-                            if (atomicAdd(&hfill[wv], 1) >= kHashMaxFill) hovf[wv] = 1;
-                            cur = bnode;
+                            cur = atomicCAS(&keys[h], -1, bnode);
+                            if (cur == -1) {
+                                const int f = atomicAdd(&hfill[wv], 1);
+                                if (f >= kHashMaxFill) hovf[wv] = 1;
+                                else used[f] = static_cast<short>(h);
+                                cur = bnode;
+                            }
                         }
+                        if (cur == bnode) {
+                            atomicAdd(&cnts[h], 1);
+                            break;
+                        }
+                        h = (h + 1) & (kHashSize - 1);
                     }
-                    if (cur == bnode) {
-                        atomicAdd(&cnts[h], 1);
-                        break;
-                    }
-                    h = (h + 1) & (kHashSize - 1);
                 }
             }
             wave_sync();
         }
         wave_sync();
-        if (hovf[wv]) {
-            // too many distinct partners for the LDS hash: redo this node in the overflow kernel
-            if (lane == 0) ovf_list[atomicAdd(ovf_n, 1)] = a;
-            continue;
-        }
+        const int fill = min(hfill[wv], kHashMaxFill);
+        const bool ovf = hovf[wv] != 0;
+        if (ovf && lane == 0) ovf_list[atomicAdd(ovf_n, 1)] = a;  // redo this node in the overflow kernel
         const unsigned long long *va = nvf + static_cast<size_t>(a) * FW;
-        for (int s = lane; s < kHashSize; s += 64) {
-            const int bnode = keys[s];
-            if (bnode < 0) continue;
-            const unsigned long long *vb = nvf + static_cast<size_t>(bnode) * FW;
-            int ob = 0;
-            for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
-            if (edge_ok(ob, cnts[s], smin, thr_ceil)) {
-                nedges++;
-                uf_unite(parent, a, bnode);
+        if (ovf) {
+            // clear every slot (inserted keys past the used list are not tracked)
+            for (int s = lane; s < kHashSize; s += 64) {
+                keys[s] = -1;
+                cnts[s] = 0;
+            }
+        } else if (MC_ABLATE_PAIRS != 3) {
+            for (int x0 = 0; x0 < fill; x0 += 64 * kTestBatch) {
+                int bn[kTestBatch], sc[kTestBatch], ob[kTestBatch];
+#pragma unroll
+                for (int r = 0; r < kTestBatch; r++) {
+                    const int x = x0 + r * 64 + lane;
+                    bn[r] = -1;
+                    sc[r] = 0;
+                    ob[r] = 0;
+                    if (x < fill) {
+                        const int sl = used[x];
+                        bn[r] = keys[sl];
+                        sc[r] = cnts[sl];
+                        keys[sl] = -1;
+                        cnts[sl] = 0;
+                    }
+                }
+                for (int w = 0; w < FW; w++) {
+                    const unsigned long long aw = va[w];
+#pragma unroll
+                    for (int r = 0; r < kTestBatch; r++)
+                        if (bn[r] >= 0) ob[r] += __popcll(aw & nvf[static_cast<size_t>(bn[r]) * FW + w]);
+                }
+#pragma unroll
+                for (int r = 0; r < kTestBatch; r++) {
+                    if (bn[r] >= 0 && edge_ok(ob[r], sc[r], er)) {
+                        nedges++;
+                        if (MC_ABLATE_PAIRS != 1) uf_unite(parent, a, bn[r]);
+                    }
+                }
+            }
+        } else {
+            for (int x = lane; x < fill; x += 64) {
+                const int sl = used[x];
+                keys[sl] = -1;
+                cnts[sl] = 0;
             }
         }
         wave_sync();
@@ -821,14 +1102,15 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
 __global__ __launch_bounds__(256) void k6_pairs_overflow(
     const int *__restrict__ ovf_list, const int *__restrict__ ovf_n, const int *__restrict__ n_off,
     const int *__restrict__ n_len, const int *__restrict__ pool, const int *__restrict__ coloff,
-    const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf, int FW,
-    const float *__restrict__ thr, int t, const int *__restrict__ smin, int *__restrict__ parent,
+    const int *__restrict__ collen, const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
+    int FW, const float *__restrict__ thr, int t, float ctf, int *__restrict__ parent,
     unsigned long long *__restrict__ edges, int *__restrict__ scratch, int *__restrict__ touched, int N0)
 {
     __shared__ int ntouch;
     __shared__ int ws[4];
     const int n = *ovf_n;
-    const int thr_ceil = thr_to_ceil(thr[t]);
+    if (n == 0) return;
+    const EdgeRule er{thr[t], ctf};
     int *scr = scratch + static_cast<size_t>(blockIdx.x) * N0;
     int *tl = touched + static_cast<size_t>(blockIdx.x) * N0;
     unsigned long long nedges = 0;
@@ -839,7 +1121,7 @@ __global__ __launch_bounds__(256) void k6_pairs_overflow(
         const int o = n_off[a], L = n_len[a];
         for (int e = 0; e < L; e++) {
             const int m = pool[o + e];
-            const int cb = coloff[m], ce = coloff[m + 1];
+            const int cb = coloff[m], ce = cb + collen[m];
             for (int k = cb + threadIdx.x; k < ce; k += 256) {
                 const int bnode = colnodes[k];
                 if (bnode <= a) continue;
@@ -856,7 +1138,7 @@ __global__ __launch_bounds__(256) void k6_pairs_overflow(
             const unsigned long long *vb = nvf + static_cast<size_t>(bnode) * FW;
             int ob = 0;
             for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
-            if (edge_ok(ob, s, smin, thr_ceil)) {
+            if (edge_ok(ob, s, er)) {
                 nedges++;
                 uf_unite(parent, a, bnode);
             }
@@ -875,7 +1157,7 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
 {
     __shared__ int ws[4];
     const int N = *dN;
-    const int thr_ceil = thr_to_ceil(thr[t]);
+    const float thr_f = thr[t];
     unsigned long long nedges = 0;
     const long long npairs = static_cast<long long>(N) * N;
     for (long long q = blockIdx.x * 256ll + threadIdx.x; q < npairs; q += gridDim.x * 256ll) {
@@ -883,7 +1165,7 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
         if (b <= a) continue;
         int ob = 0;
         for (int w = 0; w < FW; w++) ob += __popcll(nvf[static_cast<size_t>(a) * FW + w] & nvf[static_cast<size_t>(b) * FW + w]);
-        if (ob >= thr_ceil) {
+        if (!(static_cast<float>(ob) < thr_f)) {  // ct <= 0: every rate >= ct
             nedges++;
             uf_unite(parent, a, b);
         }
@@ -893,14 +1175,18 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
 }
 
 // K5: root of every node; flag roots (= smallest member of each component).
+// Also clears the row-length accumulator of the next level and the overflow count.
 __global__ __launch_bounds__(256) void k6_compress(const int *__restrict__ dN, int *__restrict__ parent,
-                                                   int *__restrict__ root, int *__restrict__ isroot)
+                                                   int *__restrict__ root, int *__restrict__ isroot,
+                                                   int *__restrict__ ublen, int *__restrict__ ovf_n)
 {
     const int N = *dN;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_n = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
         const int r = uf_find(parent, i);
         root[i] = r;
         isroot[i] = r == i ? 1 : 0;
+        ublen[i] = 0;
     }
 }
 
@@ -922,20 +1208,26 @@ __global__ __launch_bounds__(256) void k6_relabel(const int *__restrict__ dN, co
     }
 }
 
-__global__ __launch_bounds__(256) void k6_memscatter(const int *__restrict__ dN, const int *__restrict__ label,
+// K9: members of every new node (memcnt returns to zero) + object of every level-0 node.
+__global__ __launch_bounds__(256) void k6_memscatter(const int *__restrict__ dN, int N0, const int *__restrict__ label,
                                                      const int *__restrict__ memoff, int *__restrict__ memcnt,
-                                                     int *__restrict__ members)
+                                                     int *__restrict__ members, int *__restrict__ final_label)
 {
     const int N = *dN;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
-        const int k = label[i];
-        members[memoff[k] + atomicSub(&memcnt[k], 1) - 1] = i;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < max(N, N0); i += gridDim.x * 256) {
+        if (i < N) {
+            const int k = label[i];
+            members[memoff[k] + atomicSub(&memcnt[k], 1) - 1] = i;
+        }
+        if (i < N0) final_label[i] = label[final_label[i]];
     }
 }
 
 // K10: new node k = OR of its members (node.py:33-34): C row as a sorted unique union
 // (LDS bitmap over the members' [lo, hi] mask range), VF as OR of member VF words.
+// Rows are written at upper-bound offsets; the unused tail of every range gets owner -1.
 constexpr int kMergeBitWords = 8192;  // LDS bitmap: 262,144 mask ids
+constexpr int kMaxFW = 256;           // F <= 16384
 
 __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, const int *__restrict__ memoff,
                                                 const int *__restrict__ members, const int *__restrict__ n_off,
@@ -943,24 +1235,38 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
                                                 const unsigned long long *__restrict__ nvf, int FW,
                                                 const int *__restrict__ newoff, int *__restrict__ nn_off,
                                                 int *__restrict__ nn_len, int *__restrict__ npool,
-                                                unsigned long long *__restrict__ nnvf)
+                                                int *__restrict__ nowner, unsigned long long *__restrict__ nnvf)
 {
     __shared__ unsigned bits[kMergeBitWords];
+    __shared__ unsigned long long vacc[kMaxFW];
     __shared__ int ws[4];
     __shared__ int s_lo, s_hi;
     const int K = *dK;
     for (int k = blockIdx.x; k < K; k += gridDim.x) {
         const int mb = memoff[k], me = memoff[k + 1];
-        const int dst = newoff[k];
-        for (int w = threadIdx.x; w < FW; w += 256) {
-            unsigned long long acc = 0;
-            for (int q = mb; q < me; q++) acc |= nvf[static_cast<size_t>(members[q]) * FW + w];
-            nnvf[static_cast<size_t>(k) * FW + w] = acc;
+        const int dst = newoff[k], dend = newoff[k + 1];
+        if (me - mb == 1) {
+            for (int w = threadIdx.x; w < FW; w += 256)
+                nnvf[static_cast<size_t>(k) * FW + w] = nvf[static_cast<size_t>(members[mb]) * FW + w];
+        } else {
+            for (int w = threadIdx.x; w < FW; w += 256) vacc[w] = 0ull;
+            __syncthreads();
+            const int nmw = (me - mb) * FW;
+            for (int x = threadIdx.x; x < nmw; x += 256) {
+                const int q = mb + x / FW, w = x % FW;
+                const unsigned long long v = nvf[static_cast<size_t>(members[q]) * FW + w];
+                if (v) atomicOr(&vacc[w], v);
+            }
+            __syncthreads();
+            for (int w = threadIdx.x; w < FW; w += 256) nnvf[static_cast<size_t>(k) * FW + w] = vacc[w];
         }
         if (me - mb == 1) {
             const int i = members[mb];
             const int o = n_off[i], l = n_len[i];
-            for (int x = threadIdx.x; x < l; x += 256) npool[dst + x] = pool[o + x];
+            for (int x = threadIdx.x; x < l; x += 256) {
+                npool[dst + x] = pool[o + x];
+                nowner[dst + x] = k;
+            }
             if (threadIdx.x == 0) {
                 nn_off[k] = dst;
                 nn_len[k] = l;
@@ -983,6 +1289,7 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
         __syncthreads();
         const int lo = s_lo, hi = s_hi;
         if (hi < lo) {  // all members have empty rows
+            for (int x = dst + threadIdx.x; x < dend; x += 256) nowner[x] = -1;
             if (threadIdx.x == 0) {
                 nn_off[k] = dst;
                 nn_len[k] = 0;
@@ -1014,9 +1321,11 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
             while (v) {
                 const int bt = __ffs(v) - 1;
                 v &= v - 1;
+                nowner[pos] = k;
                 npool[pos++] = lo + (w << 5) + bt;
             }
         }
+        for (int x = dst + tot + threadIdx.x; x < dend; x += 256) nowner[x] = -1;
         if (threadIdx.x == 0) {
             nn_off[k] = dst;
             nn_len[k] = tot;
@@ -1025,27 +1334,125 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
     }
 }
 
-// K11: object of every level-0 node, composed over iterations.
-__global__ __launch_bounds__(256) void k6_maplevel(int N0, const int *__restrict__ label, int *__restrict__ final_label)
+// Start of S6: final_label = identity, level-0 size, edge counters.
+__global__ __launch_bounds__(256) void k6_init(int N0, int *__restrict__ final_label, const int *__restrict__ n0_src,
+                                               int n0_host, int *__restrict__ Nlev, int *__restrict__ cap0,
+                                               const int *__restrict__ cap_src, int cap_host,
+                                               unsigned long long *__restrict__ edges, int nthr)
 {
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < N0; i += gridDim.x * 256) final_label[i] = label[final_label[i]];
-}
-
-__global__ __launch_bounds__(256) void k6_iota(int n, int *__restrict__ out)
-{
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) out[i] = i;
+    const int i0 = blockIdx.x * 256 + threadIdx.x;
+    if (i0 == 0) {
+        *Nlev = n0_src ? *n0_src : n0_host;
+        *cap0 = cap_src ? *cap_src : cap_host;
+    }
+    for (int i = i0; i < nthr; i += gridDim.x * 256) edges[i] = 0ull;
+    for (int i = i0; i < N0; i += gridDim.x * 256) final_label[i] = i;
 }
 
 // ---------------------------------------------------------------------------------------------
 // Final point sets: union of the member masks' point sets (node.py:35) as per-object
 // bitmaps over each object's [min, max] point range, extracted in ascending order.
+// Graph path: one thread per scene point, objects of the point from its mask list,
+// wave-aggregated atomics (consecutive points of one object share a word).
 // ---------------------------------------------------------------------------------------------
+constexpr int kMaxObjPerPoint = 8;
+
+// object of every global mask (-1: under-segmented, not a node)
+__global__ __launch_bounds__(256) void k7_obj_of_mask(int M, const int *__restrict__ node_of_mask,
+                                                      const int *__restrict__ final_label, int *__restrict__ obj)
+{
+    for (int g = blockIdx.x * 256 + threadIdx.x; g < M; g += gridDim.x * 256) {
+        const int nd = node_of_mask[g];
+        obj[g] = nd < 0 ? -1 : final_label[nd];
+    }
+}
+
+// distinct objects of point p (from its mask list); returns count (-1 if more than cap)
+__device__ __forceinline__ int point_objects(const int *pt_off, const unsigned *pt_list, const int *frame_start,
+                                             const int *obj_of_mask, int p, int *objs)
+{
+    int n = 0;
+    const int b = pt_off[p], e = pt_off[p + 1];
+    for (int i = b; i < e; i++) {
+        const unsigned en = pt_list[i];
+        const int g = frame_start[en >> kLocalBits] + static_cast<int>(en & (kMaxMasksPerFrame - 1));
+        const int k = obj_of_mask[g];
+        if (k < 0) continue;
+        bool seen = false;
+        for (int j = 0; j < n; j++) seen |= objs[j] == k;
+        if (seen) continue;
+        if (n == kMaxObjPerPoint) return -1;
+        objs[n++] = k;
+    }
+    return n;
+}
+
+// mode 0: per-object min/max point; mode 1: set bits
+template <int MODE>
+__global__ __launch_bounds__(256) void k7p_points(int P, const int *__restrict__ pt_off, const unsigned *__restrict__ pt_list,
+                                                  const int *__restrict__ frame_start, const int *__restrict__ obj_of_mask,
+                                                  int *__restrict__ pmin,
+                                                  int *__restrict__ pmax, const int *__restrict__ woff,
+                                                  unsigned long long *__restrict__ bm, int *__restrict__ overflow)
+{
+    const int lane = lane_id();
+    const int p0 = (blockIdx.x * 256 + threadIdx.x) & ~63;
+    const int p = p0 + lane;
+    int objs[kMaxObjPerPoint];
+    int n = 0;
+    if (p < P) {
+        n = point_objects(pt_off, pt_list, frame_start, obj_of_mask, p, objs);
+        if (n < 0) {
+            atomicOr(overflow, 1);
+            n = 0;
+        }
+    }
+    int nmax = n;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, 64));
+    for (int j = 0; j < nmax; j++) {
+        int kk = j < n ? objs[j] : -1;
+        while (true) {
+            const unsigned long long act = __ballot(kk >= 0);
+            if (!act) break;
+            const int leader = __ffsll(static_cast<long long>(act)) - 1;
+            const int K = __shfl(kk, leader, 64);
+            const unsigned long long m = __ballot(kk == K);
+            if (MODE == 0) {
+                if (lane == leader) {
+                    const int lo = __ffsll(static_cast<long long>(m)) - 1;
+                    const int hi = 63 - __clzll(static_cast<long long>(m));
+                    atomicMin(&pmin[K], p0 + lo);
+                    atomicMax(&pmax[K], p0 + hi);
+                }
+            } else {
+                const int base = pmin[K];  // wave-uniform load
+                const long long off0 = static_cast<long long>(p0) - base;  // bit of lane 0
+                // lanes of m span at most two 64-bit words
+                const long long wlo = (off0 + (__ffsll(static_cast<long long>(m)) - 1)) >> 6;
+                const long long whi = (off0 + (63 - __clzll(static_cast<long long>(m)))) >> 6;
+                if (lane == leader) {
+                    for (long long w = wlo; w <= whi; w++) {
+                        const long long sh = off0 - 64 * w;  // bit of lane l in word w = sh + l
+                        unsigned long long bits;
+                        if (sh >= 0) bits = sh >= 64 ? 0ull : (m << sh);
+                        else bits = -sh >= 64 ? 0ull : (m >> (-sh));
+                        if (bits) atomicOr(&bm[woff[K] + w], bits);
+                    }
+                }
+            }
+            if (kk == K) kk = -1;
+        }
+    }
+}
+
+// general path (arbitrary level-0 nodes): wave per level-0 node
 __global__ __launch_bounds__(256) void k7_minmax(int N0, const int *__restrict__ final_label,
                                                  const int *__restrict__ ptoff, const int *__restrict__ ptlen,
                                                  const int *__restrict__ pts, int *__restrict__ pmin,
                                                  int *__restrict__ pmax)
 {
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_id();
     for (int i = (blockIdx.x * 256 + threadIdx.x) >> 6; i < N0; i += gridDim.x * 4) {
         const int k = final_label[i];
         const int o = ptoff[i], l = ptlen[i];
@@ -1067,30 +1474,50 @@ __global__ __launch_bounds__(256) void k7_minmax(int N0, const int *__restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void k7_words(const int *__restrict__ dK, const int *__restrict__ pmin,
-                                                const int *__restrict__ pmax, int *__restrict__ nwords)
-{
-    const int K = *dK;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256)
-        nwords[k] = pmax[k] >= pmin[k] ? ((pmax[k] - pmin[k]) >> 6) + 1 : 0;
-}
-
 __global__ __launch_bounds__(256) void k7_setbits(int N0, const int *__restrict__ final_label,
                                                   const int *__restrict__ ptoff, const int *__restrict__ ptlen,
                                                   const int *__restrict__ pts, const int *__restrict__ pmin,
                                                   const int *__restrict__ woff, unsigned long long *__restrict__ bm)
 {
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_id();
     for (int i = (blockIdx.x * 256 + threadIdx.x) >> 6; i < N0; i += gridDim.x * 4) {
         const int k = final_label[i];
         const int o = ptoff[i], l = ptlen[i];
         const int base = pmin[k];
         unsigned long long *row = bm + woff[k];
-        for (int x = lane; x < l; x += 64) {
-            const int p = pts[o + x] - base;
-            atomicOr(&row[p >> 6], 1ull << (p & 63));
+        for (int x0 = 0; x0 < l; x0 += 64) {
+            const int x = x0 + lane;
+            int w = -1;
+            unsigned long long bit = 0;
+            if (x < l) {
+                const int q = pts[o + x] - base;
+                w = q >> 6;
+                bit = 1ull << (q & 63);
+            }
+            // combine lanes that hit the same word
+            while (true) {
+                const unsigned long long act = __ballot(w >= 0);
+                if (!act) break;
+                const int leader = __ffsll(static_cast<long long>(act)) - 1;
+                const int W = __shfl(w, leader, 64);
+                unsigned long long v = (w == W) ? bit : 0ull;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, 64);
+                if (lane == leader) atomicOr(&row[W], v);
+                if (w == W) w = -1;
+            }
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k7_words(const int *__restrict__ dK, const int *__restrict__ pmin,
+                                                const int *__restrict__ pmax, int *__restrict__ nwords,
+                                                int *__restrict__ stat_k)
+{
+    const int K = *dK;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *stat_k = K;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256)
+        nwords[k] = pmax[k] >= pmin[k] ? ((pmax[k] - pmin[k]) >> 6) + 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void k7_count(const int *__restrict__ dK, const int *__restrict__ woff,
@@ -1134,9 +1561,13 @@ __global__ __launch_bounds__(256) void k7_extract(const int *__restrict__ dK, co
     }
 }
 
-__global__ void k_fill_i32(int *p, int n, int v)
+// pmin/pmax reset for up to n objects + zero a word range [0, *dwords) (grid-stride)
+__global__ __launch_bounds__(256) void k7_reset(int n, int *__restrict__ pmin, int *__restrict__ pmax)
 {
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = v;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        pmin[i] = INT_MAX;
+        pmax[i] = -1;
+    }
 }
 
 __global__ void k_copy_i32(const int *src, int *dst) { *dst = *src; }
