@@ -165,6 +165,15 @@ def main():
                 "frac": round(achieved / INT8_MFMA_PEAK_TOPS, 4), "traffic": None}
     roof["kernel"] = dominant
     roof["avg_launch_ms"] = round(avg_s * 1e3, 5)
+    roof["algorithmic_per_launch"] = per_launch
+    # HBM bytes per launch of the same kernel group from the committed rocprofv3 PMC passes
+    # (scripts/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)
+    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if bound == "hbm" and os.path.exists(pmc_path):
+        g = json.load(open(pmc_path)).get("groups", {}).get(dominant)
+        if g:
+            roof["traffic"] = round(g["bytes_per_launch"], 0)
+            roof["traffic_source"] = "profiles/pmc_traffic.json"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

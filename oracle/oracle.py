@@ -38,6 +38,82 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+class BpParams(ctypes.Structure):
+    """orc_bp_params (s1_oracle.c); defaults = the reference's constants
+    (utils/mask_backprojection.py:8-14,38; utils/geometry.py:10,16,22)."""
+    _fields_ = [("depth_trunc", ctypes.c_double), ("voxel_size", ctypes.c_double),
+                ("dbscan_eps", ctypes.c_double), ("component_min_fraction", ctypes.c_double),
+                ("sor_std_ratio", ctypes.c_double), ("ball_radius", ctypes.c_double),
+                ("coverage_threshold", ctypes.c_double), ("dbscan_min_points", ctypes.c_int32),
+                ("sor_neighbors", ctypes.c_int32), ("ball_k", ctypes.c_int32), ("few_points", ctypes.c_int32)]
+
+    @classmethod
+    def default(cls, **kw):
+        p = cls(20.0, 0.01, 0.04, 0.2, 2.0, 0.01, 0.3, 4, 20, 20, 25)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
+S1_STATS = ["id", "npix", "nvox", "ndbscan", "nsor", "ncand", "ncovered", "nneighbors", "kept"]
+
+
+def s1_frame(scene_f32, depth, seg, K, pose, params: BpParams | None = None):
+    """turn_mask_to_point (utils/mask_backprojection.py:70-151) for one frame.
+    Returns (labels int32 [n], off int64 [n+1], pts int32, stats int32 [n_cand, 9]).
+    Raises IndexError where the reference does (a depth pixel == DEPTH_TRUNC)."""
+    L = lib()
+    prm = params or BpParams.default()
+    scene = np.ascontiguousarray(scene_f32, np.float32).reshape(-1, 3)
+    depth = np.ascontiguousarray(depth, np.float32)
+    seg = np.ascontiguousarray(seg, np.uint8)
+    H, W = depth.shape
+    K = np.ascontiguousarray(K, np.float64).reshape(4)
+    T = np.ascontiguousarray(pose, np.float64).reshape(16)
+    labels = np.zeros(256, np.int32)
+    off = np.zeros(257, np.int64)
+    stats = np.zeros((256, len(S1_STATS)), np.int32)
+    need = ctypes.c_int64()
+    ncand = ctypes.c_int32()
+    cap = 1 << 16
+    while True:
+        pts = np.zeros(cap, np.int32)
+        n = L.orc_s1_frame(len(scene), scene.reshape(-1), H, W, depth.reshape(-1), seg.reshape(-1), K, T,
+                           ctypes.byref(prm), labels, off, pts, cap, ctypes.byref(need), stats.reshape(-1),
+                           ctypes.byref(ncand))
+        if n == -2:
+            cap = int(need.value)
+            continue
+        break
+    if n == -1:
+        raise IndexError("depth pixel equal to DEPTH_TRUNC (utils/mask_backprojection.py:100)")
+    return labels[:n].copy(), off[:n + 1].copy(), pts[:off[n]].copy(), stats[:ncand.value].copy()
+
+
+def s1_scene(frames, params: BpParams | None = None, timings: dict | None = None):
+    """All frames of a SceneFrames (maskclustering_amd.synthetic_frames) ->
+    the flat mask CSR the graph stages consume (mask_col, mask_label, mask_off,
+    mask_pts) plus the per-candidate stats with the frame column prepended."""
+    scene = np.asarray(frames.scene_points, np.float64).astype(np.float32)  # construction.py:37
+    cols, labs, offs, chunks, stats = [], [], [0], [], []
+    t0 = time.perf_counter()
+    for f in range(frames.num_frames):
+        lab, off, pts, st = s1_frame(scene, frames.depth[f], frames.seg[f], frames.intrinsics[f], frames.poses[f],
+                                     params)
+        for k in range(len(lab)):
+            cols.append(f)
+            labs.append(int(lab[k]))
+            chunks.append(pts[off[k]:off[k + 1]])
+            offs.append(offs[-1] + int(off[k + 1] - off[k]))
+        stats.append(np.concatenate([np.full((len(st), 1), f, np.int32), st], axis=1))
+    if timings is not None:
+        timings["s1"] = time.perf_counter() - t0
+    return dict(mask_col=np.asarray(cols, np.int32), mask_label=np.asarray(labs, np.int32),
+                mask_off=np.asarray(offs, np.int64),
+                mask_pts=np.concatenate(chunks).astype(np.int32) if chunks else np.zeros(0, np.int32),
+                stats=np.concatenate(stats) if stats else np.zeros((0, len(S1_STATS) + 1), np.int32))
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -59,6 +135,11 @@ def lib():
         L.orc_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p, ctypes.c_int, _f32p,
                                   ctypes.c_double, _i32p, _i32p, _i32p, _u8p, _u8p]
         L.orc_num_threads.restype = ctypes.c_int
+        _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        L.orc_s1_frame.restype = ctypes.c_int
+        L.orc_s1_frame.argtypes = [ctypes.c_int64, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _u8p, _f64p, _f64p,
+                                   ctypes.POINTER(BpParams), _i32p, _i64p, _i32p, ctypes.c_int64,
+                                   ctypes.POINTER(ctypes.c_int64), _i32p, ctypes.POINTER(ctypes.c_int32)]
         _lib = L
     return _lib
 
