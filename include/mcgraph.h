@@ -14,6 +14,9 @@
  *   graph/iterative_clustering.py:13 update_graph           -> mc_cluster_run (pair counts + edge rule)
  *   graph/iterative_clustering.py:5  cluster_into_new_nodes -> mc_cluster_run (components)
  *   graph/node.py:24           Node.create_node_from_list   -> mc_cluster_run (on-device merge)
+ *   utils/mask_backprojection.py:70 turn_mask_to_point      -> mc_backproject (S1)
+ *   utils/mask_backprojection.py:154 frame_backprojection   -> mc_backproject + mc_backproject_get_masks
+ *   utils/geometry.py:9        denoise                      -> mc_backproject (S1 denoise)
  *
  * Conventions
  *   - Every call returns 0 (MC_OK) or an MC_ERR_* code; mc_ctx_last_error()
@@ -75,6 +78,34 @@ typedef struct {
     int64_t num_object_masks;  /* sum over objects of |mask_list|     */
 } mc_cluster_info;
 
+/* S1 constants (utils/mask_backprojection.py:8-14,38; utils/geometry.py:10,16,22).
+ * Same layout as the oracle's orc_bp_params.  mc_bp_params_default() fills
+ * the reference's values. */
+typedef struct {
+    double depth_trunc;            /* DEPTH_TRUNC = 20                      */
+    double voxel_size;             /* DISTANCE_THRESHOLD = 0.01 (voxel)     */
+    double dbscan_eps;             /* 0.04                                  */
+    double component_min_fraction; /* 0.2                                   */
+    double sor_std_ratio;          /* 2.0                                   */
+    double ball_radius;            /* DISTANCE_THRESHOLD (as float32)       */
+    double coverage_threshold;     /* COVERAGE_THRESHOLD = 0.3              */
+    int32_t dbscan_min_points;     /* 4                                     */
+    int32_t sor_neighbors;         /* 20 (<= 32)                            */
+    int32_t ball_k;                /* K = 20 (<= 32)                        */
+    int32_t few_points;            /* FEW_POINTS_THRESHOLD = 25             */
+} mc_bp_params;
+
+typedef struct {
+    int32_t num_frames;
+    int32_t num_candidates;        /* (frame, id) with >= few_points pixels  */
+    int32_t num_masks;             /* kept masks (coverage >= threshold)     */
+    int32_t error_frame;           /* -1, or the first frame that raises     */
+    int64_t num_mask_points;       /* sum of the kept masks' set sizes       */
+} mc_bp_info;
+
+#define MC_BP_NSTAT 10  /* per candidate: frame, id, pixels, voxels, after DBSCAN filter,
+                           after outlier removal, -1, covered, neighbours, kept */
+
 /* ---- context ------------------------------------------------------------ */
 int mc_ctx_create(int device, mc_ctx **out);
 void mc_ctx_destroy(mc_ctx *ctx);
@@ -96,6 +127,30 @@ int mc_ctx_reset_kernel_times(mc_ctx *ctx);
 int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int32_t num_masks_in,
                        const int32_t *mask_col, const int32_t *mask_label, const int64_t *mask_off,
                        const int32_t *mask_pts, int pts_on_device);
+
+/* ---- S1: per-frame mask back-projection ---------------------------------
+ * utils/mask_backprojection.py:70-151 (turn_mask_to_point) for a batch of
+ * frames: build_point_in_mask_matrix's per-frame loop (construction.py:46-49)
+ * without the host round trips.  Scene points: float32 [P,3] (the reference
+ * casts to float32 at construction.py:37).  depth float32 [F,H,W] metres,
+ * seg uint8 [F,H,W] aligned with depth, intrinsics [F,4] = fx, fy, cx, cy,
+ * poses [F,16] row-major camera-to-world; host pointers, or device pointers
+ * when on_device != 0.  A frame with an inf pose yields no masks (:73-74); a
+ * depth pixel equal to depth_trunc in a frame with mask ids fails the call
+ * with MC_ERR_INVALID (the reference raises IndexError at :100).          */
+void mc_bp_params_default(mc_bp_params *p);
+int mc_scene_set_points(mc_ctx *ctx, int64_t num_points, const float *xyz, int on_device);
+int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
+                   const uint8_t *seg, const double *intrinsics, const double *poses, int on_device,
+                   const mc_bp_params *params);
+int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info);
+/* kept masks in frame order then id order: mask_col (frame index), mask_label
+ * (id), mask_off [M+1], mask_pts = sorted unique scene ids (mask_info[id], :148) */
+int mc_backproject_get_masks(mc_ctx *ctx, int32_t *mask_col, int32_t *mask_label, int64_t *mask_off,
+                             int32_t *mask_pts);
+int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats /* num_candidates * MC_BP_NSTAT */);
+/* the back-projected masks become the graph input (as mc_scene_set_masks, device-resident) */
+int mc_scene_use_backprojection(mc_ctx *ctx);
 
 /* ---- S2-S5: graph construction ------------------------------------------ */
 int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params);

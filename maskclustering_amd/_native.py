@@ -32,7 +32,12 @@ EXPORTED = [
     "mc_nodes_set",
     "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_partition",
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
+    "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
+    "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
 ]
+
+MC_BP_NSTAT = 10
+BP_STATS = ["frame", "id", "npix", "nvox", "ndbscan", "nsor", "ncand", "ncovered", "nneighbors", "kept"]
 
 
 class McError(RuntimeError):
@@ -59,6 +64,20 @@ class ClusterInfo(ctypes.Structure):
                 ("num_nodes0", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("num_object_points", ctypes.c_int64), ("num_object_contained", ctypes.c_int64),
                 ("num_object_masks", ctypes.c_int64)]
+
+
+class BpParams(ctypes.Structure):
+    """mc_bp_params: the S1 constants (utils/mask_backprojection.py:8-14,38; utils/geometry.py:10,16,22)."""
+    _fields_ = [("depth_trunc", ctypes.c_double), ("voxel_size", ctypes.c_double),
+                ("dbscan_eps", ctypes.c_double), ("component_min_fraction", ctypes.c_double),
+                ("sor_std_ratio", ctypes.c_double), ("ball_radius", ctypes.c_double),
+                ("coverage_threshold", ctypes.c_double), ("dbscan_min_points", ctypes.c_int32),
+                ("sor_neighbors", ctypes.c_int32), ("ball_k", ctypes.c_int32), ("few_points", ctypes.c_int32)]
+
+
+class BpInfo(ctypes.Structure):
+    _fields_ = [("num_frames", ctypes.c_int32), ("num_candidates", ctypes.c_int32), ("num_masks", ctypes.c_int32),
+                ("error_frame", ctypes.c_int32), ("num_mask_points", ctypes.c_int64)]
 
 
 _lib = None
@@ -107,6 +126,13 @@ def load():
         "mc_cluster_get_edge_counts": (ctypes.c_int, [vp, vp]),
         "mc_cluster_get_final_labels": (ctypes.c_int, [vp, vp]),
         "mc_cluster_get_objects": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "mc_bp_params_default": (None, [P(BpParams)]),
+        "mc_scene_set_points": (ctypes.c_int, [vp, i64, vp, ctypes.c_int]),
+        "mc_backproject": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, ctypes.c_int, P(BpParams)]),
+        "mc_backproject_get_info": (ctypes.c_int, [vp, P(BpInfo)]),
+        "mc_backproject_get_masks": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        "mc_backproject_get_candidates": (ctypes.c_int, [vp, vp]),
+        "mc_scene_use_backprojection": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -316,3 +342,71 @@ class Context:
                                                   _ptr(pt_idx), _ptr(m_off), _ptr(m_idx)))
         return dict(vf_bits=vf[:K, :FW], c_off=c_off, c_idx=c_idx[:c_off[-1]], pt_off=pt_off,
                     pt_idx=pt_idx[:pt_off[-1]], mask_off=m_off, mask_idx=m_idx[:m_off[-1]])
+
+
+def bp_params(**kw) -> BpParams:
+    """The reference's S1 constants, with optional overrides."""
+    p = BpParams()
+    load().mc_bp_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _bp_methods():
+    def set_points(self, xyz=None, device_ptr=None, num_points=None):
+        """Scene points as float32 [P,3] (construction.py:37 casts them to float32)."""
+        if device_ptr is not None:
+            self._check(self.L.mc_scene_set_points(self.h, int(num_points), ctypes.c_void_p(int(device_ptr)), 1))
+            return
+        pts = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        self._check(self.L.mc_scene_set_points(self.h, len(pts), _ptr(pts), 0))
+
+    def backproject(self, depth, seg, intrinsics, poses, params: BpParams | None = None, device_ptrs=None,
+                    shape=None):
+        """S1 for a batch of frames: depth float32 [F,H,W], seg uint8 [F,H,W], intrinsics [F,4],
+        poses [F,4,4].  device_ptrs = (depth, seg, intrinsics, poses) device pointers with shape=(F,H,W)."""
+        prm = params or bp_params()
+        if device_ptrs is not None:
+            F, H, W = shape
+            d, s_, k, t = (ctypes.c_void_p(int(x)) for x in device_ptrs)
+            self._check(self.L.mc_backproject(self.h, F, H, W, d, s_, k, t, 1, ctypes.byref(prm)))
+            return
+        depth = np.ascontiguousarray(depth, np.float32)
+        seg = np.ascontiguousarray(seg, np.uint8)
+        F, H, W = depth.shape
+        assert seg.shape == depth.shape
+        K = np.ascontiguousarray(intrinsics, np.float64).reshape(F, 4)
+        T = np.ascontiguousarray(poses, np.float64).reshape(F, 16)
+        self._check(self.L.mc_backproject(self.h, F, H, W, _ptr(depth), _ptr(seg), _ptr(K), _ptr(T), 0,
+                                          ctypes.byref(prm)))
+
+    def bp_info(self) -> BpInfo:
+        info = BpInfo()
+        self._check(self.L.mc_backproject_get_info(self.h, ctypes.byref(info)))
+        return info
+
+    def bp_masks(self):
+        info = self.bp_info()
+        M = info.num_masks
+        col = np.zeros(max(M, 1), np.int32)
+        lab = np.zeros(max(M, 1), np.int32)
+        off = np.zeros(M + 1, np.int64)
+        pts = np.zeros(max(info.num_mask_points, 1), np.int32)
+        self._check(self.L.mc_backproject_get_masks(self.h, _ptr(col), _ptr(lab), _ptr(off), _ptr(pts)))
+        return col[:M], lab[:M], off, pts[:info.num_mask_points]
+
+    def bp_candidates(self):
+        n = self.bp_info().num_candidates
+        st = np.zeros((max(n, 1), MC_BP_NSTAT), np.int32)
+        self._check(self.L.mc_backproject_get_candidates(self.h, _ptr(st)))
+        return st[:n]
+
+    def use_backprojection(self):
+        self._check(self.L.mc_scene_use_backprojection(self.h))
+
+    for f in (set_points, backproject, bp_info, bp_masks, bp_candidates, use_backprojection):
+        setattr(Context, f.__name__, f)
+
+
+_bp_methods()

@@ -9,6 +9,7 @@
 
 #include "mc_internal.hpp"
 #include "mc_kernels.inl"
+#include "mc_bp_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -78,6 +79,27 @@ struct mc_ctx {
     const unsigned long long *fin_vf = nullptr;
     int K = 0;
     int64_t npts = 0;
+
+    // ---- S1 back-projection ----
+    int64_t P_scene = 0;
+    bool have_points = false, have_bp = false;
+    float grid_radius = -1.f;  // scene grid built for this ball radius
+    unsigned gnb = 0;
+    DevBuf d_scene, d_gcnt, d_gstart, d_gbkt, d_gcellk, d_gpts, d_gidx, d_gcell, d_gscan_tmp;
+    DevBuf d_in_depth, d_in_seg, d_in_intr, d_in_pose;
+    DevBuf d_band, d_present, d_fflags, d_cand, d_npix, d_csidx, d_poff, d_slot_of, d_bpstat;
+    DevBuf d_slot_frame, d_slot_id, d_slot_np, d_slot_pix, d_slot_nv, d_slot_m, d_slot_ns, d_slot_box, d_slot_nn,
+        d_slot_toff, d_slot_cov;
+    DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
+        d_blist, d_ncnt, d_par, d_droot, d_rnk, d_lab, d_ccnt, d_ssidx, d_avg, d_qpts;
+    DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
+    size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
+    int bp_f_cap = 0;      // frame capacity of the per-batch arrays
+    int bp_bm_blocks = 0;
+    int bp_F = 0, bp_err_frame = -1;
+    int64_t bp_nnz = 0;
+    std::vector<int32_t> bp_col, bp_label, bp_stats;
+    std::vector<int64_t> bp_off;
 };
 
 namespace {
@@ -181,6 +203,19 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_node_of_mask, &ctx->d_ownA, &ctx->d_ownB, &ctx->d_cap, &ctx->d_obj_of_mask,
                       &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen};
     for (DevBuf *b : bufs) b->release();
+    DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
+                         &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg,
+                         &ctx->d_in_intr, &ctx->d_in_pose, &ctx->d_band, &ctx->d_present, &ctx->d_fflags,
+                         &ctx->d_cand, &ctx->d_npix, &ctx->d_csidx, &ctx->d_poff, &ctx->d_slot_of, &ctx->d_bpstat,
+                         &ctx->d_slot_frame, &ctx->d_slot_id, &ctx->d_slot_np, &ctx->d_slot_pix, &ctx->d_slot_nv,
+                         &ctx->d_slot_m, &ctx->d_slot_ns, &ctx->d_slot_box, &ctx->d_slot_nn, &ctx->d_slot_toff,
+                         &ctx->d_slot_cov, &ctx->d_pix_list, &ctx->d_hkey, &ctx->d_hvid, &ctx->d_hfirst,
+                         &ctx->d_vox_entry, &ctx->d_acc, &ctx->d_vpts, &ctx->d_pcell, &ctx->d_pbkt, &ctx->d_bcnt,
+                         &ctx->d_bstart, &ctx->d_blist, &ctx->d_ncnt, &ctx->d_par, &ctx->d_droot, &ctx->d_rnk,
+                         &ctx->d_lab, &ctx->d_ccnt, &ctx->d_ssidx, &ctx->d_avg, &ctx->d_qpts, &ctx->d_bpbm, &ctx->d_tmp,
+                         &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
+                         &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts};
+    for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1073,6 +1108,414 @@ int mc_cluster_get_objects(mc_ctx *ctx, uint64_t *vf_bits, int64_t *c_off, int32
                 for (int i = 0; i < ctx->N0; i++) mask_idx[cnt[fl[i]]++] = i;
         }
     });
+}
+
+// ---------------------------------------------------------------------------------------------
+// S1 back-projection
+// ---------------------------------------------------------------------------------------------
+__global__ void k_fill_u32(unsigned *p, size_t n, unsigned v)
+{
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += static_cast<size_t>(gridDim.x) * 256) p[i] = v;
+}
+
+}  // extern "C"
+
+namespace {
+
+void fill_u32(hipStream_t s, void *p, size_t n, unsigned v)
+{
+    if (n) hipLaunchKernelGGL(k_fill_u32, grid_for(static_cast<int64_t>(n)), dim3(256), 0, s, static_cast<unsigned *>(p), n, v);
+}
+
+// grow a device buffer, keeping its first `used` bytes
+void grow_keep(DevBuf &b, size_t bytes, size_t used, hipStream_t s)
+{
+    if (bytes <= b.bytes) return;
+    DevBuf nb;
+    nb.reserve(bytes + bytes / 2);
+    if (used) MC_HIP(hipMemcpyAsync(nb.ptr, b.ptr, used, hipMemcpyDeviceToDevice, s));
+    MC_HIP(hipStreamSynchronize(s));
+    b.release();
+    b = nb;
+    nb.ptr = nullptr;
+    nb.bytes = 0;
+}
+
+enum BpStat : int { BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ, BS_COUNT };
+
+// (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
+void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
+{
+    const size_t px = static_cast<size_t>(fb) * H * W + 1;
+    const size_t slots = static_cast<size_t>(fb) * 256 + 1;
+    ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * 256 * 4);
+    ctx->d_present.reserve(static_cast<size_t>(fb) * 8 * 4);
+    ctx->d_fflags.reserve(static_cast<size_t>(fb) * 4);
+    ctx->d_cand.reserve(slots * 4);
+    ctx->d_npix.reserve(slots * 4);
+    ctx->d_csidx.reserve((slots + 1) * 4);
+    ctx->d_poff.reserve((slots + 1) * 4);
+    ctx->d_slot_of.reserve(slots * 4);
+    ctx->d_bpstat.reserve(BS_COUNT * 4);
+    DevBuf *sl[] = {&ctx->d_slot_frame, &ctx->d_slot_id, &ctx->d_slot_np, &ctx->d_slot_pix, &ctx->d_slot_nv,
+                    &ctx->d_slot_m,     &ctx->d_slot_ns, &ctx->d_slot_nn, &ctx->d_slot_toff, &ctx->d_slot_cov,
+                    &ctx->d_kflag,      &ctx->d_ksize};
+    for (DevBuf *b : sl) b->reserve(slots * 4);
+    ctx->d_midx.reserve((slots + 1) * 4);
+    ctx->d_moff.reserve((slots + 1) * 4);
+    ctx->d_slot_box.reserve(slots * 6 * 4);
+    if (ctx->bp_px_cap < px) {
+        ctx->d_pix_list.reserve(px * 4);
+        ctx->d_hkey.reserve(2 * px * 8);
+        ctx->d_hvid.reserve(2 * px * 4);
+        ctx->d_hfirst.reserve(2 * px * 4);
+        fill_u32(s, ctx->d_hkey.ptr, 4 * px, 0xFFFFFFFFu);  // empty key, kept empty by k_bp_voxel
+        fill_u32(s, ctx->d_hvid.ptr, 2 * px, 0xFFFFFFFFu);  // -1
+        fill_u32(s, ctx->d_hfirst.ptr, 2 * px, 0x7FFFFFFFu);  // INT_MAX
+        ctx->d_vox_entry.reserve(px * 4);
+        ctx->d_acc.reserve(px * 4 * 8);
+        ctx->d_vpts.reserve(px * 3 * 8);
+        ctx->d_pcell.reserve(px * 8);
+        ctx->d_pbkt.reserve(px * 4);
+        ctx->d_bcnt.reserve(2 * px * 4);
+        fill_u32(s, ctx->d_bcnt.ptr, 2 * px, 0u);  // kept zero by k_bp_denoise
+        ctx->d_bstart.reserve((2 * px + slots + 1) * 4);
+        ctx->d_blist.reserve(px * 4);
+        ctx->d_ncnt.reserve(px * 4);
+        ctx->d_par.reserve(px * 4);
+        ctx->d_droot.reserve(px * 4);
+        ctx->d_rnk.reserve(px * 4);
+        ctx->d_lab.reserve(px * 4);
+        ctx->d_ccnt.reserve((px + slots + 1) * 4);
+        ctx->d_ssidx.reserve(px * 4);
+        ctx->d_avg.reserve(px * 8);
+        ctx->d_qpts.reserve(px * 3 * 4);
+        ctx->bp_px_cap = px;
+    }
+    ctx->bp_f_cap = std::max(ctx->bp_f_cap, fb);
+}
+
+void bp_build_grid(mc_ctx *ctx, float radius, hipStream_t s)
+{
+    const int P = static_cast<int>(ctx->P_scene);
+    const float inv = 1.0f / (2.0f * radius);
+    const unsigned nb = static_cast<unsigned>(std::max(2 * P, 16));
+    ctx->gnb = nb;
+    const bool fresh = ctx->d_gcnt.bytes < (nb + 1) * 4ull;
+    ctx->d_gcnt.reserve((nb + 1) * 4ull);
+    if (fresh) MC_HIP(hipMemsetAsync(ctx->d_gcnt.ptr, 0, ctx->d_gcnt.bytes, s));  // kept zero by k_grid_scatter
+    ctx->d_gstart.reserve((nb + 2) * 4ull);
+    ctx->d_gbkt.reserve((P + 1) * 4ull);
+    ctx->d_gcellk.reserve((P + 1) * 8ull);
+    ctx->d_gpts.reserve((P + 1) * 16ull);
+    ctx->d_gidx.reserve((P + 1) * 4ull);
+    ctx->d_gcell.reserve((P + 1) * 8ull);
+    ctx->d_gscan_tmp.reserve((2 * (nb / mc::kScanTile + 4) + 16) * 4ull);
+    if (P) {
+        hipLaunchKernelGGL(mc::k_grid_count, grid_for(P), dim3(256), 0, s, ctx->d_scene.as<float>(), P, inv, nb,
+                           ctx->d_gcnt.as<int>(), ctx->d_gbkt.as<unsigned>(), ctx->d_gcellk.as<unsigned long long>());
+    }
+    mc::scan_large(s, ctx->d_gcnt.as<int>(), ctx->d_gstart.as<int>(), static_cast<int>(nb), ctx->d_gscan_tmp.as<int>());
+    if (P)
+        hipLaunchKernelGGL(mc::k_grid_scatter, grid_for(P), dim3(256), 0, s, ctx->d_scene.as<float>(), P,
+                           ctx->d_gbkt.as<unsigned>(), ctx->d_gcellk.as<unsigned long long>(), ctx->d_gstart.as<int>(),
+                           ctx->d_gcnt.as<int>(), ctx->d_gpts.as<float4>(), ctx->d_gidx.as<int>(),
+                           ctx->d_gcell.as<unsigned long long>());
+    ctx->grid_radius = radius;
+}
+
+constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
+const int kBpStatInit[BS_COUNT] = {INT_MAX, 0, 0, 0, 0, 0, 0, 0};
+
+}  // namespace
+
+extern "C" {
+
+void mc_bp_params_default(mc_bp_params *p)
+{
+    if (!p) return;
+    p->depth_trunc = 20.0;
+    p->voxel_size = 0.01;
+    p->dbscan_eps = 0.04;
+    p->component_min_fraction = 0.2;
+    p->sor_std_ratio = 2.0;
+    p->ball_radius = 0.01;
+    p->coverage_threshold = 0.3;
+    p->dbscan_min_points = 4;
+    p->sor_neighbors = 20;
+    p->ball_k = 20;
+    p->few_points = 25;
+}
+
+int mc_scene_set_points(mc_ctx *ctx, int64_t num_points, const float *xyz, int on_device)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_points >= 0 && num_points < (int64_t(1) << 31) - 1, MC_ERR_UNSUPPORTED, "num_points out of range");
+        MC_REQUIRE(num_points == 0 || xyz, MC_ERR_INVALID, "null points");
+        hipStream_t s = ctx->stream;
+        ctx->P_scene = num_points;
+        ctx->d_scene.reserve((num_points + 1) * 12);
+        if (num_points)
+            MC_HIP(hipMemcpyAsync(ctx->d_scene.ptr, xyz, num_points * 12,
+                                  on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+        ctx->have_points = true;
+        ctx->have_bp = false;
+        ctx->grid_radius = -1.f;  // the grid is built by the next mc_backproject
+        MC_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
+                   const uint8_t *seg, const double *intrinsics, const double *poses, int on_device,
+                   const mc_bp_params *params)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_points, MC_ERR_STATE, "mc_backproject before mc_scene_set_points");
+        MC_REQUIRE(num_frames >= 0 && height > 0 && width > 0, MC_ERR_INVALID, "bad frame sizes");
+        MC_REQUIRE(num_frames == 0 || (depth && seg && intrinsics && poses), MC_ERR_INVALID, "null frame arrays");
+        MC_REQUIRE(static_cast<int64_t>(height) * width < (int64_t(1) << 31), MC_ERR_UNSUPPORTED, "image too large");
+        mc_bp_params prm;
+        if (params) prm = *params;
+        else mc_bp_params_default(&prm);
+        MC_REQUIRE(prm.sor_neighbors >= 1 && prm.sor_neighbors <= mc::kBpKnnMax, MC_ERR_UNSUPPORTED,
+                   "sor_neighbors must be in [1, 32]");
+        MC_REQUIRE(prm.ball_k >= 1 && prm.ball_k <= mc::kBpBallMax, MC_ERR_UNSUPPORTED, "ball_k must be in [1, 32]");
+        MC_REQUIRE(prm.voxel_size > 0 && prm.dbscan_eps > 0 && prm.ball_radius > 0, MC_ERR_INVALID, "bad radii");
+        hipStream_t s = ctx->stream;
+        const int F = num_frames, H = height, W = width;
+        const size_t HW = static_cast<size_t>(H) * W;
+        const int nbands = (H + mc::kBpBand - 1) / mc::kBpBand;
+        ctx->have_bp = false;
+        ctx->bp_F = F;
+        ctx->bp_err_frame = -1;
+        ctx->bp_col.clear();
+        ctx->bp_label.clear();
+        ctx->bp_off.assign(1, 0);
+        ctx->bp_stats.clear();
+        ctx->bp_nnz = 0;
+        const float rf = static_cast<float>(prm.ball_radius);
+        if (ctx->grid_radius != rf) bp_build_grid(ctx, rf, s);
+
+        const float *dep = depth;
+        const uint8_t *sg = seg;
+        const double *Kp = intrinsics, *Tp = poses;
+        if (!on_device && F) {
+            ctx->d_in_depth.reserve(F * HW * 4);
+            ctx->d_in_seg.reserve(F * HW);
+            ctx->d_in_intr.reserve(F * 4 * 8ull);
+            ctx->d_in_pose.reserve(F * 16 * 8ull);
+            MC_HIP(hipMemcpyAsync(ctx->d_in_depth.ptr, depth, F * HW * 4, hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(ctx->d_in_seg.ptr, seg, F * HW, hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(ctx->d_in_intr.ptr, intrinsics, F * 4 * 8ull, hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(ctx->d_in_pose.ptr, poses, F * 16 * 8ull, hipMemcpyHostToDevice, s));
+            dep = ctx->d_in_depth.as<float>();
+            sg = ctx->d_in_seg.as<uint8_t>();
+            Kp = ctx->d_in_intr.as<double>();
+            Tp = ctx->d_in_pose.as<double>();
+        }
+        // frames per batch: bounded pixel capacity of the per-slot arrays
+        size_t budget = static_cast<size_t>(48) << 20;
+        if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
+        const int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
+        bp_reserve(ctx, FB, H, W, nbands, s);
+        const int PW = static_cast<int>((ctx->P_scene + 63) / 64) + 1;
+        if (ctx->d_bpbm.bytes < static_cast<size_t>(kBpGrid) * PW * 8) {
+            ctx->d_bpbm.reserve(static_cast<size_t>(kBpGrid) * PW * 8);
+            MC_HIP(hipMemsetAsync(ctx->d_bpbm.ptr, 0, ctx->d_bpbm.bytes, s));  // kept zero by k_bp_query
+            ctx->bp_bm_blocks = kBpGrid;
+        }
+        size_t tmp_cap = std::max<size_t>(ctx->d_tmp.bytes / 4, std::max<size_t>(1 << 20, ctx->bp_px_cap));
+        ctx->d_tmp.reserve(tmp_cap * 4);
+
+        mc::BpDev dv;
+        dv.trunc = prm.depth_trunc;
+        dv.vs = prm.voxel_size;
+        dv.eps2 = prm.dbscan_eps * prm.dbscan_eps;
+        dv.ce = prm.dbscan_eps * 1.01;
+        dv.frac = prm.component_min_fraction;
+        dv.std_ratio = prm.sor_std_ratio;
+        dv.cov = prm.coverage_threshold;
+        dv.r2 = rf * rf;
+        dv.scene_inv = 1.0f / (2.0f * rf);
+        dv.minpts = prm.dbscan_min_points;
+        dv.knn = prm.sor_neighbors;
+        dv.kball = prm.ball_k;
+        dv.few = prm.few_points;
+        dv.H = H;
+        dv.W = W;
+        dv.nbands = nbands;
+
+        int *st = ctx->d_bpstat.as<int>();
+        std::vector<int> hs(BS_COUNT);
+        for (int b0 = 0; b0 < F;) {
+            const int fb = std::min(FB, F - b0);
+            const float *dB = dep + b0 * HW;
+            const uint8_t *sB = sg + b0 * HW;
+            const double *KB = Kp + 4 * static_cast<size_t>(b0), *TB = Tp + 16 * static_cast<size_t>(b0);
+            const int nslot = fb * 256;
+            {
+                TimedScope ts(ctx->timer, s, "bp_pixels");
+                MC_HIP(hipMemcpyAsync(st, kBpStatInit, sizeof(kBpStatInit), hipMemcpyHostToDevice, s));
+                MC_HIP(hipMemsetAsync(ctx->d_present.ptr, 0, fb * 8 * 4, s));
+                MC_HIP(hipMemsetAsync(ctx->d_fflags.ptr, 0, fb * 4, s));
+                hipLaunchKernelGGL(mc::k_bp_count, dim3(nbands, fb), dim3(256), 0, s, dB, sB, TB, dv,
+                                   ctx->d_band.as<int>(), ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>());
+                hipLaunchKernelGGL(mc::k_bp_frames, dim3(fb), dim3(256), 0, s, ctx->d_band.as<int>(),
+                                   ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(), dv, ctx->d_cand.as<int>(),
+                                   ctx->d_npix.as<int>(), st + BS_ERRF);
+                mc::scan_device_n(s, ctx->d_cand.as<int>(), ctx->d_csidx.as<int>(), nullptr, nslot, st + BS_NS,
+                                  ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), st + BS_NPX);
+                hipLaunchKernelGGL(mc::k_bp_slots, grid_for(nslot), dim3(256), 0, s, ctx->d_cand.as<int>(),
+                                   ctx->d_csidx.as<int>(), ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), nslot,
+                                   ctx->d_slot_of.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(),
+                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>());
+                hipLaunchKernelGGL(mc::k_bp_compact, dim3(nbands, fb), dim3(256), 0, s, dB, sB, ctx->d_band.as<int>(),
+                                   ctx->d_slot_of.as<int>(), ctx->d_slot_pix.as<int>(), dv,
+                                   ctx->d_pix_list.as<unsigned>());
+            }
+            {
+                TimedScope ts(ctx->timer, s, "bp_voxel");
+                hipLaunchKernelGGL(mc::k_bp_voxel, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
+                                   ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(),
+                                   ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
+                                   ctx->d_hkey.as<unsigned long long>(), ctx->d_hvid.as<int>(), ctx->d_hfirst.as<int>(),
+                                   ctx->d_vox_entry.as<int>(), ctx->d_acc.as<double>(), ctx->d_vpts.as<double>(),
+                                   ctx->d_slot_nv.as<int>(), st + BS_VOXERR);
+            }
+            {
+                TimedScope ts(ctx->timer, s, "bp_denoise");
+                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
+                                   ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                                   ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
+                                   ctx->d_bstart.as<int>(), ctx->d_blist.as<int>(), ctx->d_ncnt.as<int>(),
+                                   ctx->d_par.as<int>(), ctx->d_droot.as<int>(), ctx->d_rnk.as<int>(),
+                                   ctx->d_lab.as<int>(), ctx->d_ccnt.as<int>(), ctx->d_ssidx.as<int>(),
+                                   ctx->d_avg.as<double>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
+                                   ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
+            }
+            {
+                TimedScope ts(ctx->timer, s, "bp_query");
+                hipLaunchKernelGGL(mc::k_bp_query, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
+                                   ctx->d_slot_pix.as<int>(), ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>(),
+                                   ctx->d_qpts.as<float>(), dv, ctx->d_gpts.as<float4>(), ctx->d_gidx.as<int>(),
+                                   ctx->d_gcell.as<unsigned long long>(), ctx->d_gstart.as<int>(), ctx->gnb,
+                                   ctx->d_bpbm.as<unsigned long long>(), PW, ctx->d_tmp.as<int>(),
+                                   static_cast<int>(std::min<size_t>(tmp_cap, INT_MAX)), st + BS_TOP,
+                                   ctx->d_slot_nn.as<int>(), ctx->d_slot_toff.as<int>(), ctx->d_slot_cov.as<int>(),
+                                   st + BS_OVF);
+                hipLaunchKernelGGL(mc::k_bp_keepflags, grid_for(nslot), dim3(256), 0, s, st + BS_NS,
+                                   ctx->d_slot_nn.as<int>(), ctx->d_kflag.as<int>(), ctx->d_ksize.as<int>());
+                mc::scan_device_n(s, ctx->d_kflag.as<int>(), ctx->d_midx.as<int>(), st + BS_NS, 0, st + BS_M,
+                                  ctx->d_ksize.as<int>(), ctx->d_moff.as<int>(), st + BS_NNZ);
+            }
+            MC_HIP(hipMemcpyAsync(hs.data(), st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipStreamSynchronize(s));
+            ctx->timer.collect();
+            if (hs[BS_ERRF] != INT_MAX) {
+                ctx->bp_err_frame = b0 + hs[BS_ERRF];
+                throw McError{MC_ERR_INVALID, "frame " + std::to_string(b0 + hs[BS_ERRF]) +
+                                                  ": depth pixel equal to depth_trunc (the reference raises "
+                                                  "IndexError at utils/mask_backprojection.py:100)"};
+            }
+            MC_REQUIRE(hs[BS_VOXERR] == 0, MC_ERR_UNSUPPORTED, "voxel index beyond 2^21 per axis");
+            if (hs[BS_OVF]) {  // neighbour sets overflowed tmp: grow and redo the batch
+                tmp_cap = static_cast<size_t>(hs[BS_TOP]) + (static_cast<size_t>(hs[BS_TOP]) >> 1) + 1024;
+                ctx->d_tmp.reserve(tmp_cap * 4);
+                continue;
+            }
+            const int NS = hs[BS_NS], Mb = hs[BS_M], nnzb = hs[BS_NNZ];
+            ctx->d_out_col.reserve((Mb + 1) * 4);
+            ctx->d_out_label.reserve((Mb + 1) * 4);
+            ctx->d_out_off.reserve((Mb + 1) * 4);
+            grow_keep(ctx->d_bp_pts, (ctx->bp_nnz + nnzb + 1) * 4, ctx->bp_nnz * 4, s);
+            {
+                TimedScope ts(ctx->timer, s, "bp_query");
+                hipLaunchKernelGGL(mc::k_bp_emit, grid_for(std::max(NS, 1), 4, 4096), dim3(256), 0, s, st + BS_NS,
+                                   ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(), ctx->d_slot_nn.as<int>(),
+                                   ctx->d_slot_toff.as<int>(), ctx->d_midx.as<int>(), ctx->d_moff.as<int>(),
+                                   ctx->d_tmp.as<int>(), ctx->d_out_col.as<int>(), ctx->d_out_label.as<int>(),
+                                   ctx->d_out_off.as<int>(), ctx->d_bp_pts.as<int>() + ctx->bp_nnz);
+            }
+            std::vector<int> col(Mb), lab(Mb), off(Mb);
+            if (Mb) {
+                MC_HIP(hipMemcpyAsync(col.data(), ctx->d_out_col.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipMemcpyAsync(lab.data(), ctx->d_out_label.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipMemcpyAsync(off.data(), ctx->d_out_off.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
+            }
+            // per-candidate statistics
+            std::vector<int> sf(NS), sid(NS), snp(NS), snv(NS), sm(NS), sns(NS), scov(NS), snn(NS);
+            if (NS) {
+                const std::pair<void *, DevBuf *> cp[] = {{sf.data(), &ctx->d_slot_frame}, {sid.data(), &ctx->d_slot_id},
+                                                          {snp.data(), &ctx->d_slot_np},    {snv.data(), &ctx->d_slot_nv},
+                                                          {sm.data(), &ctx->d_slot_m},      {sns.data(), &ctx->d_slot_ns},
+                                                          {scov.data(), &ctx->d_slot_cov},  {snn.data(), &ctx->d_slot_nn}};
+                for (auto &c : cp) MC_HIP(hipMemcpyAsync(c.first, c.second->ptr, NS * 4, hipMemcpyDeviceToHost, s));
+            }
+            MC_HIP(hipStreamSynchronize(s));
+            for (int g = 0; g < Mb; g++) {
+                ctx->bp_col.push_back(b0 + col[g]);
+                ctx->bp_label.push_back(lab[g]);
+            }
+            for (int g = 0; g < Mb; g++) ctx->bp_off.push_back(ctx->bp_nnz + (g + 1 < Mb ? off[g + 1] : nnzb));
+            for (int x = 0; x < NS; x++) {
+                const int kept = snn[x] >= 0;
+                const int row[MC_BP_NSTAT] = {b0 + sf[x], sid[x], snp[x], snv[x], sm[x], sns[x], -1,
+                                              sns[x] >= prm.few_points ? scov[x] : 0, kept ? snn[x] : 0, kept};
+                ctx->bp_stats.insert(ctx->bp_stats.end(), row, row + MC_BP_NSTAT);
+            }
+            ctx->bp_nnz += nnzb;
+            b0 += fb;
+        }
+        ctx->have_bp = true;
+    });
+}
+
+int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(info, MC_ERR_INVALID, "null info");
+        info->num_frames = ctx->bp_F;
+        info->num_candidates = static_cast<int32_t>(ctx->bp_stats.size() / MC_BP_NSTAT);
+        info->num_masks = static_cast<int32_t>(ctx->bp_col.size());
+        info->error_frame = ctx->bp_err_frame;
+        info->num_mask_points = ctx->bp_nnz;
+    });
+}
+
+int mc_backproject_get_masks(mc_ctx *ctx, int32_t *mask_col, int32_t *mask_label, int64_t *mask_off,
+                             int32_t *mask_pts)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_bp, MC_ERR_STATE, "no back-projection result");
+        const size_t M = ctx->bp_col.size();
+        if (mask_col) std::copy(ctx->bp_col.begin(), ctx->bp_col.end(), mask_col);
+        if (mask_label) std::copy(ctx->bp_label.begin(), ctx->bp_label.end(), mask_label);
+        if (mask_off) std::copy(ctx->bp_off.begin(), ctx->bp_off.begin() + M + 1, mask_off);
+        if (mask_pts && ctx->bp_nnz)
+            MC_HIP(hipMemcpyAsync(mask_pts, ctx->d_bp_pts.ptr, ctx->bp_nnz * 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_bp, MC_ERR_STATE, "no back-projection result");
+        std::copy(ctx->bp_stats.begin(), ctx->bp_stats.end(), stats);
+    });
+}
+
+int mc_scene_use_backprojection(mc_ctx *ctx)
+{
+    if (!ctx) return MC_ERR_INVALID;
+    if (!ctx->have_bp) {
+        ctx->err = "no back-projection result";
+        return MC_ERR_STATE;
+    }
+    const std::vector<int32_t> col = ctx->bp_col, lab = ctx->bp_label;
+    const std::vector<int64_t> off = ctx->bp_off;
+    return mc_scene_set_masks(ctx, ctx->P_scene, ctx->bp_F, static_cast<int32_t>(col.size()), col.data(), lab.data(),
+                              off.data(), ctx->d_bp_pts.as<int32_t>(), 1);
 }
 
 }  // extern "C"

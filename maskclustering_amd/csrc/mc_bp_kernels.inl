@@ -1,0 +1,962 @@
+// mc_bp_kernels.inl — S1 mask back-projection for gfx950 (utils/mask_backprojection.py:70-151 with
+// utils/geometry.py:9-24); included by mc_api.hip after mc_kernels.inl.
+//
+// The Open3D / pytorch3d semantics restated here are those of oracle/s1_oracle.c, whose header lists
+// the choices (u1)-(u4) made where the libraries' result is not determined by their algorithm.  The
+// kernels implement the same arithmetic: built with -ffp-contract=off, so every double operation is
+// rounded where the oracle rounds it; the one FMA the CUDA ball query has is written out.
+//
+// One launch sequence per batch of frames; every data-dependent count is read on the device:
+//   k_bp_count    (band, frame)  per-id valid-pixel counts, id presence, depth == trunc, inf pose
+//   k_bp_frames   (frame)        per-id totals -> per-band offsets; candidate masks; error status
+//   scan          candidate slots (frames, then ids ascending) and their pixel ranges
+//   k_bp_slots                   slot table
+//   k_bp_compact  (band, frame)  stable row-major pixel list of every slot
+//   k_bp_voxel    WG per slot    voxel_down_sample: sums in pixel order, first-occurrence voxel order
+//   k_bp_denoise  WG per slot    DBSCAN + 20 % class filter + statistical outlier removal + f32 AABB
+//   k_bp_query    WG per slot    hashed-grid ball query (first K by scene index), coverage, the set
+//   scan + k_bp_emit             kept masks -> CSR (frame column, id, sorted unique scene ids)
+// Every per-slot array lives in the slot's pixel range [pix, pix + npix) (npix bounds every per-slot
+// count), so no allocation depends on a device result.
+#include "mc_internal.hpp"
+
+#include <cfloat>
+
+namespace mc {
+
+constexpr int kBpBand = 16;        // image rows per (band, frame) block
+constexpr int kBpKnnMax = 32;      // sor_neighbors <= 32
+constexpr int kBpBallMax = 32;     // ball_k <= 32
+constexpr int kBpStage = 2048;     // LDS staging of the outlier statistics
+constexpr unsigned long long kEmptyKey = ~0ull;
+constexpr int kCellBias = 1 << 20; // scene-grid cell coordinates in [-2^20, 2^20)
+
+struct BpDev {
+    double trunc, vs, eps2, ce, frac, std_ratio, cov;
+    float r2, scene_inv;
+    int minpts, knn, kball, few;
+    int H, W, nbands;
+};
+
+__device__ __forceinline__ unsigned bp_hash3(int x, int y, int z)
+{
+    unsigned h = static_cast<unsigned>(x) * 0x9E3779B1u;
+    h ^= static_cast<unsigned>(y) * 0x85EBCA77u + (h << 6) + (h >> 2);
+    h ^= static_cast<unsigned>(z) * 0xC2B2AE3Du + (h << 6) + (h >> 2);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return h;
+}
+__device__ __forceinline__ unsigned bp_hash64(unsigned long long k)
+{
+    k *= 0x9E3779B97F4A7C15ull;
+    return static_cast<unsigned>(k >> 32) ^ static_cast<unsigned>(k);
+}
+// h mod n without a division
+__device__ __forceinline__ unsigned mod_mul(unsigned h, unsigned n)
+{
+    return static_cast<unsigned>((static_cast<unsigned long long>(h) * n) >> 32);
+}
+__device__ __forceinline__ unsigned long long pack3(int x, int y, int z)
+{
+    return (static_cast<unsigned long long>(x) << 42) | (static_cast<unsigned long long>(y) << 21) |
+           static_cast<unsigned long long>(z);
+}
+__device__ __forceinline__ int scene_cell(float v, float inv)
+{
+    return min(max(static_cast<int>(floorf(v * inv)), -kCellBias), kCellBias - 1) + kCellBias;
+}
+
+// (a1, u1): Open3D create_from_depth_image + transform, in double, no FMA
+__device__ __forceinline__ void bp_world(const double *__restrict__ K, const double *__restrict__ T, int u, int v,
+                                         float d, double &ox, double &oy, double &oz)
+{
+    const double z = static_cast<double>(d);
+    const double x = ((static_cast<double>(u) - K[2]) * z) / K[0];
+    const double y = ((static_cast<double>(v) - K[3]) * z) / K[1];
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = (((T[4 * k] * x) + (T[4 * k + 1] * y)) + (T[4 * k + 2] * z)) + T[4 * k + 3];
+    ox = r[0] / r[3];
+    oy = r[1] / r[3];
+    oz = r[2] / r[3];
+}
+
+// (u3): nanoflann L2 for 3-D, ((dx*dx + dy*dy) + dz*dz)
+__device__ __forceinline__ double bp_d2(const double *a, const double *b)
+{
+    const double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
+    return ((dx * dx) + (dy * dy)) + (dz * dz);
+}
+
+__device__ __forceinline__ double wave_min_d(double v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = fmin(v, __shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max_d(double v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_min_i(int v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
+// block (256) min / max of 3 doubles, broadcast to every thread; red holds 2*3*4 doubles
+__device__ __forceinline__ void block_minmax3(double mn[3], double mx[3], double *red)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const double a = wave_min_d(mn[c]), b = wave_max_d(mx[c]);
+        if (lane == 0) {
+            red[c * 4 + wv] = a;
+            red[12 + c * 4 + wv] = b;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        mn[c] = fmin(fmin(red[c * 4], red[c * 4 + 1]), fmin(red[c * 4 + 2], red[c * 4 + 3]));
+        mx[c] = fmax(fmax(red[12 + c * 4], red[12 + c * 4 + 1]), fmax(red[12 + c * 4 + 2], red[12 + c * 4 + 3]));
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// scene grid (built once per scene): points bucketed by cells of 2r, sorted copy as float4
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_grid_count(const float *__restrict__ xyz, int P, float inv, unsigned nb,
+                                                    int *__restrict__ cnt, unsigned *__restrict__ bkt,
+                                                    unsigned long long *__restrict__ cellk)
+{
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < P; j += gridDim.x * 256) {
+        const int cx = scene_cell(xyz[3 * j], inv), cy = scene_cell(xyz[3 * j + 1], inv),
+                  cz = scene_cell(xyz[3 * j + 2], inv);
+        const unsigned b = mod_mul(bp_hash3(cx, cy, cz), nb);
+        bkt[j] = b;
+        cellk[j] = pack3(cx, cy, cz);
+        atomicAdd(&cnt[b], 1);
+    }
+}
+
+// cnt returns to zero (ready for the next scene)
+__global__ __launch_bounds__(256) void k_grid_scatter(const float *__restrict__ xyz, int P,
+                                                      const unsigned *__restrict__ bkt,
+                                                      const unsigned long long *__restrict__ cellk,
+                                                      const int *__restrict__ start, int *__restrict__ cnt,
+                                                      float4 *__restrict__ gpts, int *__restrict__ gidx,
+                                                      unsigned long long *__restrict__ gcell)
+{
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < P; j += gridDim.x * 256) {
+        const unsigned b = bkt[j];
+        const int pos = start[b] + atomicSub(&cnt[b], 1) - 1;
+        gpts[pos] = make_float4(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], 0.f);
+        gidx[pos] = j;
+        gcell[pos] = cellk[j];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// (a2) pixels -> masks
+// ---------------------------------------------------------------------------------------------
+// One block per (band of kBpBand rows, frame).  band_cnt[f][band][id]: valid-depth pixels of id in
+// the band (0 < d < trunc: Open3D keeps d < trunc, :22; ids != 0, :94); present[f]: ids in the
+// image (torch.unique, :77); fflags[f]: 1 = a pixel with d == trunc (the reference's IndexError
+// at :100), 2 = inf in the pose (:73-74, frame skipped).
+__global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
+                                                  const double *__restrict__ pose, BpDev pr, int *__restrict__ band_cnt,
+                                                  unsigned *__restrict__ present, int *__restrict__ fflags)
+{
+    __shared__ int cnt[256];
+    __shared__ unsigned pres[8];
+    __shared__ int sflag;
+    const int f = blockIdx.y, band = blockIdx.x, t = threadIdx.x, lane = lane_id();
+    const int W = pr.W;
+    cnt[t] = 0;
+    if (t < 8) pres[t] = 0u;
+    if (t == 0) sflag = 0;
+    __syncthreads();
+    if (t < 16 && isinf(pose[16 * static_cast<size_t>(f) + t])) atomicOr(&sflag, 2);
+    __syncthreads();
+    const bool skip = (sflag & 2) != 0;
+    const size_t fb = static_cast<size_t>(f) * pr.H * W;
+    const int i0 = band * kBpBand * W, i1 = min(pr.H, (band + 1) * kBpBand) * W;
+    int trunc = 0, lastp = -1;
+    for (int ib = i0; ib < i1; ib += 256) {
+        const int i = ib + t;
+        int id = -1;
+        if (i < i1) {
+            const int sid = seg[fb + i];
+            const float d = depth[fb + i];
+            if (sid != lastp) {
+                atomicOr(&pres[sid >> 5], 1u << (sid & 31));
+                lastp = sid;
+            }
+            if (static_cast<double>(d) == pr.trunc) trunc = 1;
+            if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id = sid;
+        }
+        unsigned long long act = __ballot(id >= 0);
+        while (act) {  // one LDS add per distinct id per wave
+            const int leader = __ffsll(static_cast<long long>(act)) - 1;
+            const int k = __shfl(id, leader, 64);
+            const unsigned long long m = __ballot(id == k);
+            if (lane == leader) atomicAdd(&cnt[k], __popcll(m));
+            act &= ~m;
+        }
+    }
+    if (trunc) atomicOr(&sflag, 1);
+    __syncthreads();
+    band_cnt[(static_cast<size_t>(f) * pr.nbands + band) * 256 + t] = cnt[t];
+    if (t < 8 && pres[t]) atomicOr(&present[f * 8 + t], pres[t]);
+    if (t == 0 && sflag) atomicOr(&fflags[f], sflag);
+}
+
+// One block per frame, thread = id: band counts -> band offsets within the id's pixel list;
+// candidate = id != 0 with >= few_points valid pixels (:101) in a frame that neither returns
+// early (inf pose) nor raises (d == trunc with ids present; *err_frame = first such frame).
+__global__ __launch_bounds__(256) void k_bp_frames(int *__restrict__ band_cnt, const unsigned *__restrict__ present,
+                                                   const int *__restrict__ fflags, BpDev pr, int *__restrict__ cand,
+                                                   int *__restrict__ npix, int *__restrict__ err_frame)
+{
+    const int f = blockIdx.x, id = threadIdx.x;
+    const int fl = fflags[f];
+    bool any_id = false;
+    for (int w = 0; w < 8; w++) any_id |= (present[f * 8 + w] & (w == 0 ? ~1u : ~0u)) != 0u;
+    const bool inf_pose = (fl & 2) != 0;
+    const bool err = !inf_pose && any_id && (fl & 1);
+    if (err && id == 0) atomicMin(err_frame, f);
+    int tot = 0;
+    int *bc = band_cnt + static_cast<size_t>(f) * pr.nbands * 256 + id;
+    for (int b = 0; b < pr.nbands; b++) {
+        const int c = bc[static_cast<size_t>(b) * 256];
+        bc[static_cast<size_t>(b) * 256] = tot;
+        tot += c;
+    }
+    const bool ok = id != 0 && !inf_pose && !err && tot >= pr.few;
+    cand[f * 256 + id] = ok ? 1 : 0;
+    npix[f * 256 + id] = ok ? tot : 0;
+}
+
+__global__ __launch_bounds__(256) void k_bp_slots(const int *__restrict__ cand, const int *__restrict__ sidx,
+                                                  const int *__restrict__ npix, const int *__restrict__ poff, int n,
+                                                  int *__restrict__ slot_of, int *__restrict__ slot_frame,
+                                                  int *__restrict__ slot_id, int *__restrict__ slot_np,
+                                                  int *__restrict__ slot_pix)
+{
+    for (int x = blockIdx.x * 256 + threadIdx.x; x < n; x += gridDim.x * 256) {
+        if (cand[x]) {
+            const int s = sidx[x];
+            slot_frame[s] = x >> 8;
+            slot_id[s] = x & 255;
+            slot_np[s] = npix[x];
+            slot_pix[s] = poff[x];
+            slot_of[x] = s;
+        } else {
+            slot_of[x] = -1;
+        }
+    }
+}
+
+// Stable compaction: every slot's pixels in row-major order (the order of view_points[valid_mask],
+// :96-100).  Per 256-pixel chunk, ranks within a wave by ballot groups; the four waves take their
+// positions in wave order (one barrier per wave), so the list order is the pixel order.
+__global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
+                                                    const int *__restrict__ band_off, const int *__restrict__ slot_of,
+                                                    const int *__restrict__ slot_pix, BpDev pr,
+                                                    unsigned *__restrict__ pix_list)
+{
+    __shared__ int cur[256];
+    __shared__ int gb[4][64];
+    const int f = blockIdx.y, band = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    const int W = pr.W;
+    {
+        const int s = slot_of[f * 256 + t];
+        cur[t] = s >= 0 ? slot_pix[s] + band_off[(static_cast<size_t>(f) * pr.nbands + band) * 256 + t] : -1;
+    }
+    __syncthreads();
+    const size_t fb = static_cast<size_t>(f) * pr.H * W;
+    const int i0 = band * kBpBand * W, i1 = min(pr.H, (band + 1) * kBpBand) * W;
+    for (int ib = i0; ib < i1; ib += 256) {
+        const int i = ib + t;
+        int id = -1;
+        if (i < i1) {
+            const int sid = seg[fb + i];
+            const float d = depth[fb + i];
+            if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && cur[sid] >= 0) id = sid;
+        }
+        int rank = 0, leader = 0, n = 0;
+        unsigned long long act = __ballot(id >= 0);
+        while (act) {
+            const int L = __ffsll(static_cast<long long>(act)) - 1;
+            const int k = __shfl(id, L, 64);
+            const unsigned long long m = __ballot(id == k);
+            if (id == k) {
+                rank = __popcll(m & ((1ull << lane) - 1ull));
+                leader = L;
+                n = __popcll(m);
+            }
+            act &= ~m;
+        }
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            if (wv == w && id >= 0 && lane == leader) {
+                gb[w][lane] = cur[id];
+                cur[id] += n;
+            }
+            __syncthreads();
+        }
+        if (id >= 0) pix_list[gb[wv][leader] + rank] = static_cast<unsigned>(i);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// (a3) voxel_down_sample(0.01) (:105), workgroup per slot
+// ---------------------------------------------------------------------------------------------
+// Open3D: min bound - voxel/2, index = floor((p - vmin) / voxel), per-voxel sum in input order,
+// mean = sum / count.  Output order (u2): first occurrence in pixel order.  Chunks of 256 pixels
+// in list order: voxel keys go into the slot's hash (2 entries per pixel, empty at rest); new
+// voxels get ids in order of their first pixel (atomicMin of the pixel rank, then an ordered
+// scan); the sums are added wave by wave, lane by lane, i.e. in pixel order.
+__global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, const int *__restrict__ slot_frame,
+                                                  const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                  const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
+                                                  const double *__restrict__ intr, const double *__restrict__ pose, BpDev pr,
+                                                  unsigned long long *__restrict__ hkey, int *__restrict__ hvid,
+                                                  int *__restrict__ hfirst, int *__restrict__ vox_entry,
+                                                  double *__restrict__ acc, double *__restrict__ vpts,
+                                                  int *__restrict__ slot_nv, int *__restrict__ errflag)
+{
+    __shared__ double sp[256 * 3];
+    __shared__ double red[24];
+    __shared__ int ws[4];
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    const int W = pr.W;
+    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+        const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
+        const double *K = intr + 4 * static_cast<size_t>(f);
+        const double *T = pose + 16 * static_cast<size_t>(f);
+        const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
+        const unsigned *pl = pix_list + base;
+        // min bound (order-free)
+        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int k = t; k < n; k += 256) {
+            const unsigned i = pl[k];
+            double p[3];
+            bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+#pragma unroll
+            for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
+        }
+        block_minmax3(mn, mx, red);
+        double vmin[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
+        const unsigned C = 2u * static_cast<unsigned>(n);
+        unsigned long long *hk = hkey + 2 * static_cast<size_t>(base);
+        int *hv = hvid + 2 * static_cast<size_t>(base);
+        int *hf = hfirst + 2 * static_cast<size_t>(base);
+        double *ac = acc + 4 * static_cast<size_t>(base);
+        int nv = 0;
+        for (int c0 = 0; c0 < n; c0 += 256) {
+            const int k = c0 + t;
+            const bool valid = k < n;
+            double p[3] = {0.0, 0.0, 0.0};
+            unsigned e = 0;
+            if (valid) {
+                const unsigned i = pl[k];
+                bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+                long long ix[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    ix[c] = static_cast<long long>(floor((p[c] - vmin[c]) / pr.vs));
+                    if (ix[c] < 0 || ix[c] >= (1ll << 21)) {
+                        atomicOr(errflag, 1);
+                        ix[c] = ix[c] < 0 ? 0 : (1ll << 21) - 1;
+                    }
+                }
+                const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
+                e = mod_mul(bp_hash64(key), C);
+                while (true) {
+                    unsigned long long cur = hk[e];
+                    if (cur == kEmptyKey) {
+                        cur = atomicCAS(&hk[e], kEmptyKey, key);
+                        if (cur == kEmptyKey) cur = key;
+                    }
+                    if (cur == key) break;
+                    e = e + 1 == C ? 0 : e + 1;
+                }
+                if (ld_agent(&hv[e]) < 0) atomicMin(&hf[e], k);
+            }
+            __syncthreads();
+            const bool first = valid && ld_agent(&hv[e]) < 0 && ld_agent(&hf[e]) == k;
+            int tot;
+            const int pos = block_excl_scan<256>(first ? 1 : 0, ws, tot);
+            if (first) {
+                const int v = nv + pos;
+                st_agent(&hv[e], v);
+                vox_entry[base + v] = static_cast<int>(e);
+                ac[4 * v] = 0.0;
+                ac[4 * v + 1] = 0.0;
+                ac[4 * v + 2] = 0.0;
+                ac[4 * v + 3] = 0.0;
+            }
+            __syncthreads();
+            const int vid = valid ? ld_agent(&hv[e]) : -1;
+            sp[3 * t] = p[0];
+            sp[3 * t + 1] = p[1];
+            sp[3 * t + 2] = p[2];
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                if (wv == w) {
+                    unsigned long long act = __ballot(vid >= 0);
+                    while (act) {
+                        const int L = __ffsll(static_cast<long long>(act)) - 1;
+                        const int kk = __shfl(vid, L, 64);
+                        const unsigned long long m = __ballot(vid == kk);
+                        if (lane == L) {  // AccumulatedPoint::AddPoint, lane (= pixel) order
+                            double ax = ac[4 * kk], ay = ac[4 * kk + 1], az = ac[4 * kk + 2], an = ac[4 * kk + 3];
+                            unsigned long long mm = m;
+                            while (mm) {
+                                const int l = __ffsll(static_cast<long long>(mm)) - 1;
+                                mm &= mm - 1;
+                                const double *q = sp + 3 * (w * 64 + l);
+                                ax = ax + q[0];
+                                ay = ay + q[1];
+                                az = az + q[2];
+                                an = an + 1.0;
+                            }
+                            ac[4 * kk] = ax;
+                            ac[4 * kk + 1] = ay;
+                            ac[4 * kk + 2] = az;
+                            ac[4 * kk + 3] = an;
+                        }
+                        act &= ~m;
+                    }
+                }
+                __syncthreads();
+            }
+            nv += tot;
+        }
+        // means; the hash entries of this slot return to empty
+        for (int v = t; v < nv; v += 256) {
+            const double cnt = ac[4 * v + 3];
+            vpts[3 * (static_cast<size_t>(base) + v)] = ac[4 * v] / cnt;
+            vpts[3 * (static_cast<size_t>(base) + v) + 1] = ac[4 * v + 1] / cnt;
+            vpts[3 * (static_cast<size_t>(base) + v) + 2] = ac[4 * v + 2] / cnt;
+            const int e = vox_entry[base + v];
+            hk[e] = kEmptyKey;
+            st_agent(&hv[e], -1);
+            st_agent(&hf[e], INT_MAX);
+        }
+        if (t == 0) slot_nv[s] = nv;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// (a4) denoise (geometry.py:9-24), workgroup per slot
+// ---------------------------------------------------------------------------------------------
+// Points are bucketed into a hashed grid of cells ce = 1.01 eps (2 buckets per point, counting
+// sort); a point is visited only from its own cell (the cell key is compared), so every
+// neighbourhood scan sees each point once.
+//   DBSCAN (Open3D ClusterDBSCAN): core = >= min_points neighbours with d2 < eps^2 (self
+//   included); clusters = connected core points, numbered in order of their smallest point (the
+//   order Open3D seeds them); a non-core point with a core neighbour joins the lowest-numbered
+//   adjacent cluster (the first cluster to reach it), else it is noise.
+//   Class filter: drop every label class (noise included) with count < 0.2 n.
+//   remove_statistical_outlier(20, 2): mean distance to the k = min(20, m) nearest points of the
+//   kept set (self included, sqrt'ed and summed in ascending order), cloud mean and Bessel std
+//   as sequential sums in index order, keep 0 < d < mean + 2 std.
+struct BpCells {
+    const unsigned long long *pc;
+    const int *bs, *bl;
+    unsigned nb;
+    int cmax[3];
+};
+
+// calls fn(j) for every point j in cell (x, y, z) (no-op outside the grid)
+template <typename Fn>
+__device__ __forceinline__ void bp_cell_points(const BpCells &g, int x, int y, int z, Fn &&fn)
+{
+    if (x < 0 || y < 0 || z < 0 || x > g.cmax[0] || y > g.cmax[1] || z > g.cmax[2]) return;
+    const unsigned long long key = pack3(x, y, z);
+    const unsigned b = mod_mul(bp_hash3(x, y, z), g.nb);
+    for (int k = g.bs[b]; k < g.bs[b + 1]; k++) {
+        const int j = g.bl[k];
+        if (g.pc[j] == key) fn(j);
+    }
+}
+
+// every point j in the (2R+1)^3 block of cells whose Chebyshev ring index is exactly R
+template <typename Fn>
+__device__ __forceinline__ void bp_shell(const BpCells &g, int cx, int cy, int cz, int R, Fn &&fn)
+{
+    for (int dz = -R; dz <= R; dz++)
+        for (int dy = -R; dy <= R; dy++) {
+            const bool edge = dz == -R || dz == R || dy == -R || dy == R;
+            for (int dx = -R; dx <= R; dx += (edge || R == 0) ? 1 : 2 * R) bp_cell_points(g, cx + dx, cy + dy, cz + dz, fn);
+        }
+}
+
+// sorted insert of v into the ascending array a[0..N) (drops the largest)
+template <int N, typename V>
+__device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
+{
+    if (!(v < a[N - 1])) return;
+#pragma unroll
+    for (int q = N - 1; q > 0; q--) {
+        const V prev = a[q - 1];
+        a[q] = (v < prev) ? prev : ((v < a[q]) ? v : a[q]);
+    }
+    a[0] = (v < a[0]) ? v : a[0];
+}
+
+template <int N, typename V>
+__device__ __forceinline__ V select_at(const V (&a)[N], int i)
+{
+    V r = a[0];
+#pragma unroll
+    for (int q = 1; q < N; q++) r = (q == i) ? a[q] : r;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_bp_denoise(
+    const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
+    const double *__restrict__ vpts, unsigned long long *__restrict__ pcell, int *__restrict__ pbkt,
+    int *__restrict__ bcnt, int *__restrict__ bstart, int *__restrict__ blist, int *__restrict__ ncnt,
+    int *__restrict__ par, int *__restrict__ root, int *__restrict__ rnk, int *__restrict__ lab,
+    int *__restrict__ ccnt, int *__restrict__ sidx, double *__restrict__ avg, float *__restrict__ qpts,
+    int *__restrict__ slot_m, int *__restrict__ slot_ns, float *__restrict__ slot_box)
+{
+    __shared__ double red[24];
+    __shared__ double s_avg[kBpStage];
+    __shared__ double s_thr;
+    __shared__ float fred[24];
+    __shared__ int ws[4];
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+        const int base = slot_pix[s], n = slot_nv[s];
+        const double *P = vpts + 3 * static_cast<size_t>(base);
+        unsigned long long *pc = pcell + base;
+        int *pb = pbkt + base, *bc = bcnt + 2 * static_cast<size_t>(base), *bs = bstart + 2 * static_cast<size_t>(base) + s;
+        int *bl = blist + base, *nc = ncnt + base, *pa = par + base, *ro = root + base, *rk = rnk + base;
+        int *lb = lab + base, *cc = ccnt + base + s, *si = sidx + base;
+        double *av = avg + base;
+        const unsigned nb = 2u * static_cast<unsigned>(n);
+        // 1. bounding box -> grid origin and cell range
+        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int i = t; i < n; i += 256)
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                mn[c] = fmin(mn[c], P[3 * i + c]);
+                mx[c] = fmax(mx[c], P[3 * i + c]);
+            }
+        block_minmax3(mn, mx, red);
+        BpCells g;
+        g.pc = pc;
+        g.bs = bs;
+        g.bl = bl;
+        g.nb = nb;
+#pragma unroll
+        for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
+        // 2. cells, bucket counts; class counters cleared
+        for (int i = t; i < n; i += 256) {
+            int cxyz[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) cxyz[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
+            pc[i] = pack3(cxyz[0], cxyz[1], cxyz[2]);
+            const unsigned b = mod_mul(bp_hash3(cxyz[0], cxyz[1], cxyz[2]), nb);
+            pb[i] = static_cast<int>(b);
+            atomicAdd(&bc[b], 1);
+        }
+        for (int i = t; i <= n; i += 256) cc[i] = 0;
+        __syncthreads();
+        // 3. bucket starts
+        {
+            int carry = 0;
+            for (int b0 = 0; b0 < static_cast<int>(nb); b0 += 256) {
+                const int b = b0 + t;
+                const int v = b < static_cast<int>(nb) ? ld_agent(&bc[b]) : 0;
+                int tot;
+                const int ex = block_excl_scan<256>(v, ws, tot);
+                if (b < static_cast<int>(nb)) bs[b] = carry + ex;
+                carry += tot;
+            }
+            if (t == 0) bs[nb] = carry;
+        }
+        __syncthreads();
+        // 4. counting-sort scatter (bucket counters return to zero)
+        for (int i = t; i < n; i += 256) {
+            const int b = pb[i];
+            bl[bs[b] + atomicSub(&bc[b], 1) - 1] = i;
+        }
+        __syncthreads();
+        auto cell_of = [&](int i, int &x, int &y, int &z) {
+            const unsigned long long k = pc[i];
+            x = static_cast<int>(k >> 42);
+            y = static_cast<int>((k >> 21) & 0x1FFFFF);
+            z = static_cast<int>(k & 0x1FFFFF);
+        };
+        // 5. eps-neighbour counts (self included) -> core
+        for (int i = t; i < n; i += 256) {
+            int x, y, z;
+            cell_of(i, x, y, z);
+            int cnt = 0;
+            const double *pi = P + 3 * i;
+            for (int R = 0; R <= 1; R++)
+                bp_shell(g, x, y, z, R, [&](int j) { cnt += bp_d2(pi, P + 3 * j) < pr.eps2 ? 1 : 0; });
+            nc[i] = cnt;
+            pa[i] = i;
+        }
+        __syncthreads();
+        // 6. connected core points (union-find, root = smallest index)
+        for (int i = t; i < n; i += 256) {
+            if (nc[i] < pr.minpts) continue;
+            int x, y, z;
+            cell_of(i, x, y, z);
+            const double *pi = P + 3 * i;
+            for (int R = 0; R <= 1; R++)
+                bp_shell(g, x, y, z, R, [&](int j) {
+                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) uf_unite(pa, i, j);
+                });
+        }
+        __syncthreads();
+        // 7. clusters numbered in order of their smallest point
+        {
+            int carry = 0;
+            for (int i0 = 0; i0 < n; i0 += 256) {
+                const int i = i0 + t;
+                int isr = 0;
+                if (i < n && nc[i] >= pr.minpts) {
+                    const int r = uf_find(pa, i);
+                    ro[i] = r;
+                    isr = r == i ? 1 : 0;
+                }
+                int tot;
+                const int ex = block_excl_scan<256>(isr, ws, tot);
+                if (isr) rk[i] = carry + ex;
+                carry += tot;
+            }
+        }
+        __syncthreads();
+        // 8. labels (+1 = the reference's shifted labels, geometry.py:10) and class counts
+        for (int i = t; i < n; i += 256) {
+            int l;
+            if (nc[i] >= pr.minpts) {
+                l = rk[ro[i]];
+            } else {
+                int x, y, z;
+                cell_of(i, x, y, z);
+                const double *pi = P + 3 * i;
+                int mr = INT_MAX;
+                for (int R = 0; R <= 1; R++)
+                    bp_shell(g, x, y, z, R, [&](int j) {
+                        if (nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) mr = min(mr, ro[j]);
+                    });
+                l = mr == INT_MAX ? -1 : rk[mr];
+            }
+            lb[i] = l;
+            atomicAdd(&cc[l + 1], 1);
+        }
+        __syncthreads();
+        // 9. class filter (geometry.py:15-20): the kept set S in index order
+        const double lim = pr.frac * static_cast<double>(n);
+        int m = 0;
+        for (int i0 = 0; i0 < n; i0 += 256) {
+            const int i = i0 + t;
+            const int keep = (i < n && !(static_cast<double>(ld_agent(&cc[lb[i] + 1])) < lim)) ? 1 : 0;
+            int tot;
+            const int ex = block_excl_scan<256>(keep, ws, tot);
+            if (keep) si[m + ex] = i;
+            if (i < n) nc[i] = keep ? (nc[i] | (1 << 30)) : (nc[i] & ~(1 << 30));
+            m += tot;
+        }
+        __syncthreads();
+        // 10. k nearest kept points
+        const int kk = min(pr.knn, m);
+        const int rmax = max(g.cmax[0], max(g.cmax[1], g.cmax[2]));
+        for (int r = t; r < m; r += 256) {
+            const int i = si[r];
+            int x, y, z;
+            cell_of(i, x, y, z);
+            const double *pi = P + 3 * i;
+            double best[kBpKnnMax];
+#pragma unroll
+            for (int q = 0; q < kBpKnnMax; q++) best[q] = DBL_MAX;
+            int found = 0;
+            for (int R = 0;; R++) {
+                bp_shell(g, x, y, z, R, [&](int j) {
+                    if (nc[j] & (1 << 30)) {
+                        sorted_insert(best, bp_d2(pi, P + 3 * j));
+                        found++;
+                    }
+                });
+                const double reach = static_cast<double>(R) * pr.ce;
+                if (found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9)) break;
+                if (R > rmax) break;
+            }
+            double sum = 0.0;
+#pragma unroll
+            for (int q = 0; q < kBpKnnMax; q++)
+                if (q < kk) sum = sum + sqrt(best[q]);
+            av[r] = sum / static_cast<double>(kk);
+        }
+        __syncthreads();
+        // 11. cloud mean and Bessel std: sequential sums in index order (std::accumulate)
+        {
+            double mean = 0.0, sq = 0.0;
+            for (int pass = 0; pass < 2; pass++) {
+                for (int c0 = 0; c0 < m; c0 += kBpStage) {
+                    const int cn = min(kBpStage, m - c0);
+                    for (int x = t; x < cn; x += 256) s_avg[x] = av[c0 + x];
+                    __syncthreads();
+                    if (t == 0) {
+                        for (int x = 0; x < cn; x++) {
+                            const double a = s_avg[x];
+                            if (pass == 0) {
+                                if (a > 0) mean = mean + a;
+                            } else {
+                                sq = sq + (a > 0 ? (a - mean) * (a - mean) : 0.0);
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+                if (pass == 0 && t == 0) mean = mean / static_cast<double>(m);
+            }
+            if (t == 0) {
+                const double sd = sqrt(sq / static_cast<double>(m - 1));
+                s_thr = mean + pr.std_ratio * sd;
+            }
+        }
+        __syncthreads();
+        const double thr = s_thr;
+        // 12. survivors -> float32 mask points (:112) and their float32 AABB (:59-61)
+        int ns = 0;
+        float flo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, fhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int r0 = 0; r0 < m; r0 += 256) {
+            const int r = r0 + t;
+            const int keep = (r < m && av[r] > 0 && av[r] < thr) ? 1 : 0;
+            int tot;
+            const int ex = block_excl_scan<256>(keep, ws, tot);
+            if (keep) {
+                const int i = si[r];
+                float *q = qpts + 3 * (static_cast<size_t>(base) + ns + ex);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    q[c] = static_cast<float>(P[3 * i + c]);
+                    flo[c] = fminf(flo[c], q[c]);
+                    fhi[c] = fmaxf(fhi[c], q[c]);
+                }
+            }
+            ns += tot;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float a = flo[c], b = fhi[c];
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                a = fminf(a, __shfl_xor(a, d, 64));
+                b = fmaxf(b, __shfl_xor(b, d, 64));
+            }
+            if (lane == 0) {
+                fred[c * 4 + wv] = a;
+                fred[12 + c * 4 + wv] = b;
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            slot_m[s] = m;
+            slot_ns[s] = ns;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                slot_box[6 * s + c] = fminf(fminf(fred[c * 4], fred[c * 4 + 1]), fminf(fred[c * 4 + 2], fred[c * 4 + 3]));
+                slot_box[6 * s + 3 + c] =
+                    fmaxf(fmaxf(fred[12 + c * 4], fred[12 + c * 4 + 1]), fmaxf(fred[12 + c * 4 + 2], fred[12 + c * 4 + 3]));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// (a5-a7) crop + ball query + coverage + neighbour set, workgroup per slot (persistent grid)
+// ---------------------------------------------------------------------------------------------
+// For every float32 mask point q: the scene points of the 27 grid cells around q that lie strictly
+// inside the mask's float32 AABB (crop_scene_points, :59-66) and have
+// fmaf(dz, dz, fmaf(dy, dy, dx*dx)) < r^2 (pytorch3d ball_query, u4); the first K of them in scene
+// index order (= crop order, :38,123-128) are accepted.  Accepted ids are OR'ed into the block's
+// private bitmap over the scene; coverage = #q with an accepted neighbour / #q (:143); a kept mask
+// (:145) emits its set in ascending order through a bump allocator into tmp.
+__global__ __launch_bounds__(256) void k_bp_query(
+    const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_ns,
+    const float *__restrict__ slot_box, const float *__restrict__ qpts, BpDev pr, const float4 *__restrict__ gpts,
+    const int *__restrict__ gidx, const unsigned long long *__restrict__ gcell, const int *__restrict__ gstart,
+    unsigned gnb, unsigned long long *__restrict__ bm, int PW, int *__restrict__ tmp, int tmp_cap,
+    int *__restrict__ tmp_top, int *__restrict__ slot_nn, int *__restrict__ slot_toff, int *__restrict__ slot_cov,
+    int *__restrict__ ovf)
+{
+    __shared__ int s_lo, s_hi, s_cov, s_base;
+    __shared__ int ws[4];
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id();
+    unsigned long long *mb = bm + static_cast<size_t>(blockIdx.x) * PW;
+    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+        const int ns = slot_ns[s];
+        if (ns < pr.few) {  // :109 (uniform)
+            if (t == 0) {
+                slot_nn[s] = -1;
+                slot_cov[s] = 0;
+                slot_toff[s] = 0;
+            }
+            continue;
+        }
+        const int base = slot_pix[s];
+        float lo[3], hi[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            lo[c] = slot_box[6 * s + c];
+            hi[c] = slot_box[6 * s + 3 + c];
+        }
+        if (t == 0) {
+            s_lo = INT_MAX;
+            s_hi = -1;
+            s_cov = 0;
+        }
+        __syncthreads();
+        int wlo = INT_MAX, whi = -1, cov = 0;
+        for (int r = t; r < ns; r += 256) {
+            const float *q = qpts + 3 * (static_cast<size_t>(base) + r);
+            const float qx = q[0], qy = q[1], qz = q[2];
+            const int cx = scene_cell(qx, pr.scene_inv), cy = scene_cell(qy, pr.scene_inv),
+                      cz = scene_cell(qz, pr.scene_inv);
+            int best[kBpBallMax];
+#pragma unroll
+            for (int x = 0; x < kBpBallMax; x++) best[x] = INT_MAX;
+            for (int dz = -1; dz <= 1; dz++)
+                for (int dy = -1; dy <= 1; dy++)
+                    for (int dx = -1; dx <= 1; dx++) {
+                        const unsigned long long key = pack3(cx + dx, cy + dy, cz + dz);
+                        const unsigned b = mod_mul(bp_hash3(cx + dx, cy + dy, cz + dz), gnb);
+                        for (int k = gstart[b]; k < gstart[b + 1]; k++) {
+                            if (gcell[k] != key) continue;
+                            const float4 p = gpts[k];
+                            if (!(p.x > lo[0] && p.x < hi[0] && p.y > lo[1] && p.y < hi[1] && p.z > lo[2] && p.z < hi[2]))
+                                continue;
+                            const float ex = qx - p.x, ey = qy - p.y, ez = qz - p.z;
+                            const float d2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, __fmul_rn(ex, ex)));
+                            if (d2 < pr.r2) sorted_insert(best, gidx[k]);
+                        }
+                    }
+            int got = 0;
+#pragma unroll
+            for (int x = 0; x < kBpBallMax; x++) {
+                if (x < pr.kball && best[x] != INT_MAX) {
+                    const int id = best[x];
+                    atomicOr(&mb[id >> 6], 1ull << (id & 63));
+                    wlo = min(wlo, id >> 6);
+                    whi = max(whi, id >> 6);
+                    got = 1;
+                }
+            }
+            cov += got;
+        }
+        wlo = wave_min_i(wlo);
+        whi = wave_max_i(whi);
+        cov = wave_sum(cov);
+        if (lane == 0) {
+            atomicMin(&s_lo, wlo);
+            atomicMax(&s_hi, whi);
+            atomicAdd(&s_cov, cov);
+        }
+        __syncthreads();
+        const int covered = s_cov, wl = s_lo, wh = s_hi;
+        const bool kept = !(static_cast<double>(covered) / static_cast<double>(ns) < pr.cov);
+        const int RW = wh >= wl ? wh - wl + 1 : 0;
+        const int per = (RW + 255) / 256;
+        const int w0 = wl + t * per, w1 = min(wl + RW, w0 + per);
+        int mine = 0;
+        if (kept)
+            for (int w = w0; w < w1; w++) mine += __popcll(__hip_atomic_load(&mb[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        int tot;
+        int pos = block_excl_scan<256>(mine, ws, tot);
+        if (t == 0) {
+            int b0 = 0;
+            if (kept) {
+                b0 = atomicAdd(tmp_top, tot);
+                if (b0 + tot > tmp_cap) atomicOr(ovf, 1);
+            }
+            s_base = b0;
+            slot_nn[s] = kept ? tot : -1;
+            slot_toff[s] = b0;
+            slot_cov[s] = covered;
+        }
+        __syncthreads();
+        const int b0 = s_base;
+        const bool room = kept && b0 + tot <= tmp_cap;
+        for (int w = w0; w < w1; w++) {
+            unsigned long long v = __hip_atomic_load(&mb[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mb[w] = 0ull;  // the bitmap returns to zero
+            if (!room) continue;
+            while (v) {
+                const int bt = __ffsll(static_cast<long long>(v)) - 1;
+                v &= v - 1;
+                tmp[b0 + pos++] = (w << 6) + bt;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// kept masks -> output CSR (one wave per slot)
+__global__ __launch_bounds__(256) void k_bp_emit(const int *__restrict__ dNS, const int *__restrict__ slot_frame,
+                                                 const int *__restrict__ slot_id, const int *__restrict__ slot_nn,
+                                                 const int *__restrict__ slot_toff, const int *__restrict__ midx,
+                                                 const int *__restrict__ moff, const int *__restrict__ tmp,
+                                                 int *__restrict__ out_col, int *__restrict__ out_label,
+                                                 int *__restrict__ out_off, int *__restrict__ out_pts)
+{
+    const int NS = *dNS;
+    const int lane = lane_id();
+    for (int s = (blockIdx.x * 256 + threadIdx.x) >> 6; s < NS; s += gridDim.x * 4) {
+        const int nn = slot_nn[s];
+        if (nn < 0) continue;
+        const int g = midx[s], o = moff[s], src = slot_toff[s];
+        if (lane == 0) {
+            out_col[g] = slot_frame[s];
+            out_label[g] = slot_id[s];
+            out_off[g] = o;
+        }
+        for (int x = lane; x < nn; x += 64) out_pts[o + x] = tmp[src + x];
+    }
+}
+
+// per-slot nn >= 0 flags and sizes for the output scan
+__global__ __launch_bounds__(256) void k_bp_keepflags(const int *__restrict__ dNS, const int *__restrict__ slot_nn,
+                                                      int *__restrict__ kflag, int *__restrict__ ksize)
+{
+    const int NS = *dNS;
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < NS; s += gridDim.x * 256) {
+        const int nn = slot_nn[s];
+        kflag[s] = nn >= 0 ? 1 : 0;
+        ksize[s] = nn > 0 ? nn : 0;
+    }
+}
+
+}  // namespace mc

@@ -1,0 +1,131 @@
+"""S1 HIP back-projection (mc_backproject) against the reference's own glue
+(golden fixtures, tests/golden/make_s1_golden.py) and the CPU restatement
+(oracle/s1_oracle.c).  Bit-exact: the outputs are integer sets; the float
+steps in between follow the same rounding as the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+# oracle stats columns: id npix nvox ndbscan nsor ncand ncovered nneighbors kept
+# device stats columns: frame id npix nvox ndbscan nsor -1 ncovered nneighbors kept
+CMP_COLS = [(1, 0), (2, 1), (3, 2), (4, 3), (5, 4), (7, 6), (8, 7), (9, 8)]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from maskclustering_amd import _native
+    return _native.Context(0)
+
+
+def _run(ctx, scene, depth, seg, K, T):
+    ctx.set_points(np.asarray(scene, np.float64).astype(np.float32))
+    ctx.backproject(depth, seg, K, T)
+    return ctx.bp_masks()
+
+
+def _check_against_oracle(ctx, fr, frames=None):
+    from oracle import oracle
+    idx = list(range(fr.num_frames)) if frames is None else frames
+    col, lab, off, pts = _run(ctx, fr.scene_points, fr.depth[idx], fr.seg[idx], fr.intrinsics[idx], fr.poses[idx])
+    st = ctx.bp_candidates()
+    scene = fr.scene_points.astype(np.float32)
+    g = 0
+    row = 0
+    for c, f in enumerate(idx):
+        ol, oo, op, ost = oracle.s1_frame(scene, fr.depth[f], fr.seg[f], fr.intrinsics[f], fr.poses[f])
+        big = ost[ost[:, 1] >= 25]
+        dev = st[st[:, 0] == c]
+        assert len(dev) == len(big), f"frame {f}: candidates {len(dev)} vs {len(big)}"
+        for dc, oc in CMP_COLS:
+            np.testing.assert_array_equal(dev[:, dc], big[:, oc], err_msg=f"frame {f} stat column {dc}")
+        row += len(dev)
+        for k in range(len(ol)):
+            assert col[g] == c and lab[g] == ol[k], (f, k)
+            np.testing.assert_array_equal(pts[off[g]:off[g + 1]], op[oo[k]:oo[k + 1]], err_msg=f"frame {f} id {ol[k]}")
+            g += 1
+    assert g == len(col)
+
+
+@pytest.mark.parametrize("name", ["s1_tiny", "s1_dense"])
+def test_backproject_matches_reference_glue(ctx, name):
+    z = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    col, lab, off, pts = _run(ctx, z["in_scene"], z["in_depth"], z["in_seg"], z["in_intrinsics"], z["in_poses"])
+    fo = z["out_frame_off"]
+    np.testing.assert_array_equal(lab, z["out_labels"])
+    np.testing.assert_array_equal(np.diff(fo), np.bincount(col, minlength=len(fo) - 1))
+    np.testing.assert_array_equal(off, z["out_off"])
+    np.testing.assert_array_equal(pts, z["out_pts"])
+
+
+def test_backproject_edge_frames(ctx):
+    """inf pose, frames without ids / with tiny masks, ids over invalid depth,
+    and the DEPTH_TRUNC pixel that makes the reference raise IndexError."""
+    from maskclustering_amd._native import McError, MC_ERR_INVALID
+    z = dict(np.load(os.path.join(GOLDEN, "s1_edge.npz")))
+    bad = int(np.nonzero(z["out_err"])[0][0])
+    with pytest.raises(McError) as e:
+        _run(ctx, z["in_scene"], z["in_depth"], z["in_seg"], z["in_intrinsics"], z["in_poses"])
+    assert e.value.code == MC_ERR_INVALID and f"frame {bad}" in str(e.value)
+    assert ctx.bp_info().error_frame == bad
+    keep = [f for f in range(len(z["in_depth"])) if not z["out_err"][f]]
+    col, lab, off, pts = _run(ctx, z["in_scene"], z["in_depth"][keep], z["in_seg"][keep], z["in_intrinsics"][keep],
+                              z["in_poses"][keep])
+    fo = z["out_frame_off"]
+    g = 0
+    for c, f in enumerate(keep):
+        for k in range(fo[f], fo[f + 1]):
+            assert col[g] == c and lab[g] == z["out_labels"][k]
+            np.testing.assert_array_equal(pts[off[g]:off[g + 1]], z["out_pts"][z["out_off"][k]:z["out_off"][k + 1]])
+            g += 1
+    assert g == len(col)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_backproject_stages_match_oracle(ctx, seed):
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=seed)
+    _check_against_oracle(ctx, fr)
+
+
+def test_backproject_dense_frames_match_oracle(ctx):
+    """640x480-like pixel density: several pixels per voxel, larger masks."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
+    _check_against_oracle(ctx, fr)
+
+
+def test_backproject_batched_equals_single(ctx, monkeypatch):
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=2)
+    a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    monkeypatch.setenv("MC_BP_BATCH_PIXELS", str(3 * fr.depth.shape[1] * fr.depth.shape[2]))
+    b = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_end_to_end_matches_oracle(ctx):
+    """S1 on the device feeding S2-S6 on the device == the oracle's S1 feeding its S2-S6."""
+    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    from oracle import oracle
+    from golden_compare import assert_matches
+    fr = make_frames_shape("small", seed=3)
+    cfg = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
+               contained_threshold=0.8)
+    m = oracle.s1_scene(fr)
+    want = oracle.run(fr.num_points, fr.num_frames, m["mask_col"], m["mask_label"], m["mask_off"], m["mask_pts"], **cfg)
+    run = GraphRun(0, ctx=ctx)
+    ctx.set_points(fr.scene_points.astype(np.float32))
+    ctx.backproject(fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    col, lab, off, pts = ctx.bp_masks()
+    run.P, run.F = fr.num_points, fr.num_frames
+    run.mask_col, run.mask_label = col, lab
+    ctx.use_backprojection()
+    run.step(**cfg)
+    assert_matches(run.canonical(), want)
