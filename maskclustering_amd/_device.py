@@ -1,0 +1,75 @@
+"""Process-wide device context of the reference-API modules (graph/, utils/).
+
+The reference keeps its tensors on the current CUDA device (``.cuda()``;
+``run.py:43`` pins one GPU per process with CUDA_VISIBLE_DEVICES), so the
+drop-in modules use one libmcgraph context on ``torch.cuda.current_device()``
+(device 0 when torch is absent), created on first use.  There is no CPU
+fallback: without the built library or a GPU the first call raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native
+
+_ctx = None
+_points_key = None
+
+
+def context() -> _native.Context:
+    global _ctx
+    if _ctx is None:
+        dev = 0
+        try:
+            import torch
+            if torch.cuda.is_available():
+                dev = torch.cuda.current_device()
+        except ImportError:
+            pass
+        _ctx = _native.Context(dev)
+    return _ctx
+
+
+def as_numpy(x) -> np.ndarray:
+    if hasattr(x, "detach"):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def set_scene_points(scene_points) -> int:
+    """Upload the scene points as float32 (construction.py:37) once per distinct array."""
+    global _points_key
+    ctx = context()
+    if hasattr(scene_points, "data_ptr") and getattr(scene_points, "is_cuda", False) \
+            and scene_points.dtype.__str__() == "torch.float32" and scene_points.is_contiguous():
+        key = ("dev", scene_points.data_ptr(), tuple(scene_points.shape), scene_points._version)
+        if key != _points_key:
+            ctx.set_points(device_ptr=scene_points.data_ptr(), num_points=int(scene_points.shape[0]))
+            _points_key = key
+        return int(scene_points.shape[0])
+    pts = np.ascontiguousarray(as_numpy(scene_points), dtype=np.float32).reshape(-1, 3)
+    key = ("host", pts.shape, hash(pts.tobytes()))
+    if key != _points_key:
+        ctx.set_points(pts)
+        _points_key = key
+    return len(pts)
+
+
+def intrinsics_tuple(intr) -> np.ndarray:
+    """fx, fy, cx, cy from an Open3D PinholeCameraIntrinsic (dataset/*.py:get_intrinsics),
+    a 3x3 / 4x4 matrix, or a 4-vector."""
+    if hasattr(intr, "get_focal_length"):
+        fx, fy = intr.get_focal_length()
+        cx, cy = intr.get_principal_point()
+        return np.array([fx, fy, cx, cy], np.float64)
+    if hasattr(intr, "intrinsic_matrix"):
+        intr = np.asarray(intr.intrinsic_matrix)
+    a = np.asarray(intr, np.float64)
+    if a.shape == (4,):
+        return a
+    return np.array([a[0, 0], a[1, 1], a[0, 2], a[1, 2]], np.float64)
+
+
+def bits_to_bool(words: np.ndarray, n: int) -> np.ndarray:
+    from .pipeline import bits_to_bool as b2b
+    return b2b(words, n)

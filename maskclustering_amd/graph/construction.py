@@ -1,0 +1,203 @@
+"""Drop-in for the reference's ``graph/construction.py`` (S1-S5).
+
+``mask_graph_construction(args, scene_points, frame_list, dataset)`` keeps the
+reference's signature and return value (construction.py:7-20):
+``(nodes, observer_num_thresholds, mask_point_clouds, point_frame_matrix)``.
+Every frame is back-projected and the graph is built on the device in one
+pass (mc_backproject + mc_graph_build); the host only stacks the dataset's
+per-frame arrays and rebuilds the Python containers the caller reads:
+
+* ``nodes``: one ``Node`` per non-under-segmented mask in global order
+  (init_nodes, :66-78), ``node_info = (0, i)``, ``point_ids`` aliasing the
+  mask's set in ``mask_point_clouds`` like the reference;
+* ``observer_num_thresholds``: ``np.float32`` values or the int 1 (:88-95);
+* ``mask_point_clouds``: ``{f"{frame_id}_{mask_id}": set}`` (:57);
+* ``point_frame_matrix``: ``np.bool_`` [P, F] (:40,52).
+
+The other public functions of the reference module are provided with the same
+signatures (build_point_in_mask_matrix, process_masks, init_nodes,
+get_observer_num_thresholds); they run the same device stages.
+Errors follow the reference: IndexError for a DEPTH_TRUNC depth pixel and for
+an empty observer-count list (np.percentile of an empty array, :89).
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+
+from .. import _device
+from .._native import MC_ERR_EMPTY_OBSERVERS, MC_ERR_INVALID, McError
+from ..pipeline import bits_to_bool, bool_to_bits
+from ..utils import mask_backprojection as _mb
+from .node import Node
+
+_tokens = itertools.count(1)
+
+
+class GraphHandle:
+    """Identifies the device graph a level-0 node list came from (fast S6 path)."""
+
+    def __init__(self, token, num_nodes, num_frames, num_masks, num_points):
+        self.token = token
+        self.num_nodes = num_nodes
+        self.num_frames = num_frames
+        self.num_masks = num_masks
+        self.num_points = num_points
+
+
+_current = {"token": None}
+
+
+def _stack_frames(frame_list, dataset):
+    depth, seg, K, T = [], [], [], []
+    for frame_id in frame_list:
+        depth.append(np.asarray(dataset.get_depth(frame_id), np.float32))
+        seg.append(_device.as_numpy(dataset.get_segmentation(frame_id, align_with_depth=True)).astype(np.uint8))
+        K.append(_device.intrinsics_tuple(dataset.get_intrinsics(frame_id)))
+        T.append(np.asarray(dataset.get_extrinsic(frame_id), np.float64).reshape(4, 4))
+    return np.stack(depth), np.stack(seg), np.stack(K), np.stack(T)
+
+
+def _backproject_all(scene_points, frame_list, dataset):
+    ctx = _device.context()
+    _device.set_scene_points(scene_points)
+    if len(frame_list) == 0:
+        ctx.backproject(np.zeros((0, 1, 1), np.float32), np.zeros((0, 1, 1), np.uint8), np.zeros((0, 4)),
+                        np.zeros((0, 4, 4)), _mb.params())
+        return ctx
+    depth, seg, K, T = _stack_frames(frame_list, dataset)
+    try:
+        ctx.backproject(depth, seg, K, T, _mb.params())
+    except McError as e:
+        if e.code == MC_ERR_INVALID and "depth_trunc" in str(e):
+            raise IndexError(str(e)) from e
+        raise
+    return ctx
+
+
+def _mask_sets(ctx, frame_list):
+    col, lab, off, pts = ctx.bp_masks()
+    gl = [(frame_list[c], np.uint8(m)) for c, m in zip(col.tolist(), lab.tolist())]
+    mpc = {}
+    for g, (fid, mid) in enumerate(gl):
+        mpc[f"{fid}_{mid}"] = set(pts[off[g]:off[g + 1]].tolist())
+    return gl, mpc
+
+
+def _thresholds(thr, isint):
+    return [1 if i else np.float32(t) for t, i in zip(thr.tolist(), isint.tolist())]
+
+
+def _build(args, scene_points, frame_list, dataset):
+    _current["token"] = None  # the device graph is about to be replaced
+    ctx = _backproject_all(scene_points, frame_list, dataset)
+    gl_in, mpc = _mask_sets(ctx, frame_list)
+    ctx.use_backprojection()
+    ctx.build(args.mask_visible_threshold, args.contained_threshold, args.undersegment_filter_threshold)
+    gi = ctx.graph_info()
+    # frames whose union is empty are skipped (construction.py:50-51): global list = kept input masks
+    gidx = ctx.global_masks(gi.num_masks)
+    gl = [gl_in[i] for i in gidx.tolist()]
+    return ctx, gi, gl, mpc
+
+
+def mask_graph_construction(args, scene_points, frame_list, dataset):
+    if args.debug:
+        print('start building point in mask matrix')
+    ctx, gi, gl, mpc = _build(args, scene_points, frame_list, dataset)
+    P, F, M = gi.num_points, gi.num_frames, gi.num_masks
+    pfm = bits_to_bool(ctx.point_frame_bits(P, F), F)
+    if gi.threshold_status == MC_ERR_EMPTY_OBSERVERS:
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0")  # np.percentile([]) (:89)
+    thr, isint = ctx.thresholds()
+    vf = bits_to_bool(ctx.visible_frame_bits(M, F), F)
+    c_off, c_idx = ctx.contained(M, gi.num_contained)
+    node0 = ctx.nodes0(gi.num_nodes0)
+    token = next(_tokens)
+    _current["token"] = token
+    handle = GraphHandle(token, len(node0), F, M, P)
+    nodes = []
+    for i, g in enumerate(node0.tolist()):
+        fid, mid = gl[g]
+        n = Node.compact([(fid, mid)], vf[g], c_idx[c_off[g]:c_off[g + 1]], M, mpc[f"{fid}_{mid}"], (0, i), None)
+        n._graph = handle
+        n._level0 = i
+        nodes.append(n)
+    return nodes, _thresholds(thr, isint), mpc, pfm
+
+
+def build_point_in_mask_matrix(args, scene_points, frame_list, dataset):
+    """construction.py:22-64 -> (boundary_points, point_in_mask_matrix, mask_point_clouds,
+    point_frame_matrix, global_frame_mask_list)."""
+    ctx, gi, gl, mpc = _build(args, scene_points, frame_list, dataset)
+    P, F = gi.num_points, gi.num_frames
+    boundary = set(np.nonzero(ctx.boundary(P))[0].tolist())
+    pim = ctx.point_in_mask(P, F).copy()
+    pfm = bits_to_bool(ctx.point_frame_bits(P, F), F)
+    return boundary, pim, mpc, pfm, gl
+
+
+def _set_masks_from_sets(ctx, frame_list, global_frame_mask_list, mask_point_clouds, num_points):
+    col_of = {}
+    for c, fid in enumerate(frame_list):
+        col_of.setdefault(fid, c)
+    cols, labs, lens, chunks = [], [], [], []
+    for fid, mid in global_frame_mask_list:
+        s = np.fromiter(mask_point_clouds[f"{fid}_{mid}"], dtype=np.int64)
+        cols.append(col_of[fid])
+        labs.append(int(mid))
+        lens.append(len(s))
+        chunks.append(s.astype(np.int32))
+    off = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    pts = np.concatenate(chunks) if chunks else np.zeros(0, np.int32)
+    ctx.set_masks(num_points, len(frame_list), cols, labs, off, pts)
+
+
+def process_masks(frame_list, global_frame_mask_list, point_in_mask_matrix, boundary_points, mask_point_clouds, args):
+    """construction.py:137-170 -> (visible_frames [M,F], contained_masks [M,M] float tensors, undersegment ids).
+    The point-in-mask matrix and boundary set are recomputed on the device from the same masks."""
+    import torch
+    ctx = _device.context()
+    _current["token"] = None
+    P = int(np.asarray(point_in_mask_matrix).shape[0])
+    _set_masks_from_sets(ctx, frame_list, global_frame_mask_list, mask_point_clouds, P)
+    ctx.build(args.mask_visible_threshold, args.contained_threshold, args.undersegment_filter_threshold)
+    gi = ctx.graph_info()
+    M, F = gi.num_masks, gi.num_frames
+    vf = bits_to_bool(ctx.visible_frame_bits(M, F), F).astype(np.float32)
+    off, idx = ctx.contained(M, gi.num_contained)
+    cm = np.zeros((M, M), np.float32)
+    cm[np.repeat(np.arange(M), np.diff(off)), idx] = 1.0
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    return (torch.from_numpy(vf).to(dev), torch.from_numpy(cm).to(dev),
+            [int(u) for u in ctx.undersegment(gi.num_undersegment)])
+
+
+def get_observer_num_thresholds(visible_frames):
+    """construction.py:80-96 (observer counts histogrammed on the device)."""
+    vf = _device.as_numpy(visible_frames) > 0
+    ctx = _device.context()
+    try:
+        thr, isint = ctx.observer_thresholds(bool_to_bits(vf), vf.shape[1])
+    except McError as e:
+        if e.code == MC_ERR_EMPTY_OBSERVERS:
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0") from e
+        raise
+    return _thresholds(thr, isint)
+
+
+def init_nodes(global_frame_mask_list, mask_project_on_all_frames, contained_masks, undersegment_mask_ids,
+               mask_point_clouds):
+    """construction.py:66-78."""
+    useg = set(int(u) for u in undersegment_mask_ids)
+    vf = _device.as_numpy(mask_project_on_all_frames) > 0
+    cm = _device.as_numpy(contained_masks) > 0
+    nodes = []
+    for g, (frame_id, mask_id) in enumerate(global_frame_mask_list):
+        if g in useg:
+            continue
+        nodes.append(Node.compact([(frame_id, mask_id)], vf[g], np.nonzero(cm[g])[0], cm.shape[1],
+                                  mask_point_clouds[f'{frame_id}_{mask_id}'], (0, len(nodes)), None))
+    return nodes

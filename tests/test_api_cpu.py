@@ -1,0 +1,54 @@
+"""Host-side logic of the drop-in modules (no GPU): imports under the
+reference's names, the Node record, and the degenerate paths that return
+before any device work."""
+import numpy as np
+import torch
+
+
+def test_modules_expose_reference_names():
+    from maskclustering_amd.graph import construction, iterative_clustering, node
+    from maskclustering_amd.utils import mask_backprojection as mb
+    for f in ("mask_graph_construction", "build_point_in_mask_matrix", "process_masks", "init_nodes",
+              "get_observer_num_thresholds"):
+        assert callable(getattr(construction, f))
+    assert callable(iterative_clustering.iterative_clustering)
+    assert callable(node.Node.create_node_from_list)
+    for f in ("turn_mask_to_point", "frame_backprojection", "get_depth_mask", "crop_scene_points"):
+        assert callable(getattr(mb, f))
+    assert (mb.COVERAGE_THRESHOLD, mb.DISTANCE_THRESHOLD, mb.FEW_POINTS_THRESHOLD, mb.DEPTH_TRUNC) == (0.3, 0.01, 25, 20)
+
+
+def test_node_merge_matches_reference_semantics():
+    """graph/node.py:24-37: OR of rows, concatenated mask lists, union of point sets."""
+    from maskclustering_amd.graph.node import Node
+    a = Node([(0, 1)], torch.tensor([1., 0, 0, 1]), torch.tensor([0., 1, 0]), {1, 2}, (0, 0), None)
+    b = Node.compact([(10, 3)], np.array([0, 1, 0, 1], bool), np.array([2]), 3, {2, 5}, (0, 1), None)
+    m = Node.create_node_from_list([a, b], (1, 0))
+    assert m.mask_list == [(0, 1), (10, 3)]
+    assert m.point_ids == {1, 2, 5}
+    assert m.son_node_info == {(0, 0), (0, 1)}
+    assert m.visible_frame.cpu().tolist() == [1., 1., 0., 1.]
+    assert m.contained_mask.cpu().tolist() == [0., 1., 1.]
+    assert m.node_info == (1, 0)
+
+
+def test_iterative_clustering_without_thresholds_returns_nodes():
+    from maskclustering_amd.graph.iterative_clustering import iterative_clustering
+    nodes = [object(), object()]
+    assert iterative_clustering(nodes, [], 0.9, False) is nodes
+
+
+def test_turn_mask_to_point_inf_pose_returns_early():
+    """mask_backprojection.py:73-74 returns ({}, [], set()) before touching the device."""
+    from maskclustering_amd.utils.mask_backprojection import turn_mask_to_point
+
+    class DS:
+        def get_intrinsics(self, f):
+            return np.array([500.0, 500.0, 32.0, 24.0])
+
+        def get_extrinsic(self, f):
+            T = np.eye(4)
+            T[0, 3] = np.inf
+            return T
+
+    assert turn_mask_to_point(DS(), np.zeros((5, 3)), np.zeros((48, 64), np.uint8), 0) == ({}, [], set())
