@@ -1,11 +1,15 @@
 """Benchmark of the view-consensus graph path on MI355X.
 
 A step = one pass of the hot path over one synthetic ScanNet-shaped scene
-(BASELINE.json configs[1]: ~250 frames, ~240k points, ~15k masks): graph
-construction S2–S5 (point lists, boundary, containment, under-segmentation,
-observer thresholds), iterative clustering S6 (all thresholds) and the final
-per-object point sets — from per-frame mask sets resident in HBM to final
-components + merged bitsets in HBM.
+(BASELINE.json configs[1]: ~250 frames, ~240k points, ~15k masks).
+
+  --variant g   (default) graph construction S2-S5 (point lists, boundary,
+                containment, under-segmentation, observer thresholds),
+                iterative clustering S6 (all thresholds) and the final
+                per-object point sets, from per-frame mask sets resident in
+                HBM to final components + merged bitsets in HBM;
+  --variant e2e the same preceded by S1 back-projection of every frame from
+                depth / segmentation / poses resident in HBM (640x480 frames).
 
 metric: mask-pair consensus counts/sec = Σ_t N_t² (the ordered node pairs whose
 view consensus the reference evaluates, graph/iterative_clustering.py:20-29)
@@ -15,7 +19,7 @@ first metric).  Multi-GPU: one process per GPU, each rank its own scene
 (scene-parallel, the reference's run.py:33-50 pattern): weak scaling, no
 data-path collective.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--shape c2] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant g|e2e] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -34,25 +38,26 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense)
 CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
            contained_threshold=0.8)  # configs/scannet.json
+G_GROUPS = ["s2_point_lists", "s3_masks", "s3_undo_s5", "s4_observer_hist", "s6_columns", "s6_pairs",
+            "s6_components", "s6_merge", "s7_points"]
+BP_GROUPS = ["bp_pixels", "bp_voxel", "bp_denoise", "bp_query"]
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_work(scene, run, F):
-    """Per-launch algorithmic bytes / ops of every timed kernel group."""
-    ctx = run.ctx
+def graph_work(ctx, mask_pts, P, F):
+    """Per-launch algorithmic bytes / ops of the graph kernel groups."""
     gi = ctx.graph_info()
-    P, M, nnz = scene.num_points, gi.num_masks, int(scene.mask_off[-1])
+    M, nnz = gi.num_masks, len(mask_pts)
     FW = (F + 63) // 64
-    deg = np.bincount(scene.mask_pts, minlength=P).astype(np.int64)
+    deg = np.bincount(mask_pts, minlength=P).astype(np.int64)
     bnd = ctx.boundary(P).astype(bool)
-    pts = scene.mask_pts
-    nb = ~bnd[pts]
+    nb = ~bnd[mask_pts]
     # S3: every mask reads its ids (4 B) + boundary flag (1 B); every non-boundary point its
     # offsets (8 B) and list entries (4 B each); writes its contained row + flags.
-    s3_bytes = 8 * M + 5 * nnz + int(np.sum(8 + 4 * deg[pts[nb]])) + 4 * gi.num_contained + 5 * M
+    s3_bytes = 8 * M + 5 * nnz + int(np.sum(8 + 4 * deg[mask_pts[nb]])) + 4 * gi.num_contained + 5 * M
     # S2: read mask ids, write + sort point lists (r/w), offsets, boundary, point-frame bits
     s2_bytes = 4 * nnz + 2 * 4 * nnz + 2 * 4 * nnz + 8 * P + P + 8 * P * FW
     # S4: dense-equivalent observer GEMM VF·VFᵀ (construction.py:84) — 2·M²·F int8 ops
@@ -66,16 +71,122 @@ def algorithmic_work(scene, run, F):
     }
 
 
-def cpu_baseline(scene, threads):
-    from oracle import oracle
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    tm = {}
-    t0 = time.perf_counter()
-    oracle.run(scene.num_points, scene.num_frames, scene.mask_col, scene.mask_label, scene.mask_off,
-               scene.mask_pts, timings=tm, **CFG)
-    wall = time.perf_counter() - t0
-    cpu_s = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
-    return tm, wall, cpu_s
+def bp_work(ctx, F, H, W):
+    """Per-launch algorithmic bytes of the S1 groups: each frame's depth + seg
+    read once and every mask pixel listed once (pixels); every mask pixel's list entry and
+    depth read, every voxel written (voxel); voxels read, float32 mask points written
+    (denoise); mask points read, neighbour ids written (query)."""
+    st = ctx.bp_candidates()
+    npx, nvox, nsor = int(st[:, 2].sum()), int(st[:, 3].sum()), int(st[:, 5].sum())
+    nnbr = int(ctx.bp_info().num_mask_points)
+    return {
+        "bp_pixels": ("hbm", float(5 * F * H * W + 4 * npx)),
+        "bp_voxel": ("hbm", float(8 * npx + 24 * nvox)),
+        "bp_denoise": ("hbm", float(24 * nvox + 12 * nsor)),
+        "bp_query": ("hbm", float(12 * nsor + 4 * nnbr)),
+    }
+
+
+class GraphStep:
+    """--variant g: per-frame mask sets resident in HBM -> final objects."""
+
+    def __init__(self, shape, seed, local):
+        import torch
+        from maskclustering_amd.pipeline import GraphRun
+        from maskclustering_amd.synthetic import SHAPES, make_shape
+        self.scene = make_shape(shape, seed=seed)
+        self.run = GraphRun(local)
+        self.run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.run.set_scene(self.scene)
+        self.groups = G_GROUPS
+        sh = SHAPES[shape]
+        self.workload = (f"{shape}: ScanNet-shaped synthetic scene (SURVEY App. C), P={sh['num_points']} "
+                         f"F={sh['num_frames']}")
+
+    def step(self):
+        self.run.step(**CFG)
+
+    def work(self):
+        s = self.scene
+        return graph_work(self.run.ctx, s.mask_pts, s.num_points, s.num_frames)
+
+    def cpu_baseline(self):
+        from oracle import oracle
+        s = self.scene
+        tm = {}
+        oracle.run(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, timings=tm, **CFG)
+        cpu_s = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
+        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
+                "sample": f"oracle/mcgraph_oracle.c S2-S6 on the same scene (1 full scene, {cpu_s:.2f} s: "
+                          f"S2 {tm['s2']:.2f} S3 {tm['s3']:.2f} S4 {tm['s4']:.2f} S6 {tm['s6']:.2f})",
+                "scene_ms": round(cpu_s * 1e3, 1)}
+
+
+class EndToEndStep:
+    """--variant e2e: depth / seg / poses resident in HBM -> back-projected masks -> final objects."""
+
+    def __init__(self, shape, seed, local):
+        import torch
+        from maskclustering_amd import _native
+        from maskclustering_amd.pipeline import GraphRun
+        from maskclustering_amd.synthetic_frames import make_frames_shape
+        t0 = time.perf_counter()
+        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}")
+        log(f"rendered {fr.num_frames} frames {fr.depth.shape[1]}x{fr.depth.shape[2]} P={fr.num_points} "
+            f"in {time.perf_counter() - t0:.1f} s")
+        self.fr = fr
+        dev = torch.device("cuda", local)
+        self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)  # construction.py:37
+        self.t_depth = torch.from_numpy(fr.depth).to(dev)
+        self.t_seg = torch.from_numpy(fr.seg).to(dev)
+        self.t_K = torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev)
+        self.t_T = torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)
+        self.run = GraphRun(local)
+        self.ctx = self.run.ctx
+        self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+        self.prm = _native.bp_params()
+        self.groups = BP_GROUPS + G_GROUPS
+        F, H, W = fr.depth.shape
+        self.shape = (F, H, W)
+        self.workload = (f"{shape}: ScanNet-shaped synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
+                         f"S1-S6")
+
+    def step(self):
+        self.ctx.backproject(None, None, None, None, self.prm, shape=self.shape,
+                             device_ptrs=(self.t_depth.data_ptr(), self.t_seg.data_ptr(), self.t_K.data_ptr(),
+                                          self.t_T.data_ptr()))
+        self.ctx.use_backprojection()
+        self.run.step(**CFG)
+
+    def work(self):
+        F, H, W = self.shape
+        col, lab, off, pts = self.ctx.bp_masks()
+        w = graph_work(self.ctx, pts, self.fr.num_points, F)
+        w.update(bp_work(self.ctx, F, H, W))
+        return w
+
+    def cpu_baseline(self, budget_s=12.0):
+        """oracle S1 on the first frames (bounded sample, extrapolated per frame) + oracle S2-S6
+        on the full mask set (identical to the device's by the parity tests)."""
+        from oracle import oracle
+        fr = self.fr
+        scene = fr.scene_points.astype(np.float32)
+        t0 = time.perf_counter()
+        k = 0
+        while k < fr.num_frames and time.perf_counter() - t0 < budget_s:
+            oracle.s1_frame(scene, fr.depth[k], fr.seg[k], fr.intrinsics[k], fr.poses[k])
+            k += 1
+        s1 = (time.perf_counter() - t0) / k * fr.num_frames
+        col, lab, off, pts = self.ctx.bp_masks()
+        tm = {}
+        oracle.run(fr.num_points, fr.num_frames, col, lab, off, pts, timings=tm, **CFG)
+        g = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
+        cpu_s = s1 + g
+        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
+                "sample": f"oracle S1 (oracle/s1_oracle.c, 1 thread) timed on {k} of {fr.num_frames} frames and "
+                          f"extrapolated ({s1:.1f} s) + oracle S2-S6 on the full scene ({g:.2f} s)",
+                "scene_ms": round(cpu_s * 1e3, 1)}
 
 
 def main():
@@ -83,6 +194,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--variant", choices=["g", "e2e"], default="g")
     ap.add_argument("--shape", default="c2")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,57 +210,51 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from maskclustering_amd.pipeline import GraphRun
-    from maskclustering_amd.synthetic import SHAPES, make_shape
-
-    scene = make_shape(args.shape, seed=args.seed + rank)  # every rank its own scene (weak scaling)
-    run = GraphRun(local)
-    run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    run.set_scene(scene)
+    # every rank its own scene (weak scaling)
+    runner = (GraphStep if args.variant == "g" else EndToEndStep)(args.shape, args.seed + rank, local)
+    ctx = runner.run.ctx
 
     for _ in range(args.warmup):
-        run.step(**CFG)
+        runner.step()
     torch.cuda.synchronize()
-    ci = run.ctx.cluster_info()
-    sizes = run.ctx.level_sizes(ci.num_iterations)
+    ci = ctx.cluster_info()
+    sizes = ctx.level_sizes(ci.num_iterations)
     pairs_per_step = int(np.sum(sizes[:-1].astype(np.int64) ** 2))
 
     # calibration pass with per-group event timing: find the dominant kernel group
-    groups = ["s2_point_lists", "s3_masks", "s3_undo_s5", "s4_observer_hist", "s6_columns", "s6_pairs",
-              "s6_components", "s6_merge", "s7_points"]
-    run.ctx.reset_kernel_times()
-    run.ctx.set_timing(True)
-    run.step(**CFG)
-    run.ctx.synchronize()
-    calib = {g: run.ctx.kernel_time(g)[0] for g in groups}
-    run.ctx.set_timing(False)
-    work = algorithmic_work(scene, run, scene.num_frames)
+    ctx.reset_kernel_times()
+    ctx.set_timing(True)
+    runner.step()
+    ctx.synchronize()
+    calib = {g: ctx.kernel_time(g)[0] for g in runner.groups}
+    ctx.set_timing(False)
+    work = runner.work()
     dominant = max((g for g in calib if g in work), key=lambda g: calib[g])
     log("calibration (ms):", json.dumps({k: round(v, 4) for k, v in calib.items()}), "dominant:", dominant)
 
     # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant
     # group only (one event pair per step)
-    run.ctx.reset_kernel_times()
-    run.ctx.set_timing_filter(dominant)
-    run.ctx.set_timing(True)
+    ctx.reset_kernel_times()
+    ctx.set_timing_filter(dominant)
+    ctx.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run.step(**CFG)
+        runner.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    run.ctx.set_timing(False)
-    dom_ms, dom_n = run.ctx.kernel_time(dominant)
+    ctx.set_timing(False)
+    dom_ms, dom_n = ctx.kernel_time(dominant)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    gi = run.ctx.graph_info()
+    gi = ctx.graph_info()
     total_pairs = pairs_per_step * args.steps * world
     value = total_pairs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -168,25 +274,18 @@ def main():
     roof["algorithmic_per_launch"] = per_launch
     # HBM bytes per launch of the same kernel group from the committed rocprofv3 PMC passes
     # (scripts/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)
-    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json" if args.variant == "g" else "pmc_traffic_e2e.json")
     if bound == "hbm" and os.path.exists(pmc_path):
         g = json.load(open(pmc_path)).get("groups", {}).get(dominant)
         if g:
             roof["traffic"] = round(g["bytes_per_launch"], 0)
-            roof["traffic_source"] = "profiles/pmc_traffic.json"
+            roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        tm, wall, cpu_s = cpu_baseline(scene, threads)
-        cpu = {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"],
-               "kind": "port",
-               "sample": f"oracle/mcgraph_oracle.c S2-S6 on the same {args.shape} scene (1 full scene, "
-                         f"{cpu_s:.2f} s: S2 {tm['s2']:.2f} S3 {tm['s3']:.2f} S4 {tm['s4']:.2f} S6 {tm['s6']:.2f})",
-               "scene_ms": round(cpu_s * 1e3, 1)}
+        cpu = runner.cpu_baseline()
 
     if rank == 0:
-        shape = SHAPES[args.shape]
         line = {
             "metric": "mask-pair consensus counts/sec (per-scene graph build+cluster)",
             "value": round(value, 1),
@@ -200,10 +299,10 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
-            "config": {"workload": f"{args.shape}: ScanNet-shaped synthetic scene (SURVEY App. C), "
-                                   f"P={shape['num_points']} F={shape['num_frames']} M={gi.num_masks}",
+            "config": {"workload": runner.workload + f" M={gi.num_masks}", "variant": args.variant,
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
+                       "stage_ms": {k: round(v, 4) for k, v in calib.items()},
                        "parallelism": f"scene-parallel x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,

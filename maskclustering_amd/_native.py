@@ -90,6 +90,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same soname as
+    # /opt/rocm's).  Whichever is loaded first serves both, and torch cannot initialise the GPU
+    # on a runtime it was not built with, so torch's is loaded before this library when present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     P = ctypes.POINTER

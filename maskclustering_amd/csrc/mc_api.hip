@@ -1278,7 +1278,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         if (params) prm = *params;
         else mc_bp_params_default(&prm);
         MC_REQUIRE(prm.sor_neighbors >= 1 && prm.sor_neighbors <= mc::kBpKnnMax, MC_ERR_UNSUPPORTED,
-                   "sor_neighbors must be in [1, 32]");
+                   "sor_neighbors must be in [1, 20]");
         MC_REQUIRE(prm.ball_k >= 1 && prm.ball_k <= mc::kBpBallMax, MC_ERR_UNSUPPORTED, "ball_k must be in [1, 32]");
         MC_REQUIRE(prm.voxel_size > 0 && prm.dbscan_eps > 0 && prm.ball_radius > 0, MC_ERR_INVALID, "bad radii");
         hipStream_t s = ctx->stream;
@@ -1384,6 +1384,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_denoise");
+                hipLaunchKernelGGL(mc::k_bp_denoise_lds, dim3(kBpGrid), dim3(mc::kBpLdsT), 0, s, st + BS_NS,
+                                   ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                                   ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
+                                   ctx->d_slot_box.as<float>());
                 hipLaunchKernelGGL(mc::k_bp_denoise, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
                                    ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                                    ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
@@ -1504,6 +1508,16 @@ int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats)
         std::copy(ctx->bp_stats.begin(), ctx->bp_stats.end(), stats);
     });
 }
+
+#ifdef MC_BP_STAMPS
+// diagnostic builds only: read (and clear) k_bp_denoise's per-step clock totals
+int mc_debug_bp_stamps(unsigned long long *out32)
+{
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 32 * 8) != hipSuccess) return MC_ERR_HIP;
+    static const unsigned long long zero[32] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_stamps), zero, 32 * 8) == hipSuccess ? MC_OK : MC_ERR_HIP;
+}
+#endif
 
 int mc_scene_use_backprojection(mc_ctx *ctx)
 {

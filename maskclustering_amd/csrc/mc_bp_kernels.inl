@@ -25,7 +25,7 @@
 namespace mc {
 
 constexpr int kBpBand = 16;        // image rows per (band, frame) block
-constexpr int kBpKnnMax = 32;      // sor_neighbors <= 32
+constexpr int kBpKnnMax = 20;      // sor_neighbors <= 20 (geometry.py:22 uses 20)
 constexpr int kBpBallMax = 32;     // ball_k <= 32
 constexpr int kBpStage = 2048;     // LDS staging of the outlier statistics
 constexpr unsigned long long kEmptyKey = ~0ull;
@@ -420,33 +420,37 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
             sp[3 * t + 1] = p[1];
             sp[3 * t + 2] = p[2];
             __syncthreads();
+            // group lanes by voxel (ballots only), then every group leader of the wave adds its
+            // group's points in lane order to the running sum at once (one round trip per wave)
+            unsigned long long gm = 0;
+            {
+                unsigned long long act = __ballot(vid >= 0);
+                while (act) {
+                    const int L = __ffsll(static_cast<long long>(act)) - 1;
+                    const int kk = __shfl(vid, L, 64);
+                    const unsigned long long m = __ballot(vid == kk);
+                    if (lane == L) gm = m;
+                    act &= ~m;
+                }
+            }
 #pragma unroll
             for (int w = 0; w < 4; w++) {
-                if (wv == w) {
-                    unsigned long long act = __ballot(vid >= 0);
-                    while (act) {
-                        const int L = __ffsll(static_cast<long long>(act)) - 1;
-                        const int kk = __shfl(vid, L, 64);
-                        const unsigned long long m = __ballot(vid == kk);
-                        if (lane == L) {  // AccumulatedPoint::AddPoint, lane (= pixel) order
-                            double ax = ac[4 * kk], ay = ac[4 * kk + 1], az = ac[4 * kk + 2], an = ac[4 * kk + 3];
-                            unsigned long long mm = m;
-                            while (mm) {
-                                const int l = __ffsll(static_cast<long long>(mm)) - 1;
-                                mm &= mm - 1;
-                                const double *q = sp + 3 * (w * 64 + l);
-                                ax = ax + q[0];
-                                ay = ay + q[1];
-                                az = az + q[2];
-                                an = an + 1.0;
-                            }
-                            ac[4 * kk] = ax;
-                            ac[4 * kk + 1] = ay;
-                            ac[4 * kk + 2] = az;
-                            ac[4 * kk + 3] = an;
-                        }
-                        act &= ~m;
+                if (wv == w && gm) {  // AccumulatedPoint::AddPoint, lane (= pixel) order
+                    double ax = ac[4 * vid], ay = ac[4 * vid + 1], az = ac[4 * vid + 2], an = ac[4 * vid + 3];
+                    unsigned long long mm = gm;
+                    while (mm) {
+                        const int l = __ffsll(static_cast<long long>(mm)) - 1;
+                        mm &= mm - 1;
+                        const double *q = sp + 3 * (w * 64 + l);
+                        ax = ax + q[0];
+                        ay = ay + q[1];
+                        az = az + q[2];
+                        an = an + 1.0;
                     }
+                    ac[4 * vid] = ax;
+                    ac[4 * vid + 1] = ay;
+                    ac[4 * vid + 2] = az;
+                    ac[4 * vid + 3] = an;
                 }
                 __syncthreads();
             }
@@ -535,6 +539,577 @@ __device__ __forceinline__ V select_at(const V (&a)[N], int i)
     return r;
 }
 
+// union-find over a workgroup's LDS parent array (root = smallest index)
+constexpr int kBpLdsUF = 8192;
+__device__ __forceinline__ int uf_find_s(volatile int *par, int x)
+{
+    while (true) {
+        const int p = par[x];
+        if (p == x) return x;
+        const int gp = par[p];
+        if (gp == p) return p;
+        par[x] = gp;
+        x = gp;
+    }
+}
+__device__ __forceinline__ void uf_unite_s(int *par, int a, int b)
+{
+    while (true) {
+        a = uf_find_s(par, a);
+        b = uf_find_s(par, b);
+        if (a == b) return;
+        if (a > b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(par + b, b, a) == b) return;
+    }
+}
+
+// Mean of sqrt of the kk smallest of d2(j) over j < m, by one wave: every lane keeps the
+// kBpKnnMax smallest of its strided share, then kk rounds of a wave-wide minimum extract them in
+// ascending order (the order Open3D sums them in).  d2fn(j) gives the j-th squared distance.
+template <typename D2>
+__device__ __forceinline__ double wave_knn_mean(int m, int kk, D2 &&d2fn)
+{
+    const int lane = lane_id();
+    double loc[kBpKnnMax];
+#pragma unroll
+    for (int k = 0; k < kBpKnnMax; k++) loc[k] = DBL_MAX;
+    for (int j = lane; j < m; j += 64) sorted_insert(loc, d2fn(j));
+    double sum = 0.0;
+    for (int k = 0; k < kk; k++) {
+        double v = loc[0];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v = fmin(v, __shfl_xor(v, d, 64));
+        const int win = __ffsll(static_cast<long long>(__ballot(loc[0] == v))) - 1;
+        sum = sum + sqrt(v);
+        if (lane == win) {
+#pragma unroll
+            for (int q = 0; q < kBpKnnMax - 1; q++) loc[q] = loc[q + 1];
+            loc[kBpKnnMax - 1] = DBL_MAX;
+        }
+    }
+    return sum / static_cast<double>(kk);
+}
+
+// mean distance of every kept point to its k nearest kept points (self included): sqrt of the
+// k smallest squared distances, summed in ascending order, / k (Open3D SearchKNN + accumulate)
+template <int N>
+__device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restrict__ P, const int *__restrict__ flag,
+                                       const int *__restrict__ si, int m, int kk, double ce, double *__restrict__ av,
+                                       int t, int *fb, int fb_cap, int *nfb)
+{
+    constexpr int kRingMax = 2;
+    if (t == 0) *nfb = 0;
+    __syncthreads();
+    for (int r = t; r < m; r += 256) {
+        const int i = si[r];
+        const unsigned long long key = g.pc[i];
+        const int x = static_cast<int>(key >> 42), y = static_cast<int>((key >> 21) & 0x1FFFFF),
+                  z = static_cast<int>(key & 0x1FFFFF);
+        const double *pi = P + 3 * i;
+        double best[N];
+#pragma unroll
+        for (int q = 0; q < N; q++) best[q] = DBL_MAX;
+        int found = 0;
+        bool done = false;
+        for (int R = 0; R <= kRingMax && !done; R++) {
+            for (int dz = -R; dz <= R; dz++)
+                for (int dy = -R; dy <= R; dy++) {
+                    const bool edge = dz == -R || dz == R || dy == -R || dy == R;
+                    const int step = (edge || R == 0) ? 1 : 2 * R;
+                    for (int dx = -R; dx <= R; dx += step) {
+                        const int cx = x + dx, cy = y + dy, cz = z + dz;
+                        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) continue;
+                        const unsigned long long ck = pack3(cx, cy, cz);
+                        const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
+                        const int kb = g.bs[b], ke = g.bs[b + 1];
+                        for (int k = kb; k < ke; k++) {
+                            const int j = g.bl[k];
+                            if (g.pc[j] != ck || !(flag[j] & (1 << 30))) continue;
+                            sorted_insert(best, bp_d2(pi, P + 3 * j));
+                            found++;
+                        }
+                    }
+                }
+            const double reach = static_cast<double>(R) * ce;
+            done = found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9);
+        }
+        if (!done) {  // sparse point: every kept point, by a whole wave below
+            const int f = atomicAdd(nfb, 1);
+            if (f < fb_cap) {
+                fb[f] = r;
+                continue;
+            }
+#pragma unroll
+            for (int q = 0; q < N; q++) best[q] = DBL_MAX;
+            for (int q = 0; q < m; q++) sorted_insert(best, bp_d2(pi, P + 3 * si[q]));
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < N; q++)
+            if (q < kk) sum = sum + sqrt(best[q]);
+        av[r] = sum / static_cast<double>(kk);
+    }
+    __syncthreads();
+    const int nf = min(*nfb, fb_cap);
+    for (int f = static_cast<int>(threadIdx.x >> 6); f < nf; f += 4) {
+        const int r = fb[f];
+        const double *pi = P + 3 * si[r];
+        const double mean = wave_knn_mean(m, kk, [&](int j) { return bp_d2(pi, P + 3 * si[j]); });
+        if (lane_id() == 0) av[r] = mean;
+    }
+}
+
+// Diagnostic build only (-DMC_BP_STAMPS): per-step shader-clock totals of k_bp_denoise, summed
+// over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
+#ifdef MC_BP_STAMPS
+__device__ unsigned long long g_bp_stamps[32];
+#define BP_STAMP(k)                                                                      \
+    do {                                                                                 \
+        __syncthreads();                                                                 \
+        if (threadIdx.x == 0) {                                                          \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                \
+            atomicAdd(&g_bp_stamps[k], now_ - stamp_prev);                               \
+            stamp_prev = now_;                                                           \
+        }                                                                                \
+    } while (0)
+#else
+#define BP_STAMP(k) do { } while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// (a4) denoise, LDS-resident variant for slots of <= kBpLdsN voxels (the bulk): the same steps as
+// k_bp_denoise below, with the points cell-sorted into LDS (SoA) so that every neighbourhood scan
+// reads LDS.  Union-find runs over sorted positions; each component is keyed by its smallest
+// original index, which numbers the clusters exactly as k_bp_denoise / Open3D do.
+// ---------------------------------------------------------------------------------------------
+#ifndef MC_ABLATE_BP
+#define MC_ABLATE_BP 0  // timing-only builds: 1 = no kNN, 2 = no DBSCAN union (results wrong)
+#endif
+constexpr int kBpLdsN = 2048;
+constexpr int kBpLdsT = 512;
+constexpr int kBpFbCount = 2 * kBpLdsN + 1;  // index of the fallback counter in sB
+
+template <int NW>
+__device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], double *red)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const double a = wave_min_d(mn[c]), b = wave_max_d(mx[c]);
+        if (lane == 0) {
+            red[c * NW + wv] = a;
+            red[3 * NW + c * NW + wv] = b;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        double a = red[c * NW], b = red[3 * NW + c * NW];
+        for (int w = 1; w < NW; w++) {
+            a = fmin(a, red[c * NW + w]);
+            b = fmax(b, red[3 * NW + c * NW + w]);
+        }
+        mn[c] = a;
+        mx[c] = b;
+    }
+    __syncthreads();
+}
+
+struct BpLdsGrid {
+    const double4 *pt;  // x, y, z, cell key bits (bit 63: kept by the class filter) per sorted position
+    const int *bs;      // bucket starts (2n + 1)
+    unsigned nb;
+    int cmax[3];
+};
+
+constexpr unsigned long long kKeptBit = 1ull << 63;
+
+// fn(q, d2) for every sorted position q of cell (x, y, z) whose key (with `with` bits set) matches;
+// d2 = squared distance from a (u3 order).  Records are read four at a time so their LDS loads overlap.
+template <typename Fn>
+__device__ __forceinline__ void lds_cell(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
+                                         double ay, double az, Fn &&fn)
+{
+    if (x < 0 || y < 0 || z < 0 || x > g.cmax[0] || y > g.cmax[1] || z > g.cmax[2]) return;
+    const unsigned long long key = pack3(x, y, z) | with;
+    const unsigned long long mask = ~0ull ^ (with ? 0ull : kKeptBit);
+    const unsigned b = mod_mul(bp_hash3(x, y, z), g.nb);
+    const int e = g.bs[b + 1];
+    int q = g.bs[b];
+    for (; q + 4 <= e; q += 4) {
+        double4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) p[u] = g.pt[q + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if ((static_cast<unsigned long long>(__double_as_longlong(p[u].w)) & mask) != key) continue;
+            const double dx = ax - p[u].x, dy = ay - p[u].y, dz = az - p[u].z;
+            fn(q + u, ((dx * dx) + (dy * dy)) + (dz * dz));
+        }
+    }
+    for (; q < e; q++) {
+        const double4 p = g.pt[q];
+        if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & mask) != key) continue;
+        const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
+        fn(q, ((dx * dx) + (dy * dy)) + (dz * dz));
+    }
+}
+
+// the 27 cells around (x, y, z)
+template <typename Fn>
+__device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
+                                            double ay, double az, Fn &&fn)
+{
+    for (int dz = -1; dz <= 1; dz++)
+        for (int dy = -1; dy <= 1; dy++)
+            for (int dx = -1; dx <= 1; dx++) lds_cell(g, x + dx, y + dy, z + dz, with, ax, ay, az, fn);
+}
+
+__device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, int &z)
+{
+    x = static_cast<int>((k >> 42) & 0x1FFFFF);
+    y = static_cast<int>((k >> 21) & 0x1FFFFF);
+    z = static_cast<int>(k & 0x1FFFFF);
+}
+
+__global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
+    const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
+    const double *__restrict__ vpts, float *__restrict__ qpts, int *__restrict__ slot_m, int *__restrict__ slot_ns,
+    float *__restrict__ slot_box)
+{
+    constexpr int NW = kBpLdsT / 64;
+    __shared__ double4 spt[kBpLdsN];                            // cell-sorted points + cell keys
+    __shared__ int sA[2 * kBpLdsN + 1];                         // bucket starts
+    __shared__ int sB[2 * kBpLdsN + 2];                         // bucket counts; then min original
+                                                                // index per root [0, n) + class counts [kBpLdsN, ..)
+    __shared__ short sorig[kBpLdsN], spos[kBpLdsN];             // sorted position <-> original index
+    __shared__ int sflag[kBpLdsN];                              // neighbour count | kept bit 30
+    __shared__ int spar[kBpLdsN];                               // union-find over positions, then roots
+    __shared__ int sX[kBpLdsN];                                 // bucket per point; rank per root; S list
+    __shared__ double savg[kBpLdsN];                            // labels (int view); then mean distances
+    __shared__ double red[6 * NW];
+    __shared__ float fred[6 * NW];
+    __shared__ int ws[NW];
+    __shared__ double s_thr;
+    int *slab = reinterpret_cast<int *>(savg);
+    int *ccnt = sB + kBpLdsN;
+    int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+#ifdef MC_BP_STAMPS
+    unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
+    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+        const int base = slot_pix[s], n = slot_nv[s];
+        if (n > kBpLdsN) continue;  // k_bp_denoise (uniform)
+        BP_STAMP(16);
+        const double *P = vpts + 3 * static_cast<size_t>(base);
+        // 1. bounding box -> grid origin and cell range
+        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int i = t; i < n; i += kBpLdsT)
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                mn[c] = fmin(mn[c], P[3 * i + c]);
+                mx[c] = fmax(mx[c], P[3 * i + c]);
+            }
+        block_minmax3_nw<NW>(mn, mx, red);
+        BpLdsGrid g;
+        g.pt = spt;
+        g.bs = sA;
+        g.nb = 2u * static_cast<unsigned>(n);
+#pragma unroll
+        for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
+        BP_STAMP(17);
+        // 2. bucket counts
+        for (int b = t; b < 2 * n; b += kBpLdsT) sB[b] = 0;
+        __syncthreads();
+        for (int i = t; i < n; i += kBpLdsT) {
+            int c3[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
+            const unsigned b = mod_mul(bp_hash3(c3[0], c3[1], c3[2]), g.nb);
+            sX[i] = static_cast<int>(b);
+            atomicAdd(&sB[b], 1);
+        }
+        __syncthreads();
+        BP_STAMP(18);
+        // 3. bucket starts
+        {
+            int carry = 0;
+            for (int b0 = 0; b0 < 2 * n; b0 += kBpLdsT) {
+                const int b = b0 + t;
+                const int v = b < 2 * n ? sB[b] : 0;
+                int tot;
+                const int ex = block_excl_scan<kBpLdsT>(v, ws, tot);
+                if (b < 2 * n) sA[b] = carry + ex;
+                carry += tot;
+            }
+            if (t == 0) sA[2 * n] = carry;
+        }
+        __syncthreads();
+        BP_STAMP(19);
+        // 4. counting-sort scatter into LDS (bucket counters return to zero)
+        for (int i = t; i < n; i += kBpLdsT) {
+            const int b = sX[i];
+            const int q = sA[b] + atomicSub(&sB[b], 1) - 1;
+            const double x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
+            const unsigned long long ck = pack3(static_cast<int>(floor((x - mn[0]) / pr.ce)),
+                                                static_cast<int>(floor((y - mn[1]) / pr.ce)),
+                                                static_cast<int>(floor((z - mn[2]) / pr.ce)));
+            spt[q] = make_double4(x, y, z, __longlong_as_double(static_cast<long long>(ck)));
+            sorig[q] = static_cast<short>(i);
+            spos[i] = static_cast<short>(q);
+        }
+        __syncthreads();
+        auto keyof = [&](int q) { return static_cast<unsigned long long>(__double_as_longlong(spt[q].w)); };
+        BP_STAMP(20);
+        // 5. eps-neighbour counts (self included)
+        for (int q = t; q < n; q += kBpLdsT) {
+            int x, y, z;
+            unpack3(keyof(q), x, y, z);
+            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            int cnt = 0;
+            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) { cnt += d2 < pr.eps2 ? 1 : 0; });
+            sflag[q] = cnt;
+            spar[q] = q;
+        }
+        __syncthreads();
+        BP_STAMP(21);
+        // 6. connected core points
+        for (int q = t; q < n; q += kBpLdsT) {
+            if (MC_ABLATE_BP == 2 || sflag[q] < pr.minpts) continue;
+            int x, y, z;
+            unpack3(keyof(q), x, y, z);
+            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            int ra = uf_find_s(spar, q);
+            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                if (q2 < q && d2 < pr.eps2 && sflag[q2] >= pr.minpts) {
+                    const int rb = uf_find_s(spar, q2);
+                    if (rb != ra) {  // most edges of a dense cluster are already joined
+                        uf_unite_s(spar, ra, rb);
+                        ra = uf_find_s(spar, ra);
+                    }
+                }
+            });
+        }
+        __syncthreads();
+        BP_STAMP(22);
+        // 7. roots; every component keyed by its smallest original index; clusters ranked by it
+        {
+            int rq[kBpLdsN / kBpLdsT];
+#pragma unroll
+            for (int k = 0; k < kBpLdsN / kBpLdsT; k++) {
+                const int q = t + k * kBpLdsT;
+                rq[k] = (q < n && sflag[q] >= pr.minpts) ? uf_find_s(spar, q) : -1;
+            }
+            __syncthreads();
+            for (int q = t; q < n; q += kBpLdsT) sB[q] = INT_MAX;
+            for (int x = t; x <= n; x += kBpLdsT) ccnt[x] = 0;
+#pragma unroll
+            for (int k = 0; k < kBpLdsN / kBpLdsT; k++) {
+                const int q = t + k * kBpLdsT;
+                if (q < n) spar[q] = rq[k];
+            }
+            __syncthreads();
+            for (int q = t; q < n; q += kBpLdsT)
+                if (spar[q] >= 0) atomicMin(&sB[spar[q]], static_cast<int>(sorig[q]));
+            __syncthreads();
+            int carry = 0;
+            for (int i0 = 0; i0 < n; i0 += kBpLdsT) {
+                const int i = i0 + t;
+                int isr = 0, r = -1;
+                if (i < n) {
+                    r = spar[spos[i]];
+                    isr = (r >= 0 && sB[r] == i) ? 1 : 0;
+                }
+                int tot;
+                const int ex = block_excl_scan<kBpLdsT>(isr, ws, tot);
+                if (isr) sX[r] = carry + ex;  // rank stored at the root position
+                carry += tot;
+            }
+        }
+        __syncthreads();
+        BP_STAMP(23);
+        // 8. labels and class counts
+        for (int q = t; q < n; q += kBpLdsT) {
+            int l;
+            if (spar[q] >= 0) {
+                l = sX[spar[q]];
+            } else {
+                int x, y, z;
+                unpack3(keyof(q), x, y, z);
+                const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+                int best = INT_MAX, broot = -1;
+                lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                    if (!(d2 < pr.eps2)) return;
+                    const int r2 = spar[q2];
+                    if (r2 >= 0 && sB[r2] < best) {
+                        best = sB[r2];
+                        broot = r2;
+                    }
+                });
+                l = broot >= 0 ? sX[broot] : -1;
+            }
+            slab[q] = l;
+            atomicAdd(&ccnt[l + 1], 1);
+        }
+        __syncthreads();
+        BP_STAMP(24);
+        // 9. class filter; S in original index order
+        const double lim = pr.frac * static_cast<double>(n);
+        for (int q = t; q < n; q += kBpLdsT)
+            if (!(static_cast<double>(ccnt[slab[q] + 1]) < lim)) {
+                sflag[q] |= 1 << 30;
+                spt[q].w = __longlong_as_double(static_cast<long long>(keyof(q) | kKeptBit));
+            }
+        __syncthreads();
+        int m = 0;
+        for (int i0 = 0; i0 < n; i0 += kBpLdsT) {
+            const int i = i0 + t;
+            const int keep = (i < n && (sflag[spos[i]] & (1 << 30))) ? 1 : 0;
+            int tot;
+            const int ex = block_excl_scan<kBpLdsT>(keep, ws, tot);
+            if (keep) sX[m + ex] = i;
+            m += tot;
+        }
+        __syncthreads();
+        BP_STAMP(25);
+        // 10. k nearest kept points (grid rings up to R = 2, then all of S)
+        const int kk = min(pr.knn, m);
+        if (t == 0) sfb[kBpFbCount] = 0;
+        __syncthreads();
+        for (int r = t; r < m; r += kBpLdsT) {
+#if MC_ABLATE_BP == 1
+            savg[r] = 1.0;
+            continue;
+#endif
+            const int q = spos[sX[r]];
+            int x, y, z;
+            unpack3(keyof(q), x, y, z);
+            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            double best[kBpKnnMax];
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+            int found = 0;
+            bool done = false;
+            int visited = 0;
+            auto take = [&](int, double d2) {
+                sorted_insert(best, d2);
+                found++;
+            };
+            for (int R = 0; R <= 2 && !done; R++) {
+                for (int dz = -R; dz <= R; dz++)
+                    for (int dy = -R; dy <= R; dy++) {
+                        const bool edge = dz == -R || dz == R || dy == -R || dy == R;
+                        const int step = (edge || R == 0) ? 1 : 2 * R;
+                        for (int dx = -R; dx <= R; dx += step) lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, ax, ay, az, take);
+                    }
+                const double reach = static_cast<double>(R) * pr.ce;
+                done = found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9);
+                visited++;
+            }
+#ifdef MC_BP_STAMPS
+            atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
+            atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(visited));
+            if (!done) atomicAdd(&g_bp_stamps[31], 1ull);
+            atomicAdd(&g_bp_stamps[13], 1ull);
+#endif
+            if (!done) {  // sparse point: every kept point, by a whole wave below
+                sfb[atomicAdd(&sfb[kBpFbCount], 1)] = r;
+                continue;
+            }
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++)
+                if (k < kk) sum = sum + sqrt(best[k]);
+            savg[r] = sum / static_cast<double>(kk);
+        }
+        __syncthreads();
+        for (int f = wv; f < sfb[kBpFbCount]; f += NW) {
+            const int r = sfb[f];
+            const double4 a = spt[spos[sX[r]]];
+            const double mean = wave_knn_mean(m, kk, [&](int j) {
+                const double4 p = spt[spos[sX[j]]];
+                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                return ((ex * ex) + (ey * ey)) + (ez * ez);
+            });
+            if (lane == 0) savg[r] = mean;
+        }
+        __syncthreads();
+        BP_STAMP(26);
+        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate)
+        if (t == 0) {
+            double mean = 0.0, sq = 0.0;
+            for (int r = 0; r < m; r++)
+                if (savg[r] > 0) mean = mean + savg[r];
+            mean = mean / static_cast<double>(m);
+            for (int r = 0; r < m; r++) {
+                const double a = savg[r];
+                sq = sq + (a > 0 ? (a - mean) * (a - mean) : 0.0);
+            }
+            const double sd = sqrt(sq / static_cast<double>(m - 1));
+            s_thr = mean + pr.std_ratio * sd;
+        }
+        __syncthreads();
+        const double thr = s_thr;
+        BP_STAMP(27);
+        // 12. survivors -> float32 mask points and their AABB
+        int ns = 0;
+        float flo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, fhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int r0 = 0; r0 < m; r0 += kBpLdsT) {
+            const int r = r0 + t;
+            const int keep = (r < m && savg[r] > 0 && savg[r] < thr) ? 1 : 0;
+            int tot;
+            const int ex = block_excl_scan<kBpLdsT>(keep, ws, tot);
+            if (keep) {
+                const int i = sX[r];
+                float *qo = qpts + 3 * (static_cast<size_t>(base) + ns + ex);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    qo[c] = static_cast<float>(P[3 * i + c]);
+                    flo[c] = fminf(flo[c], qo[c]);
+                    fhi[c] = fmaxf(fhi[c], qo[c]);
+                }
+            }
+            ns += tot;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float a = flo[c], b = fhi[c];
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                a = fminf(a, __shfl_xor(a, d, 64));
+                b = fmaxf(b, __shfl_xor(b, d, 64));
+            }
+            if (lane == 0) {
+                fred[c * NW + wv] = a;
+                fred[3 * NW + c * NW + wv] = b;
+            }
+        }
+        __syncthreads();
+        BP_STAMP(28);
+        if (t == 0) {
+            slot_m[s] = m;
+            slot_ns[s] = ns;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                float a = fred[c * NW], b = fred[3 * NW + c * NW];
+                for (int w = 1; w < NW; w++) {
+                    a = fminf(a, fred[c * NW + w]);
+                    b = fmaxf(b, fred[3 * NW + c * NW + w]);
+                }
+                slot_box[6 * s + c] = a;
+                slot_box[6 * s + 3 + c] = b;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_bp_denoise(
     const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
     const double *__restrict__ vpts, unsigned long long *__restrict__ pcell, int *__restrict__ pbkt,
@@ -545,13 +1120,20 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
 {
     __shared__ double red[24];
     __shared__ double s_avg[kBpStage];
+    __shared__ int s_par[kBpLdsUF];
+    __shared__ int s_nfb;
     __shared__ double s_thr;
     __shared__ float fred[24];
     __shared__ int ws[4];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+#ifdef MC_BP_STAMPS
+    unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+        BP_STAMP(0);
         const int base = slot_pix[s], n = slot_nv[s];
+        if (n <= kBpLdsN) continue;  // k_bp_denoise_lds (uniform)
         const double *P = vpts + 3 * static_cast<size_t>(base);
         unsigned long long *pc = pcell + base;
         int *pb = pbkt + base, *bc = bcnt + 2 * static_cast<size_t>(base), *bs = bstart + 2 * static_cast<size_t>(base) + s;
@@ -575,6 +1157,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
         g.nb = nb;
 #pragma unroll
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
+        BP_STAMP(1);
         // 2. cells, bucket counts; class counters cleared
         for (int i = t; i < n; i += 256) {
             int cxyz[3];
@@ -587,6 +1170,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
         }
         for (int i = t; i <= n; i += 256) cc[i] = 0;
         __syncthreads();
+        BP_STAMP(2);
         // 3. bucket starts
         {
             int carry = 0;
@@ -601,6 +1185,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             if (t == 0) bs[nb] = carry;
         }
         __syncthreads();
+        BP_STAMP(3);
         // 4. counting-sort scatter (bucket counters return to zero)
         for (int i = t; i < n; i += 256) {
             const int b = pb[i];
@@ -613,6 +1198,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             y = static_cast<int>((k >> 21) & 0x1FFFFF);
             z = static_cast<int>(k & 0x1FFFFF);
         };
+        BP_STAMP(4);
         // 5. eps-neighbour counts (self included) -> core
         for (int i = t; i < n; i += 256) {
             int x, y, z;
@@ -622,9 +1208,11 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             for (int R = 0; R <= 1; R++)
                 bp_shell(g, x, y, z, R, [&](int j) { cnt += bp_d2(pi, P + 3 * j) < pr.eps2 ? 1 : 0; });
             nc[i] = cnt;
-            pa[i] = i;
+            if (n <= kBpLdsUF) s_par[i] = i;
+            else pa[i] = i;
         }
         __syncthreads();
+        BP_STAMP(5);
         // 6. connected core points (union-find, root = smallest index)
         for (int i = t; i < n; i += 256) {
             if (nc[i] < pr.minpts) continue;
@@ -633,10 +1221,14 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             const double *pi = P + 3 * i;
             for (int R = 0; R <= 1; R++)
                 bp_shell(g, x, y, z, R, [&](int j) {
-                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) uf_unite(pa, i, j);
+                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) {
+                        if (n <= kBpLdsUF) uf_unite_s(s_par, i, j);
+                        else uf_unite(pa, i, j);
+                    }
                 });
         }
         __syncthreads();
+        BP_STAMP(6);
         // 7. clusters numbered in order of their smallest point
         {
             int carry = 0;
@@ -644,7 +1236,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                 const int i = i0 + t;
                 int isr = 0;
                 if (i < n && nc[i] >= pr.minpts) {
-                    const int r = uf_find(pa, i);
+                    const int r = n <= kBpLdsUF ? uf_find_s(s_par, i) : uf_find(pa, i);
                     ro[i] = r;
                     isr = r == i ? 1 : 0;
                 }
@@ -655,6 +1247,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             }
         }
         __syncthreads();
+        BP_STAMP(7);
         // 8. labels (+1 = the reference's shifted labels, geometry.py:10) and class counts
         for (int i = t; i < n; i += 256) {
             int l;
@@ -675,6 +1268,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             atomicAdd(&cc[l + 1], 1);
         }
         __syncthreads();
+        BP_STAMP(8);
         // 9. class filter (geometry.py:15-20): the kept set S in index order
         const double lim = pr.frac * static_cast<double>(n);
         int m = 0;
@@ -688,36 +1282,12 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             m += tot;
         }
         __syncthreads();
-        // 10. k nearest kept points
+        BP_STAMP(9);
+        // 10. k nearest kept points: grid rings up to R = 2, then (rare: sparse points) all of S
         const int kk = min(pr.knn, m);
-        const int rmax = max(g.cmax[0], max(g.cmax[1], g.cmax[2]));
-        for (int r = t; r < m; r += 256) {
-            const int i = si[r];
-            int x, y, z;
-            cell_of(i, x, y, z);
-            const double *pi = P + 3 * i;
-            double best[kBpKnnMax];
-#pragma unroll
-            for (int q = 0; q < kBpKnnMax; q++) best[q] = DBL_MAX;
-            int found = 0;
-            for (int R = 0;; R++) {
-                bp_shell(g, x, y, z, R, [&](int j) {
-                    if (nc[j] & (1 << 30)) {
-                        sorted_insert(best, bp_d2(pi, P + 3 * j));
-                        found++;
-                    }
-                });
-                const double reach = static_cast<double>(R) * pr.ce;
-                if (found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9)) break;
-                if (R > rmax) break;
-            }
-            double sum = 0.0;
-#pragma unroll
-            for (int q = 0; q < kBpKnnMax; q++)
-                if (q < kk) sum = sum + sqrt(best[q]);
-            av[r] = sum / static_cast<double>(kk);
-        }
+        bp_knn<kBpKnnMax>(g, P, nc, si, m, kk, pr.ce, av, t, s_par, kBpLdsUF, &s_nfb);
         __syncthreads();
+        BP_STAMP(10);
         // 11. cloud mean and Bessel std: sequential sums in index order (std::accumulate)
         {
             double mean = 0.0, sq = 0.0;
@@ -747,6 +1317,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
         }
         __syncthreads();
         const double thr = s_thr;
+        BP_STAMP(11);
         // 12. survivors -> float32 mask points (:112) and their float32 AABB (:59-61)
         int ns = 0;
         float flo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, fhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -781,6 +1352,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             }
         }
         __syncthreads();
+        BP_STAMP(12);
         if (t == 0) {
             slot_m[s] = m;
             slot_ns[s] = ns;

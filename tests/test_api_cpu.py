@@ -52,3 +52,33 @@ def test_turn_mask_to_point_inf_pose_returns_early():
             return T
 
     assert turn_mask_to_point(DS(), np.zeros((5, 3)), np.zeros((48, 64), np.uint8), 0) == ({}, [], set())
+
+
+def test_install_routes_reference_module_names(tmp_path):
+    """With a reference-shaped tree on sys.path, install() makes main.py's imports
+    (main.py:4-5) resolve to the drop-ins while other modules stay the reference's."""
+    import subprocess
+    import sys
+    import textwrap
+    from conftest import REPO
+    (tmp_path / "graph").mkdir()
+    (tmp_path / "utils").mkdir()
+    (tmp_path / "utils" / "__init__.py").write_text("")
+    (tmp_path / "utils" / "geometry.py").write_text("MARK = 'reference'\n")
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {str(tmp_path)!r})  # the reference checkout (cwd of main.py)
+        from graph.construction import mask_graph_construction
+        from graph.iterative_clustering import iterative_clustering
+        from utils.mask_backprojection import frame_backprojection
+        from utils.geometry import MARK
+        assert mask_graph_construction.__module__ == 'maskclustering_amd.graph.construction'
+        assert iterative_clustering.__module__ == 'maskclustering_amd.graph.iterative_clustering'
+        assert frame_backprojection.__module__ == 'maskclustering_amd.utils.mask_backprojection'
+        assert MARK == 'reference'
+        print('ok')
+    """)
+    import os
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(REPO, "integration"), REPO]))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=str(tmp_path), env=env)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
