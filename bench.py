@@ -274,7 +274,7 @@ def main():
     roof["algorithmic_per_launch"] = per_launch
     # HBM bytes per launch of the same kernel group from the committed rocprofv3 PMC passes
     # (scripts/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)
-    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json" if args.variant == "g" else "pmc_traffic_e2e.json")
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.variant}_{args.shape}.json")  # same workload only
     if bound == "hbm" and os.path.exists(pmc_path):
         g = json.load(open(pmc_path)).get("groups", {}).get(dominant)
         if g:

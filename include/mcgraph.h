@@ -90,7 +90,7 @@ typedef struct {
     double ball_radius;            /* DISTANCE_THRESHOLD (as float32)       */
     double coverage_threshold;     /* COVERAGE_THRESHOLD = 0.3              */
     int32_t dbscan_min_points;     /* 4                                     */
-    int32_t sor_neighbors;         /* 20 (<= 32)                            */
+    int32_t sor_neighbors;         /* 20 (<= 20)                            */
     int32_t ball_k;                /* K = 20 (<= 32)                        */
     int32_t few_points;            /* FEW_POINTS_THRESHOLD = 25             */
 } mc_bp_params;

@@ -55,7 +55,7 @@ struct mc_ctx {
     // ---- S3/S5 ----
     DevBuf d_ctmp, d_crow_len, d_useg, d_keep_cnt, d_node_flag, d_node_pos, d_c_off, d_c_idx, d_vf;
     // ---- S4 ----
-    DevBuf d_hist, d_thr, d_isint, d_stats;
+    DevBuf d_hist, d_thr, d_isint, d_stats, d_s4rng;
     // ---- level-0 nodes ----
     int N0 = 0;        // host copy (valid after sync_stats or mc_nodes_set)
     int Mn = 0;        // mask-id space of C rows
@@ -142,11 +142,13 @@ void sync_stats(mc_ctx *ctx)
 
 
 // S4 histogram launch: persistent blocks, R lane-indexed LDS replicas (odd stride)
-void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsigned long long *hist)
+// rng: >= ceil(M / 64) int2 of scratch
+void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsigned long long *hist, int2 *rng)
 {
     if (!M || !F) return;
     const int FW = (F + 63) / 64;
     const int nblk = ceil_div(M, mc::kHistTile);
+    hipLaunchKernelGGL(mc::k_s4_ranges, grid_for(static_cast<int64_t>(nblk) * 64), dim3(256), 0, s, vf, M, FW, nblk, rng);
     const long long ntiles = static_cast<long long>(nblk) * (nblk + 1) / 2;
     const int HS = (F + 1) | 1;
     int R = 32;
@@ -154,7 +156,7 @@ void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsi
     const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + static_cast<size_t>(R) * HS * 4;
     const long long grid = std::min<long long>(ntiles, 1024);
     hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(grid)), dim3(256), lds, s, vf, M, FW, F, nblk, ntiles, R,
-                       HS, hist);
+                       HS, rng, hist);
 }
 
 }  // namespace
@@ -190,7 +192,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     DevBuf *bufs[] = {&ctx->d_mask_off, &ctx->d_mask_pts, &ctx->d_mask_col, &ctx->d_mask_label, &ctx->d_frame_start,
                       &ctx->d_valid, &ctx->d_deg, &ctx->d_pt_off, &ctx->d_pt_list, &ctx->d_boundary,
                       &ctx->d_pfm, &ctx->d_scan_tmp, &ctx->d_ctmp, &ctx->d_crow_len, &ctx->d_useg, &ctx->d_keep_cnt,
-                      &ctx->d_node_flag, &ctx->d_node_pos, &ctx->d_c_off, &ctx->d_c_idx, &ctx->d_vf, &ctx->d_hist,
+                      &ctx->d_node_flag, &ctx->d_node_pos, &ctx->d_c_off, &ctx->d_c_idx, &ctx->d_vf, &ctx->d_hist, &ctx->d_s4rng,
                       &ctx->d_thr, &ctx->d_isint, &ctx->d_stats, &ctx->d_node0_g, &ctx->d_n0_off, &ctx->d_n0_len,
                       &ctx->d_n0_ptoff, &ctx->d_n0_ptlen, &ctx->d_n0_vf, &ctx->d_user_cidx, &ctx->d_user_pts,
                       &ctx->d_parent, &ctx->d_root, &ctx->d_isroot, &ctx->d_rank, &ctx->d_label, &ctx->d_levels,
@@ -401,6 +403,7 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
         ctx->d_c_idx.reserve((static_cast<size_t>(M) * F + 1) * sizeof(int));
         ctx->d_vf.reserve((static_cast<size_t>(M) * FW + 1) * sizeof(unsigned long long));
         ctx->d_hist.reserve((F + 2) * sizeof(unsigned long long));
+        ctx->d_s4rng.reserve((M / 64 + 2) * sizeof(int2));
         ctx->d_thr.reserve(32 * sizeof(float));
         ctx->d_isint.reserve(32 * sizeof(int));
         ctx->d_node0_g.reserve((M + 1) * sizeof(int));
@@ -508,7 +511,8 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         }
         {  // S4
             TimedScope ts(ctx->timer, s, "s4_observer_hist");
-            launch_hist(s, ctx->d_vf.as<unsigned long long>(), M, F, ctx->d_hist.as<unsigned long long>());
+            launch_hist(s, ctx->d_vf.as<unsigned long long>(), M, F, ctx->d_hist.as<unsigned long long>(),
+                        ctx->d_s4rng.as<int2>());
             hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
                                ctx->d_hist.as<unsigned long long>(), F, ctx->d_thr.as<float>(), ctx->d_isint.as<int>(),
                                stats + ST_NTHR, stats + ST_THR_STATUS);
@@ -675,7 +679,9 @@ int mc_observer_thresholds(mc_ctx *ctx, int32_t num_rows, int32_t num_frames, co
         st.reserve(2 * 4);
         if (M && FW) MC_HIP(hipMemcpyAsync(vf.ptr, vf_bits, static_cast<size_t>(M) * FW * 8, hipMemcpyHostToDevice, s));
         MC_HIP(hipMemsetAsync(hist.ptr, 0, (F + 1) * 8, s));
-        launch_hist(s, vf.as<unsigned long long>(), M, F, hist.as<unsigned long long>());
+        DevBuf rng;
+        rng.reserve((M / 64 + 2) * sizeof(int2));
+        launch_hist(s, vf.as<unsigned long long>(), M, F, hist.as<unsigned long long>(), rng.as<int2>());
         hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
                            hist.as<unsigned long long>(), F,
                            dthr.as<float>(), disint.as<int>(), st.as<int>(), st.as<int>() + 1);
@@ -1135,10 +1141,7 @@ void grow_keep(DevBuf &b, size_t bytes, size_t used, hipStream_t s)
     nb.reserve(bytes + bytes / 2);
     if (used) MC_HIP(hipMemcpyAsync(nb.ptr, b.ptr, used, hipMemcpyDeviceToDevice, s));
     MC_HIP(hipStreamSynchronize(s));
-    b.release();
-    b = nb;
-    nb.ptr = nullptr;
-    nb.bytes = 0;
+    b.swap(nb);  // the old buffer is freed with nb
 }
 
 enum BpStat : int { BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ, BS_COUNT };

@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -41,6 +42,14 @@ struct McError {
 struct DevBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }  // temporaries of a call free themselves (after the call's sync)
+    void swap(DevBuf &o) {
+        std::swap(ptr, o.ptr);
+        std::swap(bytes, o.bytes);
+    }
     void reserve(size_t n) {
         if (n <= bytes) return;
         if (ptr) MC_HIP(hipFree(ptr));

@@ -633,9 +633,34 @@ __global__ __launch_bounds__(256) void k_s5_nodes(const int *__restrict__ node_p
 // atomics inside a wave) and reduces them once at the end.
 constexpr int kHistTile = 64, kHistKW = 8;
 
+// Word range [lo, hi] of the nonzero VF words of every 64-row tile (lo > hi: no visible frame).
+// Masks are in frame order and each is visible in a window of frames, so far-apart tiles share no
+// word and their observer counts are all 0 -- which the histogram of positive counts never needs.
+__global__ __launch_bounds__(256) void k_s4_ranges(const unsigned long long *__restrict__ vf, int M, int FW, int nblk,
+                                                   int2 *__restrict__ rng)
+{
+    const int lane = lane_id();
+    for (int b = (blockIdx.x * 256 + threadIdx.x) >> 6; b < nblk; b += gridDim.x * 4) {
+        const long long g = static_cast<long long>(b) * kHistTile + lane;
+        int lo = INT_MAX, hi = -1;
+        if (g < M)
+            for (int w = 0; w < FW; w++)
+                if (vf[static_cast<size_t>(g) * FW + w]) {
+                    lo = min(lo, w);
+                    hi = w;
+                }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            lo = min(lo, __shfl_xor(lo, d, 64));
+            hi = max(hi, __shfl_xor(hi, d, 64));
+        }
+        if (lane == 0) rng[b] = make_int2(lo, hi);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_s4_hist(const unsigned long long *__restrict__ vf, int M, int FW, int F,
                                                  int nblk, long long ntiles, int R, int HS,
-                                                 unsigned long long *__restrict__ hist_g)
+                                                 const int2 *__restrict__ rng, unsigned long long *__restrict__ hist_g)
 {
     extern __shared__ unsigned char smem_raw[];
     unsigned long long *A = reinterpret_cast<unsigned long long *>(smem_raw);
@@ -657,19 +682,22 @@ __global__ __launch_bounds__(256) void k_s4_hist(const unsigned long long *__res
         while (bi + 1 < nblk && row_start(bi + 1) <= tile) bi++;
         const long long bj = bi + (tile - row_start(bi));
 
+        const int2 ri = rng[bi], rj = rng[bj];
+        const int wlo = max(ri.x, rj.x), whi = min(ri.y, rj.y);
+        if (wlo > whi) continue;  // no common word: every count of the tile is 0 (uniform)
         int acc[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) acc[k] = 0;
-        for (int w0 = 0; w0 < FW; w0 += kHistKW) {
+        for (int w0 = wlo; w0 <= whi; w0 += kHistKW) {
             __syncthreads();
             for (int x = threadIdx.x; x < kHistTile * kHistKW; x += 256) {
                 const int r = x / kHistKW, w = x % kHistKW;
                 const long long gi = bi * kHistTile + r, gj = bj * kHistTile + r;
-                A[x] = (gi < M && w0 + w < FW) ? vf[static_cast<size_t>(gi) * FW + w0 + w] : 0ull;
-                B[x] = (gj < M && w0 + w < FW) ? vf[static_cast<size_t>(gj) * FW + w0 + w] : 0ull;
+                A[x] = (gi < M && w0 + w <= whi) ? vf[static_cast<size_t>(gi) * FW + w0 + w] : 0ull;
+                B[x] = (gj < M && w0 + w <= whi) ? vf[static_cast<size_t>(gj) * FW + w0 + w] : 0ull;
             }
             __syncthreads();
-            const int kw = min(kHistKW, FW - w0);
+            const int kw = min(kHistKW, whi + 1 - w0);
             for (int w = 0; w < kw; w++) {
                 const unsigned long long a = A[ti * kHistKW + w];
 #pragma unroll
