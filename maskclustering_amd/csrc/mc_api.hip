@@ -38,6 +38,8 @@ struct mc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipStream_t side = nullptr;                 // S3: workgroup-per-mask kernel beside the wave kernel
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
@@ -172,6 +174,9 @@ int mc_ctx_create(int device, mc_ctx **out)
     int rc = guarded(ctx, [&] {
         MC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ctx->own_stream = true;
+        MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        MC_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        MC_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
         MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stats), ST_COUNT * sizeof(int), hipHostMallocDefault));
         ctx->d_stats.reserve(ST_COUNT * sizeof(int));
         MC_HIP(hipMemset(ctx->d_stats.ptr, 0, ST_COUNT * sizeof(int)));
@@ -220,6 +225,9 @@ void mc_ctx_destroy(mc_ctx *ctx)
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side), (void)hipStreamDestroy(ctx->side);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     delete ctx;
 }
 
@@ -425,6 +433,12 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
                 const int sz = ctx->h_off[g + 1] - ctx->h_off[g];
                 (wave_ok && sz <= mc::kS3SmallPts ? small : big).push_back(g);
             }
+            // largest masks first: the long waves start early instead of forming the tail
+            auto by_size = [&](int x, int y) {
+                return ctx->h_off[x + 1] - ctx->h_off[x] > ctx->h_off[y + 1] - ctx->h_off[y];
+            };
+            std::stable_sort(small.begin(), small.end(), by_size);
+            std::stable_sort(big.begin(), big.end(), by_size);
             ctx->n_s3_small = static_cast<int>(small.size());
             ctx->n_s3_big = static_cast<int>(big.size());
             ctx->d_s3_small.reserve((small.size() + 1) * sizeof(int));
@@ -469,8 +483,16 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         }
         if (M) {  // S3
             TimedScope ts(ctx->timer, s, "s3_masks");
+            // large masks (workgroup per mask) on the side stream, concurrent with the wave kernel
+            const bool fork = ctx->n_s3_big && ctx->n_s3_small;
+            if (fork) {
+                MC_HIP(hipEventRecord(ctx->ev_fork, s));
+                MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+            }
             if (ctx->n_s3_big)
-                hipLaunchKernelGGL(mc::k_s3_masks<4>, grid_for(ctx->n_s3_big, 1, 8192), dim3(256), 0, s,
+                hipLaunchKernelGGL(mc::k_s3_masks<mc::kS3BigW>, grid_for(ctx->n_s3_big, 1, 8192),
+                                   dim3(mc::S3Cfg<mc::kS3BigW>::NT), 0,
+                                   fork ? ctx->side : s,
                                    ctx->d_s3_big.as<int>(), ctx->n_s3_big, ctx->d_mask_off.as<int>(),
                                    ctx->d_mask_pts.as<int>(), ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(),
                                    ctx->d_boundary.as<unsigned char>(), ctx->d_pfm.as<unsigned long long>(), FW,
@@ -487,6 +509,10 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
                                    params->mask_visible_threshold, params->contained_threshold,
                                    params->undersegment_filter_threshold, ctx->d_ctmp.as<int>(),
                                    ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
+            if (fork) {
+                MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+                MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+            }
         }
         if (M) {  // S3 undo + S5
             TimedScope ts(ctx->timer, s, "s3_undo_s5");

@@ -314,25 +314,49 @@ __global__ __launch_bounds__(256) void k_s2_dense_pim(const int *__restrict__ pt
 // ---------------------------------------------------------------------------------------------
 // S3 kernel, W waves per mask (W = 1: four masks per workgroup, wave-private LDS;
 // W = 4: one mask per workgroup, for large masks).  V = S_g \ boundary, T = |V|
-// (construction.py:105).
-//  pass 1: the frames in which some point of V lies in a mask ("possibly visible",
-//          :110) = OR of the point-frame bit rows of V (no pass over list entries);
-//          touched frames are ranked by a popcount prefix over that bitmap.
-//  pass 2: per (touched frame, mask of the frame) LDS counters count the points of V in
-//          that mask (the per-frame bincount, :116); list entries are read by 16-lane
-//          groups (one point per group), so loads are coalesced.
-//  pass 3: one lane per touched frame applies the reference's rules in float64:
+// (construction.py:105).  For every frame the reference takes the bincount of the mask ids
+// that V's points carry in that frame (:110-116).  Here every list entry
+// (frame << 12 | mask-in-frame) of every point of V is counted in an LDS hash table keyed by
+// the entry itself: ONE pass over the entries, and the table only holds the (frame, mask)
+// pairs that V meets (tens per mask, against F x masks-per-frame dense counters).
+//  pass A: entries -> hash counts.  The entries of 64 points are flattened; the point of
+//          flat entry kk comes from a 64-bit bitmap of segment starts per 64 entries
+//          (popcount rank, no search), so the pt_list loads of a wave are coalesced.
+//  pass B: the touched frames (frames of the keys) are ranked by a popcount prefix over a
+//          frame bitmap; per window of 64·W ranks the keys are folded into per-frame nz and
+//          argmax (count, then smallest mask id: np.argmax order, :121-124) by LDS atomics.
+//  pass C: one lane per touched frame applies the reference's rules in float64:
 //          skip if (1 - c0/T) < mvt and nz < 500                          (:117-120)
-//          visible; argmax mask (smallest id on ties); contained if cmax/nz > ct (:121-128)
-//          otherwise split                                                 (:130)
-// Touched frames are processed in windows of 64·W frames / CNT counters.
+//          visible; contained if cmax/nz > ct (:121-128), otherwise split  (:130)
+// A table that fills up (more distinct pairs than HS) sends that mask, and only that mask,
+// to s3_dense: dense per-(frame, mask) counters over windows of frames.
 template <int W> struct S3Cfg;
-template <> struct S3Cfg<1> { static constexpr int FWMAX = 32, CNT = 1024; };   // F <= 2048
-template <> struct S3Cfg<4> { static constexpr int FWMAX = 256, CNT = 4096; };  // F <= 16384
-constexpr int kS3SmallPts = 1024;  // masks up to this size go to the W = 1 kernel
-constexpr int kS3Batch = 8;        // list entries gathered per lane before use
+template <> struct S3Cfg<1> { static constexpr int FWMAX = 32, CNT = 1024, HS = 512, NT = 256; };     // F <= 2048
+template <> struct S3Cfg<4> { static constexpr int FWMAX = 256, CNT = 4096, HS = 2048, NT = 256; };   // F <= 16384
+template <> struct S3Cfg<16> { static constexpr int FWMAX = 256, CNT = 4096, HS = 2048, NT = 1024; }; // F <= 16384
+#ifndef MC_S3_BIGW
+#define MC_S3_BIGW 4
+#endif
+constexpr int kS3BigW = MC_S3_BIGW;  // waves per mask for masks above kS3SmallPts
+#ifndef MC_S3_SMALL
+#define MC_S3_SMALL 1024
+#endif
+constexpr int kS3SmallPts = MC_S3_SMALL;  // masks up to this size go to the W = 1 kernel
+#ifndef MC_S3_BATCH
+#define MC_S3_BATCH 8
+#endif
+#ifndef MC_S3_U
+#define MC_S3_U 2
+#endif
+constexpr int kS3Batch = MC_S3_BATCH;  // list entries gathered per lane before use
+constexpr int kS3U = MC_S3_U;          // 64-point chunks per pass-A sweep
 constexpr int kS3wCounters = S3Cfg<1>::CNT;
 constexpr int kS3wFrameWords64 = S3Cfg<1>::FWMAX;
+constexpr unsigned kS3Empty = 0xffffffffu;  // never an entry (frame < 2^19)
+#ifndef MC_S3_REP
+#define MC_S3_REP 1
+#endif
+constexpr int kS3Rep = MC_S3_REP;  // count replicas (lanes >> (6 - log2 kS3Rep) pick one)
 
 template <int W>
 __device__ __forceinline__ void s3_sync()
@@ -353,6 +377,13 @@ __device__ __forceinline__ int s3_excl_scan(int v, int *ws, int &total)
     return block_excl_scan<64 * W>(v, ws, total);
 }
 
+template <int W>
+__device__ __forceinline__ int s3_sum(int v, int *ws)
+{
+    if (W == 1) return wave_sum(v);
+    return block_sum<64 * W>(v, ws);
+}
+
 __device__ __forceinline__ unsigned long long wave_or64(unsigned long long v)
 {
 #pragma unroll
@@ -360,180 +391,338 @@ __device__ __forceinline__ unsigned long long wave_or64(unsigned long long v)
     return v;
 }
 
+// rank of frame c among the touched frames (fb bitmap, wpre = popcount prefix per word)
+__device__ __forceinline__ int s3_rank(const unsigned long long *fb, const int *wpre, unsigned c)
+{
+    return wpre[c >> 6] + __popcll(fb[c >> 6] & ((1ull << (c & 63)) - 1ull));
+}
+
+// wpre[w] = number of touched frames in words < w; returns the number of touched frames
 template <int W>
-__global__ __launch_bounds__(256) void k_s3_masks(
+__device__ __forceinline__ int s3_rank_prefix(const unsigned long long *fb, int *wpre, int FB, int tl, int *ws)
+{
+    int ntf = 0;
+    for (int w0 = 0; w0 < FB; w0 += 64 * W) {
+        const int w = w0 + tl;
+        const int pc = w < FB ? __popcll(fb[w]) : 0;
+        int tot;
+        const int ex = s3_excl_scan<W>(pc, ws, tot);
+        if (w < FB) wpre[w] = ex + ntf;
+        ntf += tot;
+    }
+    return ntf;
+}
+
+// The reference's per-frame decision (construction.py:117-130): 0 not visible, 1 visible
+// and split, 2 visible and contained.
+__device__ __forceinline__ int s3_decide(int T, int nz, int bc, double mvt, double ctn)
+{
+    const int c0 = T - nz;
+    if (1.0 - static_cast<double>(c0) / static_cast<double>(T) < mvt && nz < 500) return 0;
+    if (static_cast<double>(bc) / static_cast<double>(nz) > ctn) return 2;
+    return 1;
+}
+
+// Ordered compaction of one window of decisions (lanes in frame-rank order) into the C row.
+template <int W>
+__device__ __forceinline__ void s3_emit(int dec, int tgt, int *crow, int &ncont, int &vis, int &split, int *ws)
+{
+    int ncw;
+    const int pos = s3_excl_scan<W>(dec == 2 ? 1 : 0, ws, ncw);
+    if (dec == 2) crow[ncont + pos] = tgt;
+    ncont += ncw;
+    int nv, ns;
+    s3_excl_scan<W>(dec >= 1 ? 1 : 0, ws, nv);
+    s3_excl_scan<W>(dec == 1 ? 1 : 0, ws, ns);
+    vis += nv;
+    split += ns;
+}
+
+// Fallback for masks whose (frame, mask) pairs overflow the hash table: touched frames from
+// the point-frame bit rows of V, then per window of frames whose dense counters fit in CNT,
+// one pass over V's entries (16-lane binary search over the flattened segment starts).
+template <int W>
+__device__ void s3_dense(int b, int en, int wl, int lane, int tl, int wv, const int *__restrict__ pts,
+                         const int *__restrict__ pt_off, const unsigned *__restrict__ pt_list,
+                         const unsigned char *__restrict__ boundary, const unsigned long long *__restrict__ pfm,
+                         int FW, int FB, const int *__restrict__ frame_start, const int *__restrict__ mask_label,
+                         double mvt, double ctn, int *crow, unsigned long long *fb, int *wpre, int *tf_frame,
+                         int *tf_slot, int *cnt, int *spre, int *spb, int *ws, int &ncont, int &vis, int &split)
+{
+    constexpr int CNT = S3Cfg<W>::CNT, WIN = 64 * W;
+    for (int w = tl; w < FB; w += 64 * W) fb[w] = 0ull;
+    s3_sync<W>();
+    int myT = 0;
+    for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
+        const int k = k0 + lane;
+        const int p = k < en ? pts[k] : 0;
+        const bool nb = k < en && !boundary[p];
+        myT += nb ? 1 : 0;
+        for (int w = 0; w < FW; w++) {
+            unsigned long long v = nb ? pfm[static_cast<size_t>(p) * FW + w] : 0ull;
+            v = wave_or64(v);
+            if (lane == 0 && v) atomicOr(&fb[w], v);
+        }
+    }
+    const int T = s3_sum<W>(myT, ws);
+    s3_sync<W>();
+    const int ntf = s3_rank_prefix<W>(fb, wpre, FB, tl, ws);
+    s3_sync<W>();
+    for (int j0 = 0; j0 < ntf;) {
+        for (int w = tl; w < FB; w += 64 * W) {  // frames of rank [j0, j0 + WIN)
+            unsigned long long bits = fb[w];
+            int r = wpre[w];
+            while (bits) {
+                const int bt = __ffsll(static_cast<long long>(bits)) - 1;
+                bits &= bits - 1;
+                if (r >= j0 && r < j0 + WIN) tf_frame[r - j0] = (w << 6) + bt;
+                r++;
+            }
+        }
+        s3_sync<W>();
+        const int jmax = min(WIN, ntf - j0);
+        const int fr = tl < jmax ? tf_frame[tl] : 0;
+        const int fs_l = tl < jmax ? frame_start[fr] : 0;
+        const int nm = tl < jmax ? frame_start[fr + 1] - fs_l : 0;
+        int tot;
+        const int ex = s3_excl_scan<W>(nm, ws, tot);
+        int jn;  // window = longest prefix of frames whose counters fit (at least one frame)
+        {
+            const int fits = (tl < jmax && ex + nm <= CNT) ? 1 : 0;
+            int nf;
+            s3_excl_scan<W>(fits, ws, nf);
+            jn = max(1, nf);
+        }
+        if (tl < jn) tf_slot[tl] = ex;
+        if (tl == jn - 1) tf_slot[jn] = ex + nm;
+        s3_sync<W>();
+        const int nslots = tf_slot[jn];
+        for (int x = tl; x < nslots; x += 64 * W) cnt[x] = 0;
+        s3_sync<W>();
+        for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
+            const int k = k0 + lane;
+            int pb = 0, d = 0;
+            if (k < en) {
+                const int p = pts[k];
+                if (!boundary[p]) {
+                    pb = pt_off[p];
+                    d = pt_off[p + 1] - pb;
+                }
+            }
+            const int inc = wave_incl_scan(d);
+            const int E = __shfl(inc, 63, 64);
+            spre[lane] = inc - d;
+            spb[lane] = pb;
+            wave_sync();
+            for (int kk = lane; kk < E; kk += 64) {
+                int lo = 0;
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1)
+                    if (spre[lo + st] <= kk) lo += st;
+                const unsigned e = pt_list[spb[lo] + kk - spre[lo]];
+                const int rr = s3_rank(fb, wpre, e >> kLocalBits) - j0;
+                if (rr >= 0 && rr < jn) atomicAdd(&cnt[tf_slot[rr] + static_cast<int>(e & (kMaxMasksPerFrame - 1))], 1);
+            }
+            wave_sync();
+        }
+        s3_sync<W>();
+        int dec = 0, tgt = 0;
+        if (tl < jn) {
+            const int base = tf_slot[tl];
+            int nz = 0, bc = 0, best = -1;
+            for (int l = 0; l < nm; l++) {
+                const int v = cnt[base + l];
+                nz += v;
+                if (v > bc) {
+                    bc = v;
+                    best = l;
+                } else if (v == bc && v > 0 && mask_label[fs_l + l] < mask_label[fs_l + best]) {
+                    best = l;  // np.argmax: smallest id on ties
+                }
+            }
+            dec = s3_decide(T, nz, bc, mvt, ctn);
+            tgt = fs_l + best;
+        }
+        s3_emit<W>(dec, tgt, crow, ncont, vis, split, ws);
+        j0 += jn;
+        s3_sync<W>();
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(S3Cfg<W>::NT) void k_s3_masks(
     const int *__restrict__ list, int nlist, const int *__restrict__ mask_off, const int *__restrict__ pts,
     const int *__restrict__ pt_off, const unsigned *__restrict__ pt_list, const unsigned char *__restrict__ boundary,
     const unsigned long long *__restrict__ pfm, int FW, const int *__restrict__ frame_start,
     const int *__restrict__ mask_label, int F, double mvt, double ctn, double ust, int *__restrict__ ctmp,
     int *__restrict__ crow_len, unsigned char *__restrict__ useg)
 {
-    constexpr int SLOTS = 4 / W, FWMAX = S3Cfg<W>::FWMAX, CNT = S3Cfg<W>::CNT, WIN = 64 * W;
+    constexpr int NW = S3Cfg<W>::NT / 64, SLOTS = NW / W, FWMAX = S3Cfg<W>::FWMAX, CNT = S3Cfg<W>::CNT, HS = S3Cfg<W>::HS, WIN = 64 * W;
+    constexpr int POOL = CNT > (1 + kS3Rep) * HS ? CNT : (1 + kS3Rep) * HS;
     __shared__ unsigned long long fb_s[SLOTS][FWMAX];
     __shared__ int wpre_s[SLOTS][FWMAX];
     __shared__ int tfr_s[SLOTS][WIN];
     __shared__ int tsl_s[SLOTS][WIN + 1];
-    __shared__ int cnt_s[SLOTS][CNT];
-    __shared__ int spre_s[4][64];
-    __shared__ int spb_s[4][64];
-    __shared__ int ws[4];
+    __shared__ unsigned long long fbest_s[SLOTS][WIN];
+    __shared__ int cnt_s[SLOTS][POOL];  // hash table (keys | counts) or dense counters
+    __shared__ int spre_s[NW][64];
+    __shared__ int spb_s[NW][64];
+    __shared__ unsigned long long sbits_s[NW][kS3Batch];
+    __shared__ int dl_s[NW][64 * kS3U];
+    __shared__ int ws[NW];
     const int wv = threadIdx.x >> 6, lane = lane_id();
     const int slot = wv / W, wl = wv % W, tl = wl * 64 + lane;
-    unsigned long long *fb = fb_s[slot];
-    int *wpre = wpre_s[slot], *tf_frame = tfr_s[slot], *tf_slot = tsl_s[slot], *cnt = cnt_s[slot];
+    unsigned long long *fb = fb_s[slot], *fbest = fbest_s[slot], *sbits = sbits_s[wv];
+    int *wpre = wpre_s[slot], *tf_frame = tfr_s[slot], *fnz = tsl_s[slot], *cnt = cnt_s[slot];
+    int *dl = dl_s[wv];
+    unsigned *hkey = reinterpret_cast<unsigned *>(cnt), *hval = hkey + HS;
+    unsigned *hval_l = hval + (kS3Rep > 1 ? (lane >> (6 - __builtin_ctz(kS3Rep))) * HS : 0);
     const int FB = (F + 63) >> 6;  // == FW
+    const unsigned long long le_mask = (2ull << lane) - 1ull;  // lanes <= lane
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;  // lanes < lane
 
     for (int q = blockIdx.x * SLOTS + slot; q < nlist; q += gridDim.x * SLOTS) {
         const int g = list[q];
         const int b = mask_off[g], en = mask_off[g + 1];
         int *crow = ctmp + static_cast<size_t>(g) * F;
+        for (int x = tl; x < HS; x += 64 * W) {
+            hkey[x] = kS3Empty;
+#pragma unroll
+            for (int r = 0; r < kS3Rep; r++) hval[r * HS + x] = 0u;
+        }
         for (int w = tl; w < FB; w += 64 * W) fb[w] = 0ull;
         s3_sync<W>();
-        // pass 1: touched frames = OR of pfm rows of V; T = |V|
-        int myT = 0;
-        for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
-            const int k = k0 + lane;
-            const int p = k < en ? pts[k] : 0;
-            const bool nb = k < en && !boundary[p];
-            myT += nb ? 1 : 0;
-            for (int w = 0; w < FW; w++) {
-                unsigned long long v = nb ? pfm[static_cast<size_t>(p) * FW + w] : 0ull;
-                v = wave_or64(v);
-                if (lane == 0 && v) atomicOr(&fb[w], v);
+        // pass A: sweeps of 64·kS3U points per wave (their metadata loads all in flight)
+        int myT = 0, ovf = 0;
+        for (int k0 = b + wl * 64 * kS3U; k0 < en; k0 += 64 * W * kS3U) {
+            int p[kS3U], o0[kS3U], o1[kS3U];
+            bool nb[kS3U];
+#pragma unroll
+            for (int u = 0; u < kS3U; u++) {
+                const int k = k0 + u * 64 + lane;
+                p[u] = k < en ? pts[k] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kS3U; u++) {
+                nb[u] = false;
+                o0[u] = o1[u] = 0;
+                if (p[u] >= 0) {
+                    nb[u] = !boundary[p[u]];
+                    o0[u] = pt_off[p[u]];
+                    o1[u] = pt_off[p[u] + 1];
+                }
+            }
+            int st[kS3U], d[kS3U];
+            int E = 0, nseg = 0;
+#pragma unroll
+            for (int u = 0; u < kS3U; u++) {
+                d[u] = nb[u] ? o1[u] - o0[u] : 0;  // >= 1 for a kept point: it lies in g
+                myT += nb[u] ? 1 : 0;
+                const int inc = wave_incl_scan(d[u]);
+                st[u] = E + inc - d[u];  // flat start of this lane's segment
+                E += __shfl(inc, 63, 64);
+                const unsigned long long hold = __ballot(d[u] > 0);
+                if (d[u] > 0) dl[nseg + __popcll(hold & lt_mask)] = o0[u] - st[u];  // segment rank -> pt_list - flat
+                nseg += __popcll(hold);
+            }
+            for (int base = 0; base < E; base += 64 * kS3Batch) {
+                if (lane < kS3Batch) sbits[lane] = 0ull;
+                wave_sync();
+                int run = 0;  // segments begun before base
+#pragma unroll
+                for (int u = 0; u < kS3U; u++) {
+                    if (d[u] > 0 && st[u] >= base && st[u] < base + 64 * kS3Batch)
+                        atomicOr(&sbits[(st[u] - base) >> 6], 1ull << ((st[u] - base) & 63));
+                    run += __popcll(__ballot(d[u] > 0 && st[u] < base));
+                }
+                wave_sync();
+                unsigned ent[kS3Batch];
+#pragma unroll
+                for (int r = 0; r < kS3Batch; r++) {
+                    const int kk = base + r * 64 + lane;
+                    const unsigned long long m = sbits[r];
+                    const int rk = run + __popcll(m & le_mask) - 1;
+                    run += __popcll(m);
+                    ent[r] = kk < E ? pt_list[dl[rk] + kk] : kS3Empty;
+                }
+#pragma unroll
+                for (int r = 0; r < kS3Batch; r++) {
+                    const unsigned e = ent[r];
+                    if (e == kS3Empty) continue;
+                    unsigned h = (e * 2654435761u) >> (32 - __builtin_ctz(HS));
+                    int pr = 0;
+                    for (; pr < HS; pr++) {
+                        const unsigned old = atomicCAS(&hkey[h], kS3Empty, e);
+                        if (old == kS3Empty || old == e) {
+                            atomicAdd(&hval_l[h], 1u);
+                            break;
+                        }
+                        h = (h + 1) & (HS - 1);
+                    }
+                    ovf |= pr == HS ? 1 : 0;
+                }
+                wave_sync();
             }
         }
-        int T;
-        if (W == 1) T = wave_sum(myT);
-        else T = block_sum<64 * W>(myT, ws);
-        s3_sync<W>();
-        int ntf = 0;
-        for (int w0 = 0; w0 < FB; w0 += 64 * W) {  // rank prefix over bitmap words
-            const int w = w0 + tl;
-            const int pc = w < FB ? __popcll(fb[w]) : 0;
-            int tot;
-            const int ex = s3_excl_scan<W>(pc, ws, tot);
-            if (w < FB) wpre[w] = ex + ntf;
-            ntf += tot;
-        }
+        const int T = s3_sum<W>(myT, ws);
+        const int any_ovf = s3_sum<W>(__ballot(ovf) ? 1 : 0, ws);  // wave-uniform per wave
         s3_sync<W>();
         int vis = 0, split = 0, ncont = 0;
-        for (int j0 = 0; j0 < ntf;) {
-            for (int w = tl; w < FB; w += 64 * W) {  // frames of rank [j0, j0 + WIN)
-                unsigned long long bits = fb[w];
-                int r = wpre[w];
-                while (bits) {
-                    const int bt = __ffsll(static_cast<long long>(bits)) - 1;
-                    bits &= bits - 1;
-                    if (r >= j0 && r < j0 + WIN) tf_frame[r - j0] = (w << 6) + bt;
-                    r++;
+        if (any_ovf) {
+            s3_dense<W>(b, en, wl, lane, tl, wv, pts, pt_off, pt_list, boundary, pfm, FW, FB, frame_start,
+                        mask_label, mvt, ctn, crow, fb, wpre, tf_frame, tsl_s[slot], cnt, spre_s[wv], spb_s[wv], ws,
+                        ncont, vis, split);
+        } else {
+            // pass B: touched frames = frames of the keys
+            for (int x = tl; x < HS; x += 64 * W) {
+                const unsigned key = hkey[x];
+                if (key != kS3Empty) {
+                    const unsigned c = key >> kLocalBits;
+                    atomicOr(&fb[c >> 6], 1ull << (c & 63));
                 }
             }
             s3_sync<W>();
-            const int jmax = min(WIN, ntf - j0);
-            const int fr = tl < jmax ? tf_frame[tl] : 0;
-            const int fs_l = tl < jmax ? frame_start[fr] : 0;
-            const int nm = tl < jmax ? frame_start[fr + 1] - fs_l : 0;
-            int tot;
-            const int ex = s3_excl_scan<W>(nm, ws, tot);
-            // window = longest prefix of frames whose counters fit (at least one frame)
-            int jn;
-            {
-                const int fits = (tl < jmax && ex + nm <= CNT) ? 1 : 0;
-                int nf;
-                s3_excl_scan<W>(fits, ws, nf);
-                jn = max(1, nf);
-            }
-            if (tl < jn) tf_slot[tl] = ex;
-            if (tl == jn - 1) tf_slot[jn] = ex + nm;
+            const int ntf = s3_rank_prefix<W>(fb, wpre, FB, tl, ws);
             s3_sync<W>();
-            const int nslots = tf_slot[jn];
-            for (int x = tl; x < nslots; x += 64 * W) cnt[x] = 0;
-            s3_sync<W>();
-            // pass 2: counts.  Per chunk of 64 points the list entries are flattened and
-            // gathered kS3Batch per lane before any is consumed (independent loads in flight).
-            {
-                int *spre = spre_s[wv], *spb = spb_s[wv];
-                for (int k0 = b + wl * 64; k0 < en; k0 += 64 * W) {
-                    const int k = k0 + lane;
-                    int pb = 0, d = 0;
-                    if (k < en) {
-                        const int p = pts[k];
-                        if (!boundary[p]) {
-                            pb = pt_off[p];
-                            d = pt_off[p + 1] - pb;
-                        }
-                    }
-                    const int inc = wave_incl_scan(d);
-                    const int E = __shfl(inc, 63, 64);
-                    spre[lane] = inc - d;
-                    spb[lane] = pb;
-                    wave_sync();
-                    for (int base = 0; base < E; base += 64 * kS3Batch) {
-                        unsigned ent[kS3Batch];
+            for (int j0 = 0; j0 < ntf; j0 += WIN) {
+                fnz[tl] = 0;
+                fbest[tl] = 0ull;
+                s3_sync<W>();
+                for (int x = tl; x < HS; x += 64 * W) {
+                    const unsigned key = hkey[x];
+                    if (key == kS3Empty) continue;
+                    const unsigned c = key >> kLocalBits;
+                    const int rr = s3_rank(fb, wpre, c) - j0;
+                    if (rr < 0 || rr >= WIN) continue;
+                    unsigned v = 0;
 #pragma unroll
-                        for (int r = 0; r < kS3Batch; r++) {
-                            const int kk = base + r * 64 + lane;
-                            ent[r] = 0xffffffffu;
-                            if (kk < E) {
-                                int lo = 0;
-#pragma unroll
-                                for (int st = 32; st >= 1; st >>= 1)
-                                    if (spre[lo + st] <= kk) lo += st;
-                                ent[r] = pt_list[spb[lo] + kk - spre[lo]];
-                            }
-                        }
-#pragma unroll
-                        for (int r = 0; r < kS3Batch; r++) {
-                            const unsigned e = ent[r];
-                            if (e == 0xffffffffu) continue;
-                            const unsigned c = e >> kLocalBits;
-                            const int rr = wpre[c >> 6] + __popcll(fb[c >> 6] & ((1ull << (c & 63)) - 1ull)) - j0;
-                            if (rr >= 0 && rr < jn) atomicAdd(&cnt[tf_slot[rr] + static_cast<int>(e & (kMaxMasksPerFrame - 1))], 1);
-                        }
-                    }
-                    wave_sync();
+                    for (int r = 0; r < kS3Rep; r++) v += hval[r * HS + x];
+                    const unsigned l = key & (kMaxMasksPerFrame - 1);
+                    const int fs = frame_start[c];
+                    tf_frame[rr] = fs;  // same value from every key of the frame
+                    atomicAdd(&fnz[rr], static_cast<int>(v));
+                    // count, then smallest label (labels are in [1, 65535]), then the slot
+                    const unsigned long long pk = (static_cast<unsigned long long>(v) << 32) |
+                                                  (static_cast<unsigned long long>(65535 - mask_label[fs + l]) << 16) | l;
+                    atomicMax(&fbest[rr], pk);
                 }
-            }
-            s3_sync<W>();
-            // pass 3: the reference's per-frame decision
-            int dec = 0, tgt = 0;
-            if (tl < jn) {
-                const int base = tf_slot[tl];
-                int nz = 0, bc = 0, best = -1;
-                for (int l = 0; l < nm; l++) {
-                    const int v = cnt[base + l];
-                    nz += v;
-                    if (v > bc) {
-                        bc = v;
-                        best = l;
-                    } else if (v == bc && v > 0 && mask_label[fs_l + l] < mask_label[fs_l + best]) {
-                        best = l;  // np.argmax: smallest id on ties
-                    }
+                s3_sync<W>();
+                int dec = 0, tgt = 0;
+                if (tl < min(WIN, ntf - j0)) {
+                    const unsigned long long pk = fbest[tl];
+                    dec = s3_decide(T, fnz[tl], static_cast<int>(pk >> 32), mvt, ctn);
+                    tgt = tf_frame[tl] + static_cast<int>(pk & 0xffffu);
                 }
-                const int c0 = T - nz;
-                if (1.0 - static_cast<double>(c0) / static_cast<double>(T) < mvt && nz < 500) dec = 0;
-                else if (static_cast<double>(bc) / static_cast<double>(nz) > ctn) dec = 2;
-                else dec = 1;
-                tgt = fs_l + best;
+                s3_emit<W>(dec, tgt, crow, ncont, vis, split, ws);
+                s3_sync<W>();
             }
-            // ordered compaction of contained frames -> C row entries (frame order)
-            int ncw;
-            const int pos = s3_excl_scan<W>(dec == 2 ? 1 : 0, ws, ncw);
-            if (dec == 2) crow[ncont + pos] = tgt;
-            ncont += ncw;
-            int nv, ns;
-            s3_excl_scan<W>(dec >= 1 ? 1 : 0, ws, nv);
-            s3_excl_scan<W>(dec == 1 ? 1 : 0, ws, ns);
-            vis += nv;
-            split += ns;
-            j0 += jn;
-            s3_sync<W>();
         }
         if (tl == 0) {
             crow_len[g] = ncont;
             // construction.py:132
             useg[g] = (vis == 0 || static_cast<double>(split) / static_cast<double>(vis) > ust) ? 1 : 0;
         }
+        s3_sync<W>();
     }
 }
 

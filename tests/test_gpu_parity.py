@@ -173,3 +173,31 @@ def test_repeat_is_deterministic(run):
     b = run.canonical()
     for k in a:
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+
+
+def test_s3_pair_table_overflow(run):
+    """S3 masks meeting more (frame, mask) pairs than the LDS hash table holds (512 for
+    wave masks, 2048 for workgroup masks) take the dense-counter path; results must not
+    change.  Frames 0..199 cut the points into 12 random masks each (2400 pairs per point
+    set); frame 200 adds a 1000-point mask (wave kernel), frame 201 a 4000-point mask
+    (workgroup kernel), frame 202 small masks that stay in the table."""
+    from maskclustering_amd.synthetic import SceneMasks
+    from oracle import oracle
+    rng = np.random.default_rng(7)
+    P = 4000
+    frames = []
+    for _ in range(200):
+        part = rng.integers(0, 12, P)
+        frames.append([(k + 1, np.nonzero(part == k)[0]) for k in range(12)])
+    frames.append([(1, np.arange(1000)), (2, np.arange(1000, 1500))])
+    frames.append([(3, np.arange(P))])
+    frames.append([(k + 1, np.arange(3000 + 40 * k, 3040 + 40 * k)) for k in range(5)])
+    s = SceneMasks.from_frame_lists(P, frames)
+    for cfg in ((0.05, 0.5, 0.5, 0.1), (0.2, 0.99, 0.9, 0.15)):  # configs with visible frames
+        mvt, ust, ct, cont = cfg
+        want = oracle.run(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts,
+                          mvt, ust, ct, cont)
+        inp = dict(num_points=s.num_points, num_frames=s.num_frames, mask_col=s.mask_col, mask_label=s.mask_label,
+                   mask_off=s.mask_off, mask_pts=s.mask_pts, mask_visible_threshold=mvt,
+                   undersegment_filter_threshold=ust, view_consensus_threshold=ct, contained_threshold=cont)
+        assert_matches(_run_case(run, inp), want)
