@@ -71,6 +71,7 @@ struct mc_ctx {
     // ---- S6 ----
     DevBuf d_parent, d_root, d_isroot, d_rank, d_label, d_levels, d_memcnt, d_memoff, d_ublen, d_newoff;
     DevBuf d_members, d_colcnt, d_coloff, d_colnodes, d_ovf_list, d_ovf_n, d_scratch, d_touched, d_edges;
+    DevBuf d_spread;  // spread slots of the S2 boundary counter
     DevBuf d_Nlev, d_final_label;
     DevBuf d_poolA, d_poolB, d_offA, d_offB, d_lenA, d_lenB, d_vfA, d_vfB, d_ownA, d_ownB, d_cap;
     DevBuf d_pmin, d_pmax, d_nwords, d_woff, d_bm, d_ptcnt, d_ptoff_out, d_pts_out;
@@ -203,7 +204,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_parent, &ctx->d_root, &ctx->d_isroot, &ctx->d_rank, &ctx->d_label, &ctx->d_levels,
                       &ctx->d_memcnt, &ctx->d_memoff, &ctx->d_ublen, &ctx->d_newoff, &ctx->d_members, &ctx->d_colcnt,
                       &ctx->d_coloff, &ctx->d_colnodes, &ctx->d_ovf_list, &ctx->d_ovf_n, &ctx->d_scratch,
-                      &ctx->d_touched, &ctx->d_edges, &ctx->d_Nlev, &ctx->d_final_label,
+                      &ctx->d_touched, &ctx->d_edges, &ctx->d_spread, &ctx->d_Nlev, &ctx->d_final_label,
                       &ctx->d_poolA, &ctx->d_poolB, &ctx->d_offA, &ctx->d_offB, &ctx->d_lenA, &ctx->d_lenB,
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
                       &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out, &ctx->d_owner0,
@@ -395,6 +396,7 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
 
         // S2/S3/S4 buffers (allocated once per scene; nothing is allocated while building)
         ctx->d_deg.reserve((P + 1) * sizeof(int));
+        ctx->d_spread.reserve(mc::kSpread * mc::kSpreadStrideI * sizeof(int));
         MC_HIP(hipMemsetAsync(ctx->d_deg.ptr, 0, (P + 1) * sizeof(int), s));  // kept zero by the S2 scatter
         ctx->d_pt_off.reserve((P + 2) * sizeof(int));
         ctx->d_pt_list.reserve((nnz + 1) * sizeof(unsigned));
@@ -469,7 +471,7 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         {  // S2
             TimedScope ts(ctx->timer, s, "s2_point_lists");
             hipLaunchKernelGGL(mc::k_s2_degree, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(), nnz,
-                               ctx->d_deg.as<int>(), stats, static_cast<int>(ST_COUNT));
+                               ctx->d_deg.as<int>(), stats, static_cast<int>(ST_COUNT), ctx->d_spread.as<int>());
             mc::scan_large(s, ctx->d_deg.as<int>(), ctx->d_pt_off.as<int>(), static_cast<int>(P), ctx->d_scan_tmp.as<int>());
             if (M)
                 hipLaunchKernelGGL(mc::k_s2_scatter, dim3(M), dim3(256), 0, s, ctx->d_mask_off.as<int>(),
@@ -479,7 +481,7 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
                 hipLaunchKernelGGL(mc::k_s2_points, dim3(ceil_div(P, 256)), dim3(256), 0, s, ctx->d_pt_off.as<int>(),
                                    ctx->d_pt_list.as<unsigned>(), static_cast<int>(P), FW,
                                    ctx->d_boundary.as<unsigned char>(), ctx->d_pfm.as<unsigned long long>(),
-                                   stats + ST_NBND);
+                                   ctx->d_spread.as<int>());
         }
         if (M) {  // S3
             TimedScope ts(ctx->timer, s, "s3_masks");
@@ -519,7 +521,7 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
             hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(std::max(M, F + 1), 256)), dim3(256), 0, s,
                                ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
                                ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>(),
-                               ctx->d_hist.as<unsigned long long>());
+                               ctx->d_hist.as<unsigned long long>(), ctx->d_spread.as<int>(), stats + ST_NBND);
             mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC,
                               ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), stats + ST_N0);
             hipLaunchKernelGGL(mc::k_s3_undo_write, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
@@ -859,7 +861,7 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             MC_HIP(hipMemsetAsync(ctx->d_scratch.ptr, 0, static_cast<size_t>(kOvfBlocks) * n0 * 4, s));
             ctx->scratch_n0 = N0;
         }
-        ctx->d_edges.reserve(std::max(nthr, 1) * 8);
+        ctx->d_edges.reserve(static_cast<size_t>(std::max(nthr, 1)) * mc::kSpread * mc::kSpreadStrideL * 8);  // spread slots
         ctx->d_Nlev.reserve((nthr + 2) * 4);
         ctx->d_cap.reserve((nthr + 2) * 4);
         ctx->d_final_label.reserve(n0 * 4);
@@ -1083,9 +1085,16 @@ int mc_cluster_get_edge_counts(mc_ctx *ctx, int64_t *edges)
 {
     return guarded(ctx, [&] {
         MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        const size_t per = static_cast<size_t>(mc::kSpread) * mc::kSpreadStrideL;
+        std::vector<unsigned long long> h(static_cast<size_t>(ctx->n_iter) * per);
         if (ctx->n_iter)
-            MC_HIP(hipMemcpyAsync(edges, ctx->d_edges.ptr, ctx->n_iter * 8, hipMemcpyDeviceToHost, ctx->stream));
+            MC_HIP(hipMemcpyAsync(h.data(), ctx->d_edges.ptr, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
         MC_HIP(hipStreamSynchronize(ctx->stream));
+        for (int t = 0; t < ctx->n_iter; t++) {  // fold the spread slots
+            unsigned long long v = 0;
+            for (int k = 0; k < mc::kSpread; k++) v += h[t * per + k * mc::kSpreadStrideL];
+            edges[t] = static_cast<int64_t>(v);
+        }
     });
 }
 

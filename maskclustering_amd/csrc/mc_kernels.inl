@@ -87,6 +87,21 @@ __device__ __forceinline__ void st_agent(int *p, int v)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Counters that many workgroups add to: one atomic on a single address serialises at its L2
+// channel (~10 ns each, measured: 8192 waves -> ~90 us), so adds go to one of kSpread slots
+// 128 B apart, picked by workgroup, and the reader folds the slots.
+constexpr int kSpread = 64;
+constexpr int kSpreadStrideI = 32;   // ints
+constexpr int kSpreadStrideL = 16;   // u64
+__device__ __forceinline__ void spread_add(int *base, int v)
+{
+    atomicAdd(base + (blockIdx.x & (kSpread - 1)) * kSpreadStrideI, v);
+}
+__device__ __forceinline__ void spread_add(unsigned long long *base, unsigned long long v)
+{
+    atomicAdd(base + (blockIdx.x & (kSpread - 1)) * kSpreadStrideL, v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // scans
 // ---------------------------------------------------------------------------------------------
@@ -202,9 +217,10 @@ void scan_large(hipStream_t s, const int *in, int *out, int n, int *tmp /* >= 2*
 // ---------------------------------------------------------------------------------------------
 // deg[p] += 1 for every (mask, point) entry.  Block 0 also clears the statistics block.
 __global__ __launch_bounds__(256) void k_s2_degree(const int *__restrict__ pts, int nnz, int *__restrict__ deg,
-                                                   int *__restrict__ stats, int nstats)
+                                                   int *__restrict__ stats, int nstats, int *__restrict__ spread)
 {
     if (blockIdx.x == 0 && threadIdx.x < nstats) stats[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kSpread) spread[threadIdx.x * kSpreadStrideI] = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nnz; i += gridDim.x * 256) atomicAdd(&deg[pts[i]], 1);
 }
 
@@ -289,7 +305,7 @@ __global__ __launch_bounds__(256) void k_s2_points(const int *__restrict__ pt_of
     }
     if (p < P) boundary[p] = static_cast<unsigned char>(isb);
     const unsigned long long bal = __ballot(isb);
-    if (lane_id() == 0 && bal) atomicAdd(nbnd, __popcll(bal));
+    if (lane_id() == 0 && bal) spread_add(nbnd, __popcll(bal));  // folded by k_s3_undo_count
 }
 
 // Dense point_in_mask_matrix (uint16 P×F) for the getter only (construction.py:39,58,61).
@@ -732,9 +748,14 @@ __global__ __launch_bounds__(S3Cfg<W>::NT) void k_s3_masks(
 __global__ __launch_bounds__(256) void k_s3_undo_count(const int *__restrict__ ctmp, const int *__restrict__ crow_len,
                                                        const unsigned char *__restrict__ useg, int M, int F,
                                                        int *__restrict__ keep_cnt, int *__restrict__ node_flag,
-                                                       unsigned long long *__restrict__ hist)
+                                                       unsigned long long *__restrict__ hist,
+                                                       const int *__restrict__ nbnd_spread, int *__restrict__ nbnd)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // fold the boundary count of k_s2_points
+        const int v = wave_sum(threadIdx.x < kSpread ? nbnd_spread[threadIdx.x * kSpreadStrideI] : 0);
+        if (threadIdx.x == 0) *nbnd = v;
+    }
     for (int v = g; v <= F; v += gridDim.x * 256) hist[v] = 0ull;
     if (g >= M) return;
     const int *row = ctmp + static_cast<size_t>(g) * F;
@@ -1138,6 +1159,11 @@ __global__ __launch_bounds__(64) void k6_colupdate(int Mn, const int *__restrict
 struct EdgeRule {
     float thr;  // observer_num_threshold (np.float32 or the int 1) as float32
     float ct;   // connect_threshold as float32
+    int omin;   // smallest integer O with fl32(O) >= thr
+    __device__ EdgeRule(float thr_, float ct_) : thr(thr_), ct(ct_)
+    {
+        omin = !(thr_ > 0.0f) ? 0 : (thr_ > 1.0e9f ? 1000000000 : static_cast<int>(ceilf(thr_)));
+    }
 };
 
 __device__ __forceinline__ bool edge_ok(int o, int s, EdgeRule er)
@@ -1148,6 +1174,11 @@ __device__ __forceinline__ bool edge_ok(int o, int s, EdgeRule er)
     return rate >= er.ct;
 }
 
+// Exact pre-filter on the supporter count alone: the rule is monotone non-increasing in O
+// (int->float, +1e-7, S/x and every rounding are monotone), so if it fails at the smallest
+// admissible O it fails for every O and the pair needs no observer count.
+__device__ __forceinline__ bool edge_possible(int s, EdgeRule er) { return edge_ok(er.omin, s, er); }
+
 // K4: supporter counts by sparse expansion (Gustavson row-by-row C·Cᵀ), one wave per node a:
 //   S[a,b] = |C_a ∩ C_b| = #{m in C_a : b in col(m)}, accumulated in an LDS hash for b > a.
 // Only pairs with S >= 1 can pass the rate test when ct > 0, so every candidate edge is
@@ -1155,9 +1186,10 @@ __device__ __forceinline__ bool edge_ok(int o, int s, EdgeRule er)
 // merged with union-find at once.  Loads are batched (independent gathers in flight
 // before use); only the hash slots actually used are scanned and reset.
 constexpr int kHashBits = 9, kHashSize = 1 << kHashBits, kHashMaxFill = (kHashSize * 3) / 4;
-constexpr int kPairWaves = 4, kPairBatch = 8, kTestBatch = 4;
+constexpr int kPairWaves = 4, kPairBatch = 8, kTestBatch = 4, kTestWords = 4;
 // Profiling ablations (timing-only builds, results wrong): 1 = no union-find,
-// 2 = no hash insert (expansion loads only), 3 = no partner test phase.
+// 2 = no hash insert (expansion loads only), 3 = no partner test phase, 4 = no edge-count
+// atomic, 5 = neither edge-count atomic nor union-find.
 #ifndef MC_ABLATE_PAIRS
 #define MC_ABLATE_PAIRS 0
 #endif
@@ -1283,19 +1315,28 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                         sc[r] = cnts[sl];
                         keys[sl] = -1;
                         cnts[sl] = 0;
+                        if (!edge_possible(sc[r], er)) bn[r] = -1;
                     }
                 }
-                for (int w = 0; w < FW; w++) {
-                    const unsigned long long aw = va[w];
+                for (int w0 = 0; w0 < FW; w0 += kTestWords) {  // all words of a chunk in flight at once
+                    unsigned long long aw[kTestWords], bw[kTestBatch][kTestWords];
+#pragma unroll
+                    for (int j = 0; j < kTestWords; j++) aw[j] = w0 + j < FW ? va[w0 + j] : 0ull;
 #pragma unroll
                     for (int r = 0; r < kTestBatch; r++)
-                        if (bn[r] >= 0) ob[r] += __popcll(aw & nvf[static_cast<size_t>(bn[r]) * FW + w]);
+#pragma unroll
+                        for (int j = 0; j < kTestWords; j++)
+                            bw[r][j] = (bn[r] >= 0 && w0 + j < FW) ? nvf[static_cast<size_t>(bn[r]) * FW + w0 + j] : 0ull;
+#pragma unroll
+                    for (int r = 0; r < kTestBatch; r++)
+#pragma unroll
+                        for (int j = 0; j < kTestWords; j++) ob[r] += __popcll(aw[j] & bw[r][j]);
                 }
 #pragma unroll
                 for (int r = 0; r < kTestBatch; r++) {
                     if (bn[r] >= 0 && edge_ok(ob[r], sc[r], er)) {
                         nedges++;
-                        if (MC_ABLATE_PAIRS != 1) uf_unite(parent, a, bn[r]);
+                        if (MC_ABLATE_PAIRS != 1 && MC_ABLATE_PAIRS != 5) uf_unite(parent, a, bn[r]);
                     }
                 }
             }
@@ -1311,7 +1352,8 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     // wave-reduce the edge count
     int ne = static_cast<int>(nedges);
     ne = wave_sum(ne);
-    if (lane == 0 && ne) atomicAdd(edges + t, static_cast<unsigned long long>(ne));
+    if (MC_ABLATE_PAIRS >= 4) return;
+    if (lane == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
 }
 
 // K4b: nodes whose partner set overflowed the LDS hash.  Dense global counters per
@@ -1352,6 +1394,7 @@ __global__ __launch_bounds__(256) void k6_pairs_overflow(
             const int bnode = tl[k];
             const int s = scr[bnode];
             scr[bnode] = 0;
+            if (!edge_possible(s, er)) continue;
             const unsigned long long *vb = nvf + static_cast<size_t>(bnode) * FW;
             int ob = 0;
             for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
@@ -1363,7 +1406,7 @@ __global__ __launch_bounds__(256) void k6_pairs_overflow(
         __syncthreads();
     }
     int ne = block_sum<256>(static_cast<int>(nedges), ws);
-    if (threadIdx.x == 0 && ne) atomicAdd(edges + t, static_cast<unsigned long long>(ne));
+    if (threadIdx.x == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
 }
 
 // Dense observer-only pairs for ct <= 0 (every pair with O >= thr is an edge, S unused).
@@ -1388,7 +1431,7 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
         }
     }
     int ne = block_sum<256>(static_cast<int>(nedges), ws);
-    if (threadIdx.x == 0 && ne) atomicAdd(edges + t, static_cast<unsigned long long>(ne));
+    if (threadIdx.x == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
 }
 
 // K5: root of every node; flag roots (= smallest member of each component).
@@ -1562,7 +1605,7 @@ __global__ __launch_bounds__(256) void k6_init(int N0, int *__restrict__ final_l
         *Nlev = n0_src ? *n0_src : n0_host;
         *cap0 = cap_src ? *cap_src : cap_host;
     }
-    for (int i = i0; i < nthr; i += gridDim.x * 256) edges[i] = 0ull;
+    for (int i = i0; i < nthr * kSpread; i += gridDim.x * 256) edges[static_cast<size_t>(i) * kSpreadStrideL] = 0ull;
     for (int i = i0; i < N0; i += gridDim.x * 256) final_label[i] = i;
 }
 
