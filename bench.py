@@ -189,6 +189,55 @@ class EndToEndStep:
                 "scene_ms": round(cpu_s * 1e3, 1)}
 
 
+class ShardedEndToEndStep(EndToEndStep):
+    """--variant e2e --shard frames: ONE scene per step for the whole job.  Rank r holds its
+    frame slice in HBM, back-projects it, the mask lists are all-gathered over RCCL and
+    S2-S6 run replicated (maskclustering_amd/frame_shard.py)."""
+
+    def __init__(self, shape, seed, local):
+        import torch
+        from maskclustering_amd import _native
+        from maskclustering_amd.frame_shard import FrameShardedScene
+        from maskclustering_amd.pipeline import GraphRun
+        from maskclustering_amd.synthetic_frames import make_frames_shape
+        t0 = time.perf_counter()
+        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}")
+        self.fr = fr
+        dev = torch.device("cuda", local)
+        self.run = GraphRun(local)
+        self.ctx = self.run.ctx
+        self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
+        self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+        self.sh = FrameShardedScene(self.run, fr.num_points, fr.num_frames)
+        lo, hi = self.sh.lo, self.sh.hi
+        up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+        self.t_depth = up(fr.depth[lo:hi], torch.float32)
+        self.t_seg = up(fr.seg[lo:hi], torch.uint8)
+        self.t_K = up(fr.intrinsics[lo:hi], torch.float64)
+        self.t_T = up(fr.poses[lo:hi].reshape(-1, 16), torch.float64)
+        self.prm = _native.bp_params()
+        self.groups = BP_GROUPS + G_GROUPS
+        F, H, W = fr.depth.shape
+        self.shape = (hi - lo, H, W)
+        log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F}, rendered in {time.perf_counter() - t0:.1f} s")
+        self.workload = (f"{shape}: ScanNet-shaped synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
+                         f"S1-S6, frames sharded over {self.sh.world} GPU(s)")
+
+    def step(self):
+        self.sh.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
+        self.sh.step(**CFG)
+
+    def work(self):
+        F, H, W = self.shape
+        n = int(self.ctx.graph_info().num_masks)
+        pts = self.sh.pts.cpu().numpy()
+        w = graph_work(self.ctx, pts, self.fr.num_points, self.fr.num_frames)
+        w.update(bp_work(self.ctx, F, H, W))
+        assert n > 0
+        return w
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,6 +247,9 @@ def main():
     ap.add_argument("--shape", default="c2")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=["scene", "frames"], default="scene",
+                    help="scene: every rank its own scene (weak scaling); frames: one scene, frames split "
+                         "over the ranks (e2e only, strong scaling)")
     args = ap.parse_args()
 
     import torch
@@ -210,8 +262,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    # every rank its own scene (weak scaling)
-    runner = (GraphStep if args.variant == "g" else EndToEndStep)(args.shape, args.seed + rank, local)
+    frames = args.shard == "frames"
+    if frames and args.variant != "e2e":
+        raise SystemExit("--shard frames needs --variant e2e (S1 is the stage that shards by frame)")
+    if frames:  # one scene, frame slices per rank (strong scaling)
+        runner = ShardedEndToEndStep(args.shape, args.seed, local)
+    else:  # every rank its own scene (weak scaling)
+        runner = (GraphStep if args.variant == "g" else EndToEndStep)(args.shape, args.seed + rank, local)
     ctx = runner.run.ctx
 
     for _ in range(args.warmup):
@@ -255,7 +312,7 @@ def main():
     elapsed = float(t.item())
 
     gi = ctx.graph_info()
-    total_pairs = pairs_per_step * args.steps * world
+    total_pairs = pairs_per_step * args.steps * (1 if frames else world)
     value = total_pairs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -282,7 +339,7 @@ def main():
             roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames:
         cpu = runner.cpu_baseline()
 
     if rank == 0:
@@ -295,7 +352,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if frames else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
@@ -303,7 +360,7 @@ def main():
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
                        "stage_ms": {k: round(v, 4) for k, v in calib.items()},
-                       "parallelism": f"scene-parallel x{world}"},
+                       "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -149,6 +149,11 @@ int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info);
 int mc_backproject_get_masks(mc_ctx *ctx, int32_t *mask_col, int32_t *mask_label, int64_t *mask_off,
                              int32_t *mask_pts);
 int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats /* num_candidates * MC_BP_NSTAT */);
+/* mask_pts into a device buffer (stream-ordered on the context stream, no host copy): the
+ * frame-sharded path all-gathers the per-rank point lists over RCCL;
+ * mask_col / mask_label / mask_off come from mc_backproject_get_masks with mask_pts = NULL */
+int mc_backproject_copy_points_device(mc_ctx *ctx, int32_t *mask_pts_dev);
+
 /* the back-projected masks become the graph input (as mc_scene_set_masks, device-resident) */
 int mc_scene_use_backprojection(mc_ctx *ctx);
 

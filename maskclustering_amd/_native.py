@@ -34,6 +34,7 @@ EXPORTED = [
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
+    "mc_backproject_copy_points_device",
 ]
 
 MC_BP_NSTAT = 10
@@ -138,6 +139,7 @@ def load():
         "mc_backproject": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, ctypes.c_int, P(BpParams)]),
         "mc_backproject_get_info": (ctypes.c_int, [vp, P(BpInfo)]),
         "mc_backproject_get_masks": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        "mc_backproject_copy_points_device": (ctypes.c_int, [vp, vp]),
         "mc_backproject_get_candidates": (ctypes.c_int, [vp, vp]),
         "mc_scene_use_backprojection": (ctypes.c_int, [vp]),
     }
@@ -403,6 +405,19 @@ def _bp_methods():
         self._check(self.L.mc_backproject_get_masks(self.h, _ptr(col), _ptr(lab), _ptr(off), _ptr(pts)))
         return col[:M], lab[:M], off, pts[:info.num_mask_points]
 
+    def bp_mask_index(self):
+        """(mask_col, mask_label, mask_off) of the back-projected masks, without the point lists."""
+        M = self.bp_info().num_masks
+        col = np.zeros(max(M, 1), np.int32)
+        lab = np.zeros(max(M, 1), np.int32)
+        off = np.zeros(M + 1, np.int64)
+        self._check(self.L.mc_backproject_get_masks(self.h, _ptr(col), _ptr(lab), _ptr(off), None))
+        return col[:M], lab[:M], off
+
+    def bp_points_to_device(self, dst_ptr):
+        """Stream-ordered device-to-device copy of the mask point lists (int32) to dst_ptr."""
+        self._check(self.L.mc_backproject_copy_points_device(self.h, ctypes.c_void_p(int(dst_ptr))))
+
     def bp_candidates(self):
         n = self.bp_info().num_candidates
         st = np.zeros((max(n, 1), MC_BP_NSTAT), np.int32)
@@ -412,7 +427,8 @@ def _bp_methods():
     def use_backprojection(self):
         self._check(self.L.mc_scene_use_backprojection(self.h))
 
-    for f in (set_points, backproject, bp_info, bp_masks, bp_candidates, use_backprojection):
+    for f in (set_points, backproject, bp_info, bp_masks, bp_mask_index, bp_points_to_device, bp_candidates,
+              use_backprojection):
         setattr(Context, f.__name__, f)
 
 

@@ -1539,6 +1539,16 @@ int mc_backproject_get_masks(mc_ctx *ctx, int32_t *mask_col, int32_t *mask_label
     });
 }
 
+int mc_backproject_copy_points_device(mc_ctx *ctx, int32_t *mask_pts_dev)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_bp, MC_ERR_STATE, "no back-projection result");
+        MC_REQUIRE(mask_pts_dev || !ctx->bp_nnz, MC_ERR_INVALID, "null destination");
+        if (ctx->bp_nnz)
+            MC_HIP(hipMemcpyAsync(mask_pts_dev, ctx->d_bp_pts.ptr, ctx->bp_nnz * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    });
+}
+
 int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats)
 {
     return guarded(ctx, [&] {

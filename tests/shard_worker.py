@@ -1,0 +1,63 @@
+"""Worker processes of the frame-sharding tests (tests/test_frame_shard*.py).
+
+    python tests/shard_worker.py <mode> <rank> <world> <port> <out.npz>
+
+mode "gather" (CPU, gloo): every rank cuts the synthetic scene's masks to its frame slice,
+all-gathers them with maskclustering_amd.frame_shard.gather_masks and saves the result.
+mode "e2e" (GPU, gloo over host tensors: all ranks share cuda:0): every rank back-projects
+its frame slice on the device, all-gathers, runs S2-S6 and saves the canonical outputs.
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from maskclustering_amd.frame_shard import FrameShardedScene, frame_slice, gather_masks  # noqa: E402
+
+
+def local_masks(scene, lo, hi):
+    sel = np.nonzero((scene.mask_col >= lo) & (scene.mask_col < hi))[0]
+    lens = np.diff(scene.mask_off)[sel]
+    off = np.zeros(len(sel) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    pts = np.concatenate([scene.mask_points(g) for g in sel]) if len(sel) else np.zeros(0, np.int32)
+    return scene.mask_col[sel] - lo, scene.mask_label[sel], off, pts.astype(np.int32)
+
+
+def main():
+    mode, rank, world, port, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        if mode == "gather":
+            from maskclustering_amd.synthetic import make_shape
+            s = make_shape("tiny", seed=4)
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+            g = gather_masks(col, lab, off, torch.from_numpy(pts), lo)
+            np.savez(out, col=g[0], label=g[1], off=g[2], pts=g[3].numpy())
+        else:
+            from maskclustering_amd.pipeline import GraphRun
+            from maskclustering_amd.synthetic_frames import make_frames_shape
+            fr = make_frames_shape("small", seed=3)
+            run = GraphRun(0)
+            run.ctx.set_points(fr.scene_points.astype(np.float32))
+            sh = FrameShardedScene(run, fr.num_points, fr.num_frames)
+            lo, hi = sh.lo, sh.hi
+            dev = torch.device("cuda", 0)
+            t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+            sh.backproject(t(fr.depth[lo:hi], torch.float32), t(fr.seg[lo:hi], torch.uint8),
+                           t(fr.intrinsics[lo:hi], torch.float64), t(fr.poses[lo:hi].reshape(-1, 16), torch.float64))
+            sh.step(0.3, 0.3, 0.9, 0.8)
+            np.savez(out, **{k: np.asarray(v) for k, v in run.canonical().items()})
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
