@@ -96,6 +96,8 @@ struct mc_ctx {
     DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
         d_blist, d_ncnt, d_par, d_droot, d_rnk, d_lab, d_ccnt, d_ssidx, d_avg, d_qpts;
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
+    DevBuf d_cls_list, d_nbl;  // denoise size-class slot lists; per-workgroup eps-neighbour lists
+    int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
     int bp_bm_blocks = 0;
@@ -173,6 +175,8 @@ int mc_ctx_create(int device, mc_ctx **out)
     mc_ctx *ctx = new mc_ctx();
     ctx->device = device;
     int rc = guarded(ctx, [&] {
+        MC_HIP(hipSetDevice(ctx->device));
+        MC_HIP(hipDeviceGetAttribute(&ctx->num_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
         MC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ctx->own_stream = true;
         MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
@@ -222,7 +226,8 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_bstart, &ctx->d_blist, &ctx->d_ncnt, &ctx->d_par, &ctx->d_droot, &ctx->d_rnk,
                          &ctx->d_lab, &ctx->d_ccnt, &ctx->d_ssidx, &ctx->d_avg, &ctx->d_qpts, &ctx->d_bpbm, &ctx->d_tmp,
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
-                         &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts};
+                         &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
+                         &ctx->d_cls_list, &ctx->d_nbl};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1179,13 +1184,20 @@ void grow_keep(DevBuf &b, size_t bytes, size_t used, hipStream_t s)
     b.swap(nb);  // the old buffer is freed with nb
 }
 
-enum BpStat : int { BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ, BS_COUNT };
+enum BpStat : int {
+    BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
+    BS_CLS,             // 4 denoise size-class counts
+    BS_TK = BS_CLS + 4,  // 3 ticket counters of the LDS denoise classes
+    BS_COUNT = BS_TK + 3
+};
+
+size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
 void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
 {
     const size_t px = static_cast<size_t>(fb) * H * W + 1;
-    const size_t slots = static_cast<size_t>(fb) * 256 + 1;
+    const size_t slots = slots_cap(fb);
     ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * 256 * 4);
     ctx->d_present.reserve(static_cast<size_t>(fb) * 8 * 4);
     ctx->d_fflags.reserve(static_cast<size_t>(fb) * 4);
@@ -1202,6 +1214,8 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_midx.reserve((slots + 1) * 4);
     ctx->d_moff.reserve((slots + 1) * 4);
     ctx->d_slot_box.reserve(slots * 6 * 4);
+    ctx->d_cls_list.reserve(4 * slots * 4);
+    ctx->d_nbl.reserve(static_cast<size_t>(ctx->num_cu) * 2048 * mc::kBpNbCap * 2);  // every class: N x WGs/CU = 2048
     if (ctx->bp_px_cap < px) {
         ctx->d_pix_list.reserve(px * 4);
         ctx->d_hkey.reserve(2 * px * 8);
@@ -1263,7 +1277,20 @@ void bp_build_grid(mc_ctx *ctx, float radius, hipStream_t s)
 }
 
 constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
-const int kBpStatInit[BS_COUNT] = {INT_MAX, 0, 0, 0, 0, 0, 0, 0};
+
+// one LDS size class of the denoise: as many workgroups as are resident at once, each taking the
+// class's slots from a ticket counter
+template <int N>
+void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, const mc::BpDev &dv)
+{
+    using C = mc::BpLdsClass<N>;
+    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu), dim3(C::T), 0, s, st + BS_CLS + cls,
+                       ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
+                       ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                       ctx->d_nbl.as<unsigned short>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
+                       ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
+}
+const int kBpStatInit[BS_COUNT] = {INT_MAX};  // the rest zero
 
 }  // namespace
 
@@ -1422,18 +1449,26 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_denoise");
-                hipLaunchKernelGGL(mc::k_bp_denoise_lds, dim3(kBpGrid), dim3(mc::kBpLdsT), 0, s, st + BS_NS,
-                                   ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
-                                   ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
-                                   ctx->d_slot_box.as<float>());
-                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
-                                   ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                const int ncap = static_cast<int>(slots_cap(fb));
+                hipLaunchKernelGGL(mc::k_bp_classify, dim3(64), dim3(256), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
+                                   ncap, st + BS_CLS, ctx->d_cls_list.as<int>());
+                // the few slots beyond the LDS classes run on the side stream, beside the classes
+                MC_HIP(hipEventRecord(ctx->ev_fork, s));
+                MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + 3,
+                                   ctx->d_cls_list.as<int>() + 3 * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                                    ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
                                    ctx->d_bstart.as<int>(), ctx->d_blist.as<int>(), ctx->d_ncnt.as<int>(),
                                    ctx->d_par.as<int>(), ctx->d_droot.as<int>(), ctx->d_rnk.as<int>(),
                                    ctx->d_lab.as<int>(), ctx->d_ccnt.as<int>(), ctx->d_ssidx.as<int>(),
                                    ctx->d_avg.as<double>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
                                    ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
+                MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+                bp_denoise_class<2048>(ctx, s, 2, ncap, st, dv);
+                bp_denoise_class<1024>(ctx, s, 1, ncap, st, dv);
+                bp_denoise_class<512>(ctx, s, 0, ncap, st, dv);
+                MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_query");

@@ -530,15 +530,6 @@ __device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
     a[0] = (v < a[0]) ? v : a[0];
 }
 
-template <int N, typename V>
-__device__ __forceinline__ V select_at(const V (&a)[N], int i)
-{
-    V r = a[0];
-#pragma unroll
-    for (int q = 1; q < N; q++) r = (q == i) ? a[q] : r;
-    return r;
-}
-
 // union-find over a workgroup's LDS parent array (root = smallest index)
 constexpr int kBpLdsUF = 8192;
 __device__ __forceinline__ int uf_find_s(volatile int *par, int x)
@@ -615,7 +606,10 @@ __device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restric
         for (int q = 0; q < N; q++) best[q] = DBL_MAX;
         int found = 0;
         bool done = false;
-        for (int R = 0; R <= kRingMax && !done; R++) {
+        // the ring search serves the full-k case only (kk == N: k-th smallest = best[N-1], a static
+        // index; a dynamic one would mirror best[] into scratch on every insert); m < N goes to the
+        // whole-wave path, which takes any kk
+        for (int R = 0; R <= kRingMax && !done && kk == N; R++) {
             for (int dz = -R; dz <= R; dz++)
                 for (int dy = -R; dy <= R; dy++) {
                     const bool edge = dz == -R || dz == R || dy == -R || dy == R;
@@ -635,7 +629,7 @@ __device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restric
                     }
                 }
             const double reach = static_cast<double>(R) * ce;
-            done = found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9);
+            done = found >= kk && best[N - 1] < reach * reach * (1.0 - 1e-9);
         }
         if (!done) {  // sparse point: every kept point, by a whole wave below
             const int f = atomicAdd(nfb, 1);
@@ -680,18 +674,40 @@ __device__ unsigned long long g_bp_stamps[32];
 #define BP_STAMP(k) do { } while (0)
 #endif
 
-// ---------------------------------------------------------------------------------------------
-// (a4) denoise, LDS-resident variant for slots of <= kBpLdsN voxels (the bulk): the same steps as
-// k_bp_denoise below, with the points cell-sorted into LDS (SoA) so that every neighbourhood scan
-// reads LDS.  Union-find runs over sorted positions; each component is keyed by its smallest
-// original index, which numbers the clusters exactly as k_bp_denoise / Open3D do.
-// ---------------------------------------------------------------------------------------------
-#ifndef MC_ABLATE_BP
-#define MC_ABLATE_BP 0  // timing-only builds: 1 = no kNN, 2 = no DBSCAN union (results wrong)
-#endif
+// acc + v(lane 0) + v(lane 1) + ... + v(lane 63), in lane order, skipping lanes with v <= 0 (a
+// std::accumulate step over 64 values); the lane values are read as scalars
+__device__ __forceinline__ double seq_add64_pos(double acc, double v)
+{
+    const long long bits = __double_as_longlong(v);
+    const int lo = static_cast<int>(bits), hi = static_cast<int>(bits >> 32);
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const unsigned long long b = (static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readlane(hi, j))) << 32) |
+                                     static_cast<unsigned>(__builtin_amdgcn_readlane(lo, j));
+        const double a = __longlong_as_double(static_cast<long long>(b));
+        if (a > 0) acc = acc + a;
+    }
+    return acc;
+}
+
+// Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
+// the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
 constexpr int kBpLdsN = 2048;
-constexpr int kBpLdsT = 512;
-constexpr int kBpFbCount = 2 * kBpLdsN + 1;  // index of the fallback counter in sB
+constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
+template <int N>
+struct BpLdsClass;
+template <>
+struct BpLdsClass<512> {
+    static constexpr int T = 256, kWgPerCu = 4;
+};
+template <>
+struct BpLdsClass<1024> {
+    static constexpr int T = 512, kWgPerCu = 2;
+};
+template <>
+struct BpLdsClass<2048> {
+    static constexpr int T = 512, kWgPerCu = 1;
+};
 
 template <int NW>
 __device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], double *red)
@@ -727,9 +743,10 @@ struct BpLdsGrid {
 };
 
 constexpr unsigned long long kKeptBit = 1ull << 63;
+constexpr int kLdsCellUnroll = 2;  // records in flight per cell scan (VGPR budget: 128 at 4 waves/SIMD)
 
 // fn(q, d2) for every sorted position q of cell (x, y, z) whose key (with `with` bits set) matches;
-// d2 = squared distance from a (u3 order).  Records are read four at a time so their LDS loads overlap.
+// d2 = squared distance from a (u3 order).  Records are read kLdsCellUnroll at a time so their LDS loads overlap.
 template <typename Fn>
 __device__ __forceinline__ void lds_cell(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
                                          double ay, double az, Fn &&fn)
@@ -740,12 +757,12 @@ __device__ __forceinline__ void lds_cell(const BpLdsGrid &g, int x, int y, int z
     const unsigned b = mod_mul(bp_hash3(x, y, z), g.nb);
     const int e = g.bs[b + 1];
     int q = g.bs[b];
-    for (; q + 4 <= e; q += 4) {
-        double4 p[4];
+    for (; q + kLdsCellUnroll <= e; q += kLdsCellUnroll) {
+        double4 p[kLdsCellUnroll];
 #pragma unroll
-        for (int u = 0; u < 4; u++) p[u] = g.pt[q + u];
+        for (int u = 0; u < kLdsCellUnroll; u++) p[u] = g.pt[q + u];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kLdsCellUnroll; u++) {
             if ((static_cast<unsigned long long>(__double_as_longlong(p[u].w)) & mask) != key) continue;
             const double dx = ax - p[u].x, dy = ay - p[u].y, dz = az - p[u].z;
             fn(q + u, ((dx * dx) + (dy * dy)) + (dz * dz));
@@ -769,6 +786,22 @@ __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, in
             for (int dx = -1; dx <= 1; dx++) lds_cell(g, x + dx, y + dy, z + dz, with, ax, ay, az, fn);
 }
 
+// fn(q2) for the first cnt entries of a point's eps-neighbour list (column-major, stride N), read
+// B at a time so that the global loads are in flight together
+template <int N, int B = 8, typename Fn>
+__device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nb, int cnt, Fn &&fn)
+{
+    int k = 0;
+    for (; k + B <= cnt; k += B) {
+        unsigned short v[B];
+#pragma unroll
+        for (int u = 0; u < B; u++) v[u] = nb[(k + u) * N];
+#pragma unroll
+        for (int u = 0; u < B; u++) fn(static_cast<int>(v[u]));
+    }
+    for (; k < cnt; k++) fn(static_cast<int>(nb[k * N]));
+}
+
 __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, int &z)
 {
     x = static_cast<int>((k >> 42) & 0x1FFFFF);
@@ -776,41 +809,88 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
     z = static_cast<int>(k & 0x1FFFFF);
 }
 
-__global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
-    const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
-    const double *__restrict__ vpts, float *__restrict__ qpts, int *__restrict__ slot_m, int *__restrict__ slot_ns,
+// Slots of each LDS size class (unordered: every slot is processed independently); class 3 =
+// more than kBpLdsN voxels.  cls_cnt[4] must be zero.
+__global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
+                                                     int cap, int *__restrict__ cls_cnt, int *__restrict__ cls_list)
+{
+    const int NS = *dNS;
+    for (int s = blockIdx.x * 256 + threadIdx.x; s - static_cast<int>(threadIdx.x) < NS; s += gridDim.x * 256) {
+        const bool live = s < NS;
+        const int n = live ? slot_nv[s] : 0;
+        const int c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= kBpLdsN ? 2 : 3;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long b = __ballot(live && c == k);
+            if (!b) continue;
+            const int leader = __ffsll(static_cast<long long>(b)) - 1;
+            int base = 0;
+            if (lane_id() == leader) base = atomicAdd(&cls_cnt[k], __popcll(b));
+            base = __shfl(base, leader, 64);
+            if (live && c == k) cls_list[k * cap + base + __popcll(b & ((1ull << lane_id()) - 1))] = s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// (a4) denoise, LDS-resident variant for slots of <= N voxels (the bulk): the same steps as
+// k_bp_denoise below, with the points cell-sorted into LDS so that every neighbourhood scan reads
+// LDS.  Union-find runs over sorted positions; each component is keyed by its smallest original
+// index, which numbers the clusters exactly as k_bp_denoise / Open3D do.  The eps-neighbour scan
+// records every point's neighbour positions (<= kBpNbCap, in a per-workgroup global list), so the
+// union, border-label and k-NN steps visit those instead of walking 27 hashed cells: the 20 nearest
+// kept points of a point with >= 20 kept eps-neighbours are among them (every other point is at
+// distance >= eps).  Workgroups take slots of their size class from a ticket counter.
+// ---------------------------------------------------------------------------------------------
+#ifndef MC_ABLATE_BP
+#define MC_ABLATE_BP 0  // timing-only builds: 1 = no kNN, 2 = no DBSCAN union (results wrong)
+#endif
+
+template <int N>
+__global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsClass<N>::T / 256) void k_bp_denoise_lds(
+    const int *__restrict__ cls_cnt, const int *__restrict__ cls_list, int *__restrict__ ticket,
+    const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
+    unsigned short *__restrict__ nbl, float *__restrict__ qpts, int *__restrict__ slot_m, int *__restrict__ slot_ns,
     float *__restrict__ slot_box)
 {
-    constexpr int NW = kBpLdsT / 64;
-    __shared__ double4 spt[kBpLdsN];                            // cell-sorted points + cell keys
-    __shared__ int sA[2 * kBpLdsN + 1];                         // bucket starts
-    __shared__ int sB[2 * kBpLdsN + 2];                         // bucket counts; then min original
-                                                                // index per root [0, n) + class counts [kBpLdsN, ..)
-    __shared__ short sorig[kBpLdsN], spos[kBpLdsN];             // sorted position <-> original index
-    __shared__ int sflag[kBpLdsN];                              // neighbour count | kept bit 30
-    __shared__ int spar[kBpLdsN];                               // union-find over positions, then roots
-    __shared__ int sX[kBpLdsN];                                 // bucket per point; rank per root; S list
-    __shared__ double savg[kBpLdsN];                            // labels (int view); then mean distances
+    constexpr int T = BpLdsClass<N>::T;
+    constexpr int NW = T / 64;
+    constexpr int kFbCount = 2 * N + 1;  // index of the fallback counter in sB
+    __shared__ double4 spt[N];           // cell-sorted points + cell keys
+    __shared__ int sA[2 * N + 1];        // bucket starts
+    __shared__ int sB[2 * N + 2];        // bucket counts; then min original index per root [0, n) +
+                                         // class counts [N, ..); then the k-NN fallback list
+    __shared__ short sorig[N], spos[N];  // sorted position <-> original index
+    __shared__ int sflag[N];             // eps-neighbour count | kept bit 30
+    __shared__ int spar[N];              // union-find over positions, then roots, then kept ranks
+    __shared__ int sX[N];                // bucket per point; rank per root; S list
+    __shared__ double savg[N];           // labels (int view); then mean distances
     __shared__ double red[6 * NW];
     __shared__ float fred[6 * NW];
     __shared__ int ws[NW];
     __shared__ double s_thr;
+    __shared__ int s_slot;
     int *slab = reinterpret_cast<int *>(savg);
-    int *ccnt = sB + kBpLdsN;
+    int *ccnt = sB + N;
     int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
-    const int NS = *dNS;
+    const int cnt_cls = *cls_cnt;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    unsigned short *nbw = nbl + static_cast<size_t>(blockIdx.x) * N * kBpNbCap;
 #ifdef MC_BP_STAMPS
     unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
 #endif
-    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+    while (true) {
+        if (t == 0) s_slot = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int tk = s_slot;
+        if (tk >= cnt_cls) break;
+        const int s = cls_list[tk];
         const int base = slot_pix[s], n = slot_nv[s];
-        if (n > kBpLdsN) continue;  // k_bp_denoise (uniform)
         BP_STAMP(16);
         const double *P = vpts + 3 * static_cast<size_t>(base);
         // 1. bounding box -> grid origin and cell range
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        for (int i = t; i < n; i += kBpLdsT)
+        for (int i = t; i < n; i += T)
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 mn[c] = fmin(mn[c], P[3 * i + c]);
@@ -825,9 +905,9 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
         BP_STAMP(17);
         // 2. bucket counts
-        for (int b = t; b < 2 * n; b += kBpLdsT) sB[b] = 0;
+        for (int b = t; b < 2 * n; b += T) sB[b] = 0;
         __syncthreads();
-        for (int i = t; i < n; i += kBpLdsT) {
+        for (int i = t; i < n; i += T) {
             int c3[3];
 #pragma unroll
             for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
@@ -840,11 +920,11 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         // 3. bucket starts
         {
             int carry = 0;
-            for (int b0 = 0; b0 < 2 * n; b0 += kBpLdsT) {
+            for (int b0 = 0; b0 < 2 * n; b0 += T) {
                 const int b = b0 + t;
                 const int v = b < 2 * n ? sB[b] : 0;
                 int tot;
-                const int ex = block_excl_scan<kBpLdsT>(v, ws, tot);
+                const int ex = block_excl_scan<T>(v, ws, tot);
                 if (b < 2 * n) sA[b] = carry + ex;
                 carry += tot;
             }
@@ -853,7 +933,7 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         __syncthreads();
         BP_STAMP(19);
         // 4. counting-sort scatter into LDS (bucket counters return to zero)
-        for (int i = t; i < n; i += kBpLdsT) {
+        for (int i = t; i < n; i += T) {
             const int b = sX[i];
             const int q = sA[b] + atomicSub(&sB[b], 1) - 1;
             const double x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
@@ -867,59 +947,73 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         __syncthreads();
         auto keyof = [&](int q) { return static_cast<unsigned long long>(__double_as_longlong(spt[q].w)); };
         BP_STAMP(20);
-        // 5. eps-neighbour counts (self included)
-        for (int q = t; q < n; q += kBpLdsT) {
+        // 5. eps-neighbour counts (self included) and lists
+        for (int q = t; q < n; q += T) {
             int x, y, z;
             unpack3(keyof(q), x, y, z);
             const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            unsigned short *my = nbw + q;
             int cnt = 0;
-            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) { cnt += d2 < pr.eps2 ? 1 : 0; });
+            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                if (d2 < pr.eps2) {
+                    if (cnt < kBpNbCap) my[cnt * N] = static_cast<unsigned short>(q2);
+                    cnt++;
+                }
+            });
             sflag[q] = cnt;
             spar[q] = q;
         }
         __syncthreads();
         BP_STAMP(21);
         // 6. connected core points
-        for (int q = t; q < n; q += kBpLdsT) {
-            if (MC_ABLATE_BP == 2 || sflag[q] < pr.minpts) continue;
-            int x, y, z;
-            unpack3(keyof(q), x, y, z);
-            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+        for (int q = t; q < n; q += T) {
+            const int cnt = sflag[q];
+            if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
             int ra = uf_find_s(spar, q);
-            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                if (q2 < q && d2 < pr.eps2 && sflag[q2] >= pr.minpts) {
+            auto join = [&](int q2) {
+                if (q2 < q && sflag[q2] >= pr.minpts) {
                     const int rb = uf_find_s(spar, q2);
                     if (rb != ra) {  // most edges of a dense cluster are already joined
                         uf_unite_s(spar, ra, rb);
                         ra = uf_find_s(spar, ra);
                     }
                 }
-            });
+            };
+            if (cnt <= kBpNbCap) {
+                nb_list<N>(nbw + q, cnt, join);
+            } else {
+                int x, y, z;
+                unpack3(keyof(q), x, y, z);
+                const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+                lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                    if (d2 < pr.eps2) join(q2);
+                });
+            }
         }
         __syncthreads();
         BP_STAMP(22);
         // 7. roots; every component keyed by its smallest original index; clusters ranked by it
         {
-            int rq[kBpLdsN / kBpLdsT];
+            int rq[N / T];
 #pragma unroll
-            for (int k = 0; k < kBpLdsN / kBpLdsT; k++) {
-                const int q = t + k * kBpLdsT;
+            for (int k = 0; k < N / T; k++) {
+                const int q = t + k * T;
                 rq[k] = (q < n && sflag[q] >= pr.minpts) ? uf_find_s(spar, q) : -1;
             }
             __syncthreads();
-            for (int q = t; q < n; q += kBpLdsT) sB[q] = INT_MAX;
-            for (int x = t; x <= n; x += kBpLdsT) ccnt[x] = 0;
+            for (int q = t; q < n; q += T) sB[q] = INT_MAX;
+            for (int x = t; x <= n; x += T) ccnt[x] = 0;
 #pragma unroll
-            for (int k = 0; k < kBpLdsN / kBpLdsT; k++) {
-                const int q = t + k * kBpLdsT;
+            for (int k = 0; k < N / T; k++) {
+                const int q = t + k * T;
                 if (q < n) spar[q] = rq[k];
             }
             __syncthreads();
-            for (int q = t; q < n; q += kBpLdsT)
+            for (int q = t; q < n; q += T)
                 if (spar[q] >= 0) atomicMin(&sB[spar[q]], static_cast<int>(sorig[q]));
             __syncthreads();
             int carry = 0;
-            for (int i0 = 0; i0 < n; i0 += kBpLdsT) {
+            for (int i0 = 0; i0 < n; i0 += T) {
                 const int i = i0 + t;
                 int isr = 0, r = -1;
                 if (i < n) {
@@ -927,31 +1021,38 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
                     isr = (r >= 0 && sB[r] == i) ? 1 : 0;
                 }
                 int tot;
-                const int ex = block_excl_scan<kBpLdsT>(isr, ws, tot);
+                const int ex = block_excl_scan<T>(isr, ws, tot);
                 if (isr) sX[r] = carry + ex;  // rank stored at the root position
                 carry += tot;
             }
         }
         __syncthreads();
         BP_STAMP(23);
-        // 8. labels and class counts
-        for (int q = t; q < n; q += kBpLdsT) {
+        // 8. labels and class counts (a border point joins the adjacent cluster of smallest key)
+        for (int q = t; q < n; q += T) {
             int l;
             if (spar[q] >= 0) {
                 l = sX[spar[q]];
             } else {
-                int x, y, z;
-                unpack3(keyof(q), x, y, z);
-                const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+                const int cnt = sflag[q];
                 int best = INT_MAX, broot = -1;
-                lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                    if (!(d2 < pr.eps2)) return;
+                auto near = [&](int q2) {
                     const int r2 = spar[q2];
                     if (r2 >= 0 && sB[r2] < best) {
                         best = sB[r2];
                         broot = r2;
                     }
-                });
+                };
+                if (cnt <= kBpNbCap) {
+                    nb_list<N>(nbw + q, cnt, near);
+                } else {
+                    int x, y, z;
+                    unpack3(keyof(q), x, y, z);
+                    const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+                    lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                        if (d2 < pr.eps2) near(q2);
+                    });
+                }
                 l = broot >= 0 ? sX[broot] : -1;
             }
             slab[q] = l;
@@ -959,100 +1060,146 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         }
         __syncthreads();
         BP_STAMP(24);
-        // 9. class filter; S in original index order
+        // 9. class filter; S in original index order; kept rank per sorted position
         const double lim = pr.frac * static_cast<double>(n);
-        for (int q = t; q < n; q += kBpLdsT)
+        for (int q = t; q < n; q += T)
             if (!(static_cast<double>(ccnt[slab[q] + 1]) < lim)) {
                 sflag[q] |= 1 << 30;
                 spt[q].w = __longlong_as_double(static_cast<long long>(keyof(q) | kKeptBit));
             }
         __syncthreads();
         int m = 0;
-        for (int i0 = 0; i0 < n; i0 += kBpLdsT) {
+        for (int i0 = 0; i0 < n; i0 += T) {
             const int i = i0 + t;
             const int keep = (i < n && (sflag[spos[i]] & (1 << 30))) ? 1 : 0;
             int tot;
-            const int ex = block_excl_scan<kBpLdsT>(keep, ws, tot);
-            if (keep) sX[m + ex] = i;
+            const int ex = block_excl_scan<T>(keep, ws, tot);
+            if (keep) {
+                sX[m + ex] = i;
+                spar[spos[i]] = m + ex;
+            }
             m += tot;
         }
         __syncthreads();
         BP_STAMP(25);
-        // 10. k nearest kept points (grid rings up to R = 2, then all of S)
+        // 10. k nearest kept points: the eps list when it holds >= k kept points, else grid rings up
+        //     to R = 2, else (sparse point, or m < k) all of S by a whole wave
         const int kk = min(pr.knn, m);
-        if (t == 0) sfb[kBpFbCount] = 0;
+        if (t == 0) sfb[kFbCount] = 0;
         __syncthreads();
-        for (int r = t; r < m; r += kBpLdsT) {
+        for (int q = t; q < n; q += T) {
+            const int fl = sflag[q];
+            if (!(fl & (1 << 30))) continue;
+            const int r = spar[q];
 #if MC_ABLATE_BP == 1
             savg[r] = 1.0;
             continue;
 #endif
-            const int q = spos[sX[r]];
-            int x, y, z;
-            unpack3(keyof(q), x, y, z);
-            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            const double4 a = spt[q];
             double best[kBpKnnMax];
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
             int found = 0;
             bool done = false;
-            int visited = 0;
-            auto take = [&](int, double d2) {
-                sorted_insert(best, d2);
-                found++;
-            };
-            for (int R = 0; R <= 2 && !done; R++) {
-                for (int dz = -R; dz <= R; dz++)
-                    for (int dy = -R; dy <= R; dy++) {
-                        const bool edge = dz == -R || dz == R || dy == -R || dy == R;
-                        const int step = (edge || R == 0) ? 1 : 2 * R;
-                        for (int dx = -R; dx <= R; dx += step) lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, ax, ay, az, take);
-                    }
-                const double reach = static_cast<double>(R) * pr.ce;
-                done = found >= kk && select_at(best, kk - 1) < reach * reach * (1.0 - 1e-9);
-                visited++;
+            const int cnt = fl & ((1 << 30) - 1);
+            if (kk == kBpKnnMax && cnt <= kBpNbCap) {
+                nb_list<N, 4>(nbw + q, cnt, [&](int q2) {
+                    const double4 p = spt[q2];
+                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+                    found++;
+                });
+                done = found >= kk;
+            }
+            if (!done && kk == kBpKnnMax) {
+#pragma unroll
+                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+                found = 0;
+                int x, y, z;
+                unpack3(keyof(q), x, y, z);
+                auto take = [&](int, double d2) {
+                    sorted_insert(best, d2);
+                    found++;
+                };
+                for (int R = 0; R <= 2 && !done; R++) {
+                    for (int dz = -R; dz <= R; dz++)
+                        for (int dy = -R; dy <= R; dy++) {
+                            const bool edge = dz == -R || dz == R || dy == -R || dy == R;
+                            const int step = (edge || R == 0) ? 1 : 2 * R;
+                            for (int dx = -R; dx <= R; dx += step)
+                                lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
+                        }
+                    const double reach = static_cast<double>(R) * pr.ce;
+                    done = found >= kk && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
+                }
             }
 #ifdef MC_BP_STAMPS
             atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
-            atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(visited));
             if (!done) atomicAdd(&g_bp_stamps[31], 1ull);
             atomicAdd(&g_bp_stamps[13], 1ull);
 #endif
-            if (!done) {  // sparse point: every kept point, by a whole wave below
-                sfb[atomicAdd(&sfb[kBpFbCount], 1)] = r;
+            if (!done) {  // whole-wave path below
+                sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
                 continue;
             }
             double sum = 0.0;
 #pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++)
-                if (k < kk) sum = sum + sqrt(best[k]);
+            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
             savg[r] = sum / static_cast<double>(kk);
         }
         __syncthreads();
-        for (int f = wv; f < sfb[kBpFbCount]; f += NW) {
-            const int r = sfb[f];
-            const double4 a = spt[spos[sX[r]]];
-            const double mean = wave_knn_mean(m, kk, [&](int j) {
-                const double4 p = spt[spos[sX[j]]];
-                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                return ((ex * ex) + (ey * ey)) + (ez * ez);
-            });
-            if (lane == 0) savg[r] = mean;
+        const int nfb = sfb[kFbCount];
+        if (nfb > 2 * NW && kk == kBpKnnMax) {
+            // many sparse points: one per lane, every kept point scanned in sorted order (the same
+            // position for all lanes at once: LDS broadcast reads)
+            for (int f0 = 0; f0 < nfb; f0 += T) {
+                const int f = f0 + t;
+                const int r = f < nfb ? sfb[f] : -1;
+                const double4 a = spt[r >= 0 ? spos[sX[r]] : 0];
+                double best[kBpKnnMax];
+#pragma unroll
+                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+                for (int q2 = 0; q2 < n; q2++) {
+                    const double4 p = spt[q2];
+                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+                }
+                double sum = 0.0;
+#pragma unroll
+                for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
+                if (r >= 0) savg[r] = sum / static_cast<double>(kk);
+            }
+        } else {
+            for (int f = wv; f < nfb; f += NW) {
+                const int r = sfb[f];
+                const double4 a = spt[spos[sX[r]]];
+                const double mean = wave_knn_mean(m, kk, [&](int j) {
+                    const double4 p = spt[spos[sX[j]]];
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    return ((ex * ex) + (ey * ey)) + (ez * ez);
+                });
+                if (lane == 0) savg[r] = mean;
+            }
         }
         __syncthreads();
         BP_STAMP(26);
-        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate)
-        if (t == 0) {
+        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate), by wave 0:
+        //     64 values per step are read at once, then added in order (lane reads are scalar)
+        if (wv == 0) {
             double mean = 0.0, sq = 0.0;
-            for (int r = 0; r < m; r++)
-                if (savg[r] > 0) mean = mean + savg[r];
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;  // 0 adds nothing below
+                mean = seq_add64_pos(mean, v);
+            }
             mean = mean / static_cast<double>(m);
-            for (int r = 0; r < m; r++) {
-                const double a = savg[r];
-                sq = sq + (a > 0 ? (a - mean) * (a - mean) : 0.0);
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;
+                sq = seq_add64_pos(sq, v > 0 ? (v - mean) * (v - mean) : 0.0);
             }
             const double sd = sqrt(sq / static_cast<double>(m - 1));
-            s_thr = mean + pr.std_ratio * sd;
+            if (lane == 0) s_thr = mean + pr.std_ratio * sd;
         }
         __syncthreads();
         const double thr = s_thr;
@@ -1060,11 +1207,11 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
         // 12. survivors -> float32 mask points and their AABB
         int ns = 0;
         float flo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, fhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (int r0 = 0; r0 < m; r0 += kBpLdsT) {
+        for (int r0 = 0; r0 < m; r0 += T) {
             const int r = r0 + t;
             const int keep = (r < m && savg[r] > 0 && savg[r] < thr) ? 1 : 0;
             int tot;
-            const int ex = block_excl_scan<kBpLdsT>(keep, ws, tot);
+            const int ex = block_excl_scan<T>(keep, ws, tot);
             if (keep) {
                 const int i = sX[r];
                 float *qo = qpts + 3 * (static_cast<size_t>(base) + ns + ex);
@@ -1111,7 +1258,7 @@ __global__ __launch_bounds__(kBpLdsT) void k_bp_denoise_lds(
 }
 
 __global__ __launch_bounds__(256) void k_bp_denoise(
-    const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
+    const int *__restrict__ cls_cnt, const int *__restrict__ cls_list, const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr,
     const double *__restrict__ vpts, unsigned long long *__restrict__ pcell, int *__restrict__ pbkt,
     int *__restrict__ bcnt, int *__restrict__ bstart, int *__restrict__ blist, int *__restrict__ ncnt,
     int *__restrict__ par, int *__restrict__ root, int *__restrict__ rnk, int *__restrict__ lab,
@@ -1125,15 +1272,15 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
     __shared__ double s_thr;
     __shared__ float fred[24];
     __shared__ int ws[4];
-    const int NS = *dNS;
+    const int NL = *cls_cnt;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
 #ifdef MC_BP_STAMPS
     unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
 #endif
-    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+    for (int k = blockIdx.x; k < NL; k += gridDim.x) {  // the slots of more than kBpLdsN voxels
         BP_STAMP(0);
+        const int s = cls_list[k];
         const int base = slot_pix[s], n = slot_nv[s];
-        if (n <= kBpLdsN) continue;  // k_bp_denoise_lds (uniform)
         const double *P = vpts + 3 * static_cast<size_t>(base);
         unsigned long long *pc = pcell + base;
         int *pb = pbkt + base, *bc = bcnt + 2 * static_cast<size_t>(base), *bs = bstart + 2 * static_cast<size_t>(base) + s;
