@@ -96,7 +96,7 @@ struct mc_ctx {
     DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
         d_blist, d_ncnt, d_par, d_droot, d_rnk, d_lab, d_ccnt, d_ssidx, d_avg, d_qpts;
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
-    DevBuf d_cls_list, d_nbl;  // denoise size-class slot lists; per-workgroup eps-neighbour lists
+    DevBuf d_cls_list, d_nbl, d_lean;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
@@ -227,7 +227,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_lab, &ctx->d_ccnt, &ctx->d_ssidx, &ctx->d_avg, &ctx->d_qpts, &ctx->d_bpbm, &ctx->d_tmp,
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
-                         &ctx->d_cls_list, &ctx->d_nbl};
+                         &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1186,9 +1186,9 @@ void grow_keep(DevBuf &b, size_t bytes, size_t used, hipStream_t s)
 
 enum BpStat : int {
     BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
-    BS_CLS,             // 4 denoise size-class counts
-    BS_TK = BS_CLS + 4,  // 3 ticket counters of the LDS denoise classes
-    BS_COUNT = BS_TK + 3
+    BS_CLS,             // 5 denoise size-class counts (4 LDS classes + the global-memory kernel)
+    BS_TK = BS_CLS + 5,  // ticket counters of the LDS classes
+    BS_COUNT = BS_TK + 4
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
@@ -1214,8 +1214,10 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_midx.reserve((slots + 1) * 4);
     ctx->d_moff.reserve((slots + 1) * 4);
     ctx->d_slot_box.reserve(slots * 6 * 4);
-    ctx->d_cls_list.reserve(4 * slots * 4);
-    ctx->d_nbl.reserve(static_cast<size_t>(ctx->num_cu) * 2048 * mc::kBpNbCap * 2);  // every class: N x WGs/CU = 2048
+    ctx->d_cls_list.reserve(5 * slots * 4);
+    // per-workgroup eps-neighbour lists: N x WGs per CU is 2048 for the 512/1024/2048 classes, 3072 for the lean one
+    ctx->d_nbl.reserve(static_cast<size_t>(ctx->num_cu) * 3072 * mc::kBpNbCap * 2);
+    ctx->d_lean.reserve(static_cast<size_t>(ctx->num_cu) * mc::kBpLeanInts<3072> * 4);
     if (ctx->bp_px_cap < px) {
         ctx->d_pix_list.reserve(px * 4);
         ctx->d_hkey.reserve(2 * px * 8);
@@ -1287,7 +1289,7 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
     hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
-                       ctx->d_nbl.as<unsigned short>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
+                       ctx->d_nbl.as<unsigned short>(), ctx->d_lean.as<int>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
                        ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
 }
 const int kBpStatInit[BS_COUNT] = {INT_MAX};  // the rest zero
@@ -1378,6 +1380,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             Kp = ctx->d_in_intr.as<double>();
             Tp = ctx->d_in_pose.as<double>();
         }
+        // test knob: smallest denoise size class (0 = by size; 3 = the lean LDS class, 4 = the
+        // global-memory kernel for every slot)
+        int min_cls = 0;
+        if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(4, std::max(0, atoi(e)));
         // frames per batch: bounded pixel capacity of the per-slot arrays
         size_t budget = static_cast<size_t>(48) << 20;
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
@@ -1451,12 +1457,12 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 TimedScope ts(ctx->timer, s, "bp_denoise");
                 const int ncap = static_cast<int>(slots_cap(fb));
                 hipLaunchKernelGGL(mc::k_bp_classify, dim3(64), dim3(256), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
-                                   ncap, st + BS_CLS, ctx->d_cls_list.as<int>());
+                                   ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>());
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
                 MC_HIP(hipEventRecord(ctx->ev_fork, s));
                 MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + 3,
-                                   ctx->d_cls_list.as<int>() + 3 * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + 4,
+                                   ctx->d_cls_list.as<int>() + 4 * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                                    ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
                                    ctx->d_bstart.as<int>(), ctx->d_blist.as<int>(), ctx->d_ncnt.as<int>(),
                                    ctx->d_par.as<int>(), ctx->d_droot.as<int>(), ctx->d_rnk.as<int>(),
@@ -1464,6 +1470,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_avg.as<double>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
                                    ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
                 MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+                bp_denoise_class<3072>(ctx, s, 3, ncap, st, dv);
                 bp_denoise_class<2048>(ctx, s, 2, ncap, st, dv);
                 bp_denoise_class<1024>(ctx, s, 1, ncap, st, dv);
                 bp_denoise_class<512>(ctx, s, 0, ncap, st, dv);
@@ -1594,6 +1601,11 @@ int mc_backproject_get_candidates(mc_ctx *ctx, int32_t *stats)
 
 #ifdef MC_BP_STAMPS
 // diagnostic builds only: read (and clear) k_bp_denoise's per-step clock totals
+int mc_debug_bp_slot_times(unsigned *out, int n)
+{
+    n = std::min(n, 1 << 16);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mc::g_bp_slot_time), n * 4) == hipSuccess ? MC_OK : MC_ERR_HIP;
+}
 int mc_debug_bp_stamps(unsigned long long *out32)
 {
     if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 32 * 8) != hipSuccess) return MC_ERR_HIP;

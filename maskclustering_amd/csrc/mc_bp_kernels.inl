@@ -532,14 +532,18 @@ __device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
 
 // union-find over a workgroup's LDS parent array (root = smallest index)
 constexpr int kBpLdsUF = 8192;
-__device__ __forceinline__ int uf_find_s(volatile int *par, int x)
+// (relaxed workgroup-scope atomic loads / stores: other lanes update the array concurrently, and
+// unlike volatile they keep the LDS address space, i.e. ds_read / ds_write instead of flat ops)
+__device__ __forceinline__ int ld_wg(int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void st_wg(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ int uf_find_s(int *par, int x)
 {
     while (true) {
-        const int p = par[x];
+        const int p = ld_wg(par + x);
         if (p == x) return x;
-        const int gp = par[p];
+        const int gp = ld_wg(par + p);
         if (gp == p) return p;
-        par[x] = gp;
+        st_wg(par + x, gp);
         x = gp;
     }
 }
@@ -657,15 +661,16 @@ __device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restric
     }
 }
 
-// Diagnostic build only (-DMC_BP_STAMPS): per-step shader-clock totals of k_bp_denoise, summed
+// Diagnostic build only (-DMC_BP_STAMPS): per-step real-time-clock (100 MHz) totals of k_bp_denoise, summed
 // over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
 #ifdef MC_BP_STAMPS
 __device__ unsigned long long g_bp_stamps[32];
+__device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks), last batch
 #define BP_STAMP(k)                                                                      \
     do {                                                                                 \
         __syncthreads();                                                                 \
         if (threadIdx.x == 0) {                                                          \
-            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                \
+            const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                \
             atomicAdd(&g_bp_stamps[k], now_ - stamp_prev);                               \
             stamp_prev = now_;                                                           \
         }                                                                                \
@@ -692,7 +697,7 @@ __device__ __forceinline__ double seq_add64_pos(double acc, double v)
 
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
-constexpr int kBpLdsN = 2048;
+constexpr int kBpLdsN = 3072;  // largest LDS class
 constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
 template <int N>
 struct BpLdsClass;
@@ -708,6 +713,15 @@ template <>
 struct BpLdsClass<2048> {
     static constexpr int T = 512, kWgPerCu = 1;
 };
+template <>  // lean: one bucket per point; sort/rank/label/statistics arrays in global scratch
+struct BpLdsClass<3072> {
+    static constexpr int T = 512, kWgPerCu = 1;
+};
+template <int N>
+constexpr bool kBpLean = N > 2048;
+// global scratch ints per workgroup of a lean class: savg (2N), sB (2N + 2), sX (N), sorig + spos (N)
+template <int N>
+constexpr size_t kBpLeanInts = kBpLean<N> ? 6 * static_cast<size_t>(N) + 2 : 0;
 
 template <int NW>
 __device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], double *red)
@@ -781,25 +795,45 @@ template <typename Fn>
 __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
                                             double ay, double az, Fn &&fn)
 {
-    for (int dz = -1; dz <= 1; dz++)
-        for (int dy = -1; dy <= 1; dy++)
-            for (int dx = -1; dx <= 1; dx++) lds_cell(g, x + dx, y + dy, z + dz, with, ax, ay, az, fn);
+#pragma unroll 1
+    for (int d = 0; d < 27; d++) {  // rolled: one copy of fn (instruction cache)
+        const int dz = d / 9 - 1, dy = (d / 3) % 3 - 1, dx = d % 3 - 1;
+        lds_cell(g, x + dx, y + dy, z + dz, with, ax, ay, az, fn);
+    }
 }
 
-// fn(q2) for the first cnt entries of a point's eps-neighbour list (column-major, stride N), read
-// B at a time so that the global loads are in flight together
-template <int N, int B = 8, typename Fn>
-__device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nb, int cnt, Fn &&fn)
+// Per-workgroup eps-neighbour lists: entry k of sorted position q is the u16 at
+// uint4 index (k / 8) * N + q, half-word k % 8: a wave's stores of one k fall on 16-byte strided
+// words (few cache lines), and a point's whole list (<= 64 entries) is 8 uint4 loads that are all
+// issued before the first is used.
+template <int N>
+__device__ __forceinline__ void nb_put(unsigned short *__restrict__ nbw, int q, int k, int q2)
 {
-    int k = 0;
-    for (; k + B <= cnt; k += B) {
-        unsigned short v[B];
+    nbw[(static_cast<size_t>(k >> 3) * N + q) * 8 + (k & 7)] = static_cast<unsigned short>(q2);
+}
+
+// fn(q2) for the first cnt (<= kBpNbCap) entries of sorted position q's list: the two halves of
+// 32 entries are loaded before either is processed; the entries are then visited by one rolled
+// loop with a wave-uniform index (register-relative moves), so fn's code appears once: unrolled
+// copies of a 20-step insertion overflow the instruction cache.
+template <int N, typename Fn>
+__device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nbw, int q, int cnt, Fn &&fn)
+{
+    static_assert(kBpNbCap == 64, "eight uint4 per point");
+    const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
+    unsigned w[32];
 #pragma unroll
-        for (int u = 0; u < B; u++) v[u] = nb[(k + u) * N];
-#pragma unroll
-        for (int u = 0; u < B; u++) fn(static_cast<int>(v[u]));
+    for (int u = 0; u < 8; u++) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
+        w[4 * u] = v.x;
+        w[4 * u + 1] = v.y;
+        w[4 * u + 2] = v.z;
+        w[4 * u + 3] = v.w;
     }
-    for (; k < cnt; k++) fn(static_cast<int>(nb[k * N]));
+    // k is the same in every active lane (lanes only leave), so w[k >> 1] is a uniform index
+#pragma unroll 1
+    for (int k = 0; k < cnt; k++) fn(static_cast<int>((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu));
 }
 
 __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, int &z)
@@ -809,18 +843,20 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
     z = static_cast<int>(k & 0x1FFFFF);
 }
 
-// Slots of each LDS size class (unordered: every slot is processed independently); class 3 =
-// more than kBpLdsN voxels.  cls_cnt[4] must be zero.
+// Slots of each size class (unordered: every slot is processed independently); class 4 = more than
+// kBpLdsN voxels (the global-memory kernel).  min_cls > 0 sends small slots to a larger class (tests:
+// every class gives the same results).  cls_cnt[5] must be zero.
 __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
-                                                     int cap, int *__restrict__ cls_cnt, int *__restrict__ cls_list)
+                                                     int cap, int min_cls, int *__restrict__ cls_cnt,
+                                                     int *__restrict__ cls_list)
 {
     const int NS = *dNS;
     for (int s = blockIdx.x * 256 + threadIdx.x; s - static_cast<int>(threadIdx.x) < NS; s += gridDim.x * 256) {
         const bool live = s < NS;
         const int n = live ? slot_nv[s] : 0;
-        const int c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= kBpLdsN ? 2 : 3;
+        const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= kBpLdsN ? 3 : 4);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < 5; k++) {
             const unsigned long long b = __ballot(live && c == k);
             if (!b) continue;
             const int leader = __ffsll(static_cast<long long>(b)) - 1;
@@ -843,33 +879,43 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 // distance >= eps).  Workgroups take slots of their size class from a ticket counter.
 // ---------------------------------------------------------------------------------------------
 #ifndef MC_ABLATE_BP
-#define MC_ABLATE_BP 0  // timing-only builds: 1 = no kNN, 2 = no DBSCAN union (results wrong)
+#define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union,
+                        // 3 = k-NN list pass without the sorted inserts, 4 = k-NN list pass on self only
 #endif
 
 template <int N>
 __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsClass<N>::T / 256) void k_bp_denoise_lds(
     const int *__restrict__ cls_cnt, const int *__restrict__ cls_list, int *__restrict__ ticket,
     const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
-    unsigned short *__restrict__ nbl, float *__restrict__ qpts, int *__restrict__ slot_m, int *__restrict__ slot_ns,
-    float *__restrict__ slot_box)
+    unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, float *__restrict__ qpts, int *__restrict__ slot_m,
+    int *__restrict__ slot_ns, float *__restrict__ slot_box)
 {
     constexpr int T = BpLdsClass<N>::T;
     constexpr int NW = T / 64;
+    constexpr bool kLean = kBpLean<N>;
+    constexpr int NBK = kLean ? 1 : 2;   // hash buckets per point
     constexpr int kFbCount = 2 * N + 1;  // index of the fallback counter in sB
+    constexpr int NL = kLean ? 1 : N;    // extent of the arrays a lean class keeps in global scratch
     __shared__ double4 spt[N];           // cell-sorted points + cell keys
-    __shared__ int sA[2 * N + 1];        // bucket starts
-    __shared__ int sB[2 * N + 2];        // bucket counts; then min original index per root [0, n) +
+    __shared__ int sA[NBK * N + 1];      // bucket starts
+    __shared__ int sB_l[2 * NL + 2];     // bucket counts; then min original index per root [0, n) +
                                          // class counts [N, ..); then the k-NN fallback list
-    __shared__ short sorig[N], spos[N];  // sorted position <-> original index
+    __shared__ short sorig_l[NL], spos_l[NL];  // sorted position <-> original index
     __shared__ int sflag[N];             // eps-neighbour count | kept bit 30
     __shared__ int spar[N];              // union-find over positions, then roots, then kept ranks
-    __shared__ int sX[N];                // bucket per point; rank per root; S list
-    __shared__ double savg[N];           // labels (int view); then mean distances
+    __shared__ int sX_l[NL];             // bucket per point; rank per root; S list
+    __shared__ double savg_l[NL];        // labels (int view); then mean distances
+    int *const gs = lean_scr + static_cast<size_t>(blockIdx.x) * kBpLeanInts<N>;
+    double *const savg = kLean ? reinterpret_cast<double *>(gs) : savg_l;
+    int *const sB = kLean ? gs + 2 * N : sB_l;
+    int *const sX = kLean ? gs + 4 * N + 2 : sX_l;
+    short *const sorig = kLean ? reinterpret_cast<short *>(gs + 5 * N + 2) : sorig_l;
+    short *const spos = kLean ? sorig + N : spos_l;
     __shared__ double red[6 * NW];
     __shared__ float fred[6 * NW];
     __shared__ int ws[NW];
     __shared__ double s_thr;
-    __shared__ int s_slot;
+    __shared__ int s_slot, s_ndef;
     int *slab = reinterpret_cast<int *>(savg);
     int *ccnt = sB + N;
     int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
@@ -877,7 +923,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     unsigned short *nbw = nbl + static_cast<size_t>(blockIdx.x) * N * kBpNbCap;
 #ifdef MC_BP_STAMPS
-    unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+    unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
 #endif
     while (true) {
         if (t == 0) s_slot = atomicAdd(ticket, 1);
@@ -886,6 +932,13 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         if (tk >= cnt_cls) break;
         const int s = cls_list[tk];
         const int base = slot_pix[s], n = slot_nv[s];
+#ifdef MC_BP_STAMPS
+        const unsigned long long slot_t0 = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            atomicAdd(&g_bp_stamps[14], 1ull);
+            atomicAdd(&g_bp_stamps[15], static_cast<unsigned long long>(n));
+        }
+#endif
         BP_STAMP(16);
         const double *P = vpts + 3 * static_cast<size_t>(base);
         // 1. bounding box -> grid origin and cell range
@@ -900,12 +953,12 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         BpLdsGrid g;
         g.pt = spt;
         g.bs = sA;
-        g.nb = 2u * static_cast<unsigned>(n);
+        g.nb = static_cast<unsigned>(NBK * n);
 #pragma unroll
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
         BP_STAMP(17);
         // 2. bucket counts
-        for (int b = t; b < 2 * n; b += T) sB[b] = 0;
+        for (int b = t; b < NBK * n; b += T) sB[b] = 0;
         __syncthreads();
         for (int i = t; i < n; i += T) {
             int c3[3];
@@ -920,15 +973,15 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         // 3. bucket starts
         {
             int carry = 0;
-            for (int b0 = 0; b0 < 2 * n; b0 += T) {
+            for (int b0 = 0; b0 < NBK * n; b0 += T) {
                 const int b = b0 + t;
-                const int v = b < 2 * n ? sB[b] : 0;
+                const int v = b < NBK * n ? sB[b] : 0;
                 int tot;
                 const int ex = block_excl_scan<T>(v, ws, tot);
-                if (b < 2 * n) sA[b] = carry + ex;
+                if (b < NBK * n) sA[b] = carry + ex;
                 carry += tot;
             }
-            if (t == 0) sA[2 * n] = carry;
+            if (t == 0) sA[NBK * n] = carry;
         }
         __syncthreads();
         BP_STAMP(19);
@@ -952,11 +1005,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             int x, y, z;
             unpack3(keyof(q), x, y, z);
             const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-            unsigned short *my = nbw + q;
             int cnt = 0;
             lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
                 if (d2 < pr.eps2) {
-                    if (cnt < kBpNbCap) my[cnt * N] = static_cast<unsigned short>(q2);
+                    if (cnt < kBpNbCap) nb_put<N>(nbw, q, cnt, q2);
                     cnt++;
                 }
             });
@@ -965,12 +1017,19 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         __syncthreads();
         BP_STAMP(21);
-        // 6. connected core points
+        // 6. connected core points: list points first; points with more than kBpNbCap neighbours
+        //    are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
+        if (t == 0) s_ndef = 0;
+        __syncthreads();
         for (int q = t; q < n; q += T) {
             const int cnt = sflag[q];
             if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
+            if (cnt > kBpNbCap) {
+                sX[atomicAdd(&s_ndef, 1)] = q;
+                continue;
+            }
             int ra = uf_find_s(spar, q);
-            auto join = [&](int q2) {
+            nb_list<N>(nbw, q, cnt, [&](int q2) {
                 if (q2 < q && sflag[q2] >= pr.minpts) {
                     const int rb = uf_find_s(spar, q2);
                     if (rb != ra) {  // most edges of a dense cluster are already joined
@@ -978,17 +1037,24 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         ra = uf_find_s(spar, ra);
                     }
                 }
-            };
-            if (cnt <= kBpNbCap) {
-                nb_list<N>(nbw + q, cnt, join);
-            } else {
-                int x, y, z;
-                unpack3(keyof(q), x, y, z);
-                const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-                lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                    if (d2 < pr.eps2) join(q2);
-                });
-            }
+            });
+        }
+        __syncthreads();
+        for (int f = t; f < s_ndef; f += T) {
+            const int q = sX[f];
+            int x, y, z;
+            unpack3(keyof(q), x, y, z);
+            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+            int ra = uf_find_s(spar, q);
+            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
+                if (d2 < pr.eps2 && q2 < q && sflag[q2] >= pr.minpts) {
+                    const int rb = uf_find_s(spar, q2);
+                    if (rb != ra) {
+                        uf_unite_s(spar, ra, rb);
+                        ra = uf_find_s(spar, ra);
+                    }
+                }
+            });
         }
         __syncthreads();
         BP_STAMP(22);
@@ -1044,7 +1110,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     }
                 };
                 if (cnt <= kBpNbCap) {
-                    nb_list<N>(nbw + q, cnt, near);
+                    nb_list<N>(nbw, q, cnt, near);
                 } else {
                     int x, y, z;
                     unpack3(keyof(q), x, y, z);
@@ -1082,11 +1148,22 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         __syncthreads();
         BP_STAMP(25);
-        // 10. k nearest kept points: the eps list when it holds >= k kept points, else grid rings up
-        //     to R = 2, else (sparse point, or m < k) all of S by a whole wave
+        // 10. k nearest kept points: the eps list when it holds >= k kept points; else (deferred to a
+        //     compacted pass, so that few waves walk cells) grid rings up to R = 2; else (sparse
+        //     point, or m < k) all of S, by a whole wave or one lane per point
         const int kk = min(pr.knn, m);
-        if (t == 0) sfb[kFbCount] = 0;
+        int *const sring = sB + N;  // deferred ring-search positions (sB is free after the filter)
+        if (t == 0) {
+            sfb[kFbCount] = 0;
+            s_ndef = 0;
+        }
         __syncthreads();
+        auto put_mean = [&](int r, const double(&best)[kBpKnnMax]) {
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
+            savg[r] = sum / static_cast<double>(kk);
+        };
         for (int q = t; q < n; q += T) {
             const int fl = sflag[q];
             if (!(fl & (1 << 30))) continue;
@@ -1095,58 +1172,76 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             savg[r] = 1.0;
             continue;
 #endif
+            const int cnt = fl & ((1 << 30) - 1);
+            if (kk != kBpKnnMax) {
+                sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
+                continue;
+            }
+            if (cnt > kBpNbCap) {
+                sring[atomicAdd(&s_ndef, 1)] = q;
+                continue;
+            }
+            const double4 a = spt[q];
+            double best[kBpKnnMax];
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+            int found = 0;
+            nb_list<N>(nbw, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](int q2) {
+                const double4 p = spt[q2];
+                if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
+                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                if (MC_ABLATE_BP == 3) best[0] += ((ex * ex) + (ey * ey)) + (ez * ez);
+                else sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+                found++;
+            });
+#if MC_ABLATE_BP == 3 || MC_ABLATE_BP == 4
+            found = kk;
+#endif
+#ifdef MC_BP_STAMPS
+            atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
+            atomicAdd(&g_bp_stamps[13], 1ull);
+#endif
+            if (found < kk) {
+                sring[atomicAdd(&s_ndef, 1)] = q;
+                continue;
+            }
+            put_mean(r, best);
+        }
+        __syncthreads();
+#ifdef MC_BP_STAMPS
+        if (t == 0) atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(s_ndef));
+#endif
+        for (int f = t; f < s_ndef; f += T) {
+            const int q = sring[f];
+            const int r = spar[q];
             const double4 a = spt[q];
             double best[kBpKnnMax];
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
             int found = 0;
             bool done = false;
-            const int cnt = fl & ((1 << 30) - 1);
-            if (kk == kBpKnnMax && cnt <= kBpNbCap) {
-                nb_list<N, 4>(nbw + q, cnt, [&](int q2) {
-                    const double4 p = spt[q2];
-                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
-                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                    sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
-                    found++;
-                });
-                done = found >= kk;
+            int x, y, z;
+            unpack3(keyof(q), x, y, z);
+            auto take = [&](int, double d2) {
+                sorted_insert(best, d2);
+                found++;
+            };
+            for (int R = 0; R <= 2 && !done; R++) {
+                for (int dz = -R; dz <= R; dz++)
+                    for (int dy = -R; dy <= R; dy++) {
+                        const bool edge = dz == -R || dz == R || dy == -R || dy == R;
+                        const int step = (edge || R == 0) ? 1 : 2 * R;
+                        for (int dx = -R; dx <= R; dx += step)
+                            lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
+                    }
+                const double reach = static_cast<double>(R) * pr.ce;
+                done = found >= kk && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
             }
-            if (!done && kk == kBpKnnMax) {
-#pragma unroll
-                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-                found = 0;
-                int x, y, z;
-                unpack3(keyof(q), x, y, z);
-                auto take = [&](int, double d2) {
-                    sorted_insert(best, d2);
-                    found++;
-                };
-                for (int R = 0; R <= 2 && !done; R++) {
-                    for (int dz = -R; dz <= R; dz++)
-                        for (int dy = -R; dy <= R; dy++) {
-                            const bool edge = dz == -R || dz == R || dy == -R || dy == R;
-                            const int step = (edge || R == 0) ? 1 : 2 * R;
-                            for (int dx = -R; dx <= R; dx += step)
-                                lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
-                        }
-                    const double reach = static_cast<double>(R) * pr.ce;
-                    done = found >= kk && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
-                }
-            }
-#ifdef MC_BP_STAMPS
-            atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
-            if (!done) atomicAdd(&g_bp_stamps[31], 1ull);
-            atomicAdd(&g_bp_stamps[13], 1ull);
-#endif
-            if (!done) {  // whole-wave path below
+            if (!done) {
                 sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
                 continue;
             }
-            double sum = 0.0;
-#pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
-            savg[r] = sum / static_cast<double>(kk);
+            put_mean(r, best);
         }
         __syncthreads();
         const int nfb = sfb[kFbCount];
@@ -1239,6 +1334,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         __syncthreads();
         BP_STAMP(28);
+#ifdef MC_BP_STAMPS
+        if (t == 0 && s < (1 << 16)) g_bp_slot_time[s] = static_cast<unsigned>(__builtin_amdgcn_s_memrealtime() - slot_t0);
+#endif
         if (t == 0) {
             slot_m[s] = m;
             slot_ns[s] = ns;
@@ -1275,7 +1373,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
     const int NL = *cls_cnt;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
 #ifdef MC_BP_STAMPS
-    unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+    unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int k = blockIdx.x; k < NL; k += gridDim.x) {  // the slots of more than kBpLdsN voxels
         BP_STAMP(0);

@@ -1,5 +1,5 @@
 mkdir -p gpurun_out/abl
-for L in libmcgraph.so libmcgraph_abl1.so libmcgraph_abl2.so; do
+for L in libmcgraph.so libmcgraph_abl1.so libmcgraph_abl2.so libmcgraph_abl3.so libmcgraph_abl4.so; do
   MCGRAPH_LIB=maskclustering_amd/$L timeout -k 10 200 python - >> gpurun_out/abl/out.txt 2>&1 <<'PY'
 import os, sys, time
 sys.path.insert(0, '.')

@@ -37,13 +37,17 @@ for rep in range(3):
 names = ["slot-top", "bbox", "cells", "bucket-scan", "scatter", "ncount", "union", "ranks", "labels", "filter",
          "knn", "stats", "survivors"]
 print("call ms", round(dt * 1e3, 2), groups)
+nslots = max(int(buf[14]), 1)
+print("LDS-class slots", int(buf[14]), "mean voxels", round(float(buf[15]) / nslots, 1))
 for off, kern in ((16, "k_bp_denoise_lds"), (0, "k_bp_denoise (large slots)")):
     tot = float(buf[off:off + 13].sum())
-    print(kern, "total clock", tot)
+    print(kern, "total workgroup-busy ms (100 MHz clock)", round(tot / 1e5, 2))
     for k, n in enumerate(names):
-        print(f"  {n:12s} {100.0 * float(buf[off + k]) / max(tot, 1):6.2f} %")
+        per = f"{float(buf[off + k]) / 100.0 / nslots:8.2f} us/slot" if off == 16 else ""
+        print(f"  {n:12s} {100.0 * float(buf[off + k]) / max(tot, 1):6.2f} % {per}")
+print("k-NN points deferred to the ring search", int(buf[30]))
 print("knn points", int(buf[13]), "candidates/point", round(float(buf[29]) / max(int(buf[13]), 1), 1),
-      "rings/point", round(float(buf[30]) / max(int(buf[13]), 1), 2), "fallbacks", int(buf[31]))
+      "fallbacks", int(buf[31]))
 st = ctx.bp_candidates()
 for c, n in ((2, "npix"), (3, "nvox"), (4, "ndbscan"), (5, "nsor")):
     v = st[:, c]

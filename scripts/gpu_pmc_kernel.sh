@@ -15,7 +15,7 @@ for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS
            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $SET --kernel-include-regex "$K" --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 scripts/ablate.py "$SHAPE" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+      python3 ${PROG:-scripts/ablate.py} "$SHAPE" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   find "$OUT/p$i" -name "*counter_collection.csv" -exec mv {} "$OUT/p$i.csv" \;
   rm -rf "$OUT/p$i"
 done
