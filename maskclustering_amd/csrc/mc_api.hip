@@ -32,6 +32,11 @@ enum Stat : int {
     ST_COUNT = 9,
 };
 
+// S6 levels t >= 1 of scenes with at most this many level-0 nodes run the component labelling in
+// one workgroup (k6_components, one launch); level 0 and larger scenes use the multi-workgroup
+// kernels (k6_compress .. k6_memscatter, five launches)
+constexpr int kFusedComponentsMaxN0 = 32768;
+
 }  // namespace
 
 struct mc_ctx {
@@ -921,12 +926,6 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             int *nx_own = toA ? ctx->d_ownA.as<int>() : ctx->d_ownB.as<int>();
             unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
             if (!dense_obs) {
-                if (t > 0) {
-                    TimedScope ts(ctx->timer, s, "s6_columns");
-                    hipLaunchKernelGGL(mc::k6_colupdate, gC, dim3(64), 0, s, Mn, dN, ctx->d_coloff.as<int>(),
-                                       ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), ctx->d_label.as<int>(),
-                                       ctx->d_parent.as<int>());
-                }
                 TimedScope ts(ctx->timer, s, "s6_pairs");
                 hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
                                    ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
@@ -948,24 +947,39 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             }
             {
                 TimedScope ts(ctx->timer, s, "s6_components");
-                hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
-                                   ctx->d_root.as<int>(), ctx->d_isroot.as<int>(), ctx->d_ublen.as<int>(),
-                                   ctx->d_ovf_n.as<int>());
-                mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
-                hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(), ctx->d_rank.as<int>(),
-                                   cur_len, ctx->d_label.as<int>(), ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0,
-                                   ctx->d_memcnt.as<int>(), ctx->d_ublen.as<int>());
-                mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr,
-                                  ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dcap + t + 1);
-                hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, N0, ctx->d_label.as<int>(),
-                                   ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>(),
-                                   ctx->d_final_label.as<int>());
+                if (t > 0 && N0 <= kFusedComponentsMaxN0) {  // N_t <= N_1, typically N0 / 8: one workgroup
+                    hipLaunchKernelGGL(mc::k6_components, dim3(1), dim3(1024), 0, s, dN, dNn, ctx->d_parent.as<int>(),
+                                       ctx->d_root.as<int>(), ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
+                                       ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
+                                       ctx->d_memoff.as<int>(), ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(),
+                                       dcap + t + 1, ctx->d_members.as<int>(), ctx->d_ovf_n.as<int>());
+                } else {
+                    hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
+                                       ctx->d_root.as<int>(), ctx->d_isroot.as<int>(), ctx->d_ublen.as<int>(),
+                                       ctx->d_ovf_n.as<int>());
+                    mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
+                    hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(),
+                                       ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
+                                       ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
+                                       ctx->d_ublen.as<int>());
+                    mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr,
+                                      ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dcap + t + 1);
+                    hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, 0, ctx->d_label.as<int>(),
+                                       ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>(),
+                                       nullptr);
+                }
             }
             {
                 TimedScope ts(ctx->timer, s, "s6_merge");
+                // + the next iteration's column lists (nodes containing each mask, relabelled)
+                const bool cols = !dense_obs && t + 1 < nthr;
+                const mc::ColUpdate cu{Mn, dNn, ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(),
+                                       ctx->d_colnodes.as<int>(), cols ? ctx->d_label.as<int>() : nullptr,
+                                       ctx->d_parent.as<int>(), N0, ctx->d_label.as<int>(),
+                                       ctx->d_final_label.as<int>()};
                 hipLaunchKernelGGL(mc::k6_merge, gK, dim3(256), 0, s, dNn, ctx->d_memoff.as<int>(),
                                    ctx->d_members.as<int>(), cur_off, cur_len, cur_pool, cur_vf, FW,
-                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_own, nx_vf);
+                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_own, nx_vf, cu);
             }
             cur_off = nx_off;
             cur_len = nx_len;

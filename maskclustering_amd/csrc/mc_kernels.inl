@@ -1116,7 +1116,40 @@ __device__ __forceinline__ int col_sort_unique(int *c, int n)
     return u;
 }
 
-// one wave per 64 columns
+// the columns [64 blk, 64 blk + 64) by one wave (lane = column), staged in LDS when they fit
+__device__ __forceinline__ void col_update_block(int blk, int Mn, const int *__restrict__ coloff,
+                                                 int *__restrict__ collen, int *__restrict__ colnodes,
+                                                 const int *__restrict__ label, int *stage)
+{
+    const int lane = lane_id();
+    const int m0 = blk * 64, m1 = min(Mn, m0 + 64);
+    const int m = m0 + lane;
+    if (!label) {
+        if (m < m1) collen[m] = coloff[m + 1] - coloff[m];
+        return;
+    }
+    const int eb = coloff[m0], ee = coloff[m1];
+    if (ee - eb <= kColStage) {
+        for (int x = lane; x < ee - eb; x += 64) stage[x] = colnodes[eb + x];
+        wave_sync();
+        if (m < m1) {
+            int *c = stage + coloff[m] - eb;
+            const int n = collen[m];
+            for (int j = 0; j < n; j++) c[j] = label[c[j]];
+            collen[m] = col_sort_unique(c, n);
+        }
+        wave_sync();
+        for (int x = lane; x < ee - eb; x += 64) colnodes[eb + x] = stage[x];
+        wave_sync();
+    } else if (m < m1) {
+        int *c = colnodes + coloff[m];
+        const int n = collen[m];
+        for (int j = 0; j < n; j++) c[j] = label[c[j]];
+        collen[m] = col_sort_unique(c, n);
+    }
+}
+
+// one wave per 64 columns (level-0 lengths; k6_merge carries the per-iteration update)
 __global__ __launch_bounds__(64) void k6_colupdate(int Mn, const int *__restrict__ dN, const int *__restrict__ coloff,
                                                    int *__restrict__ collen, int *__restrict__ colnodes,
                                                    const int *__restrict__ label, int *__restrict__ parent)
@@ -1125,34 +1158,25 @@ __global__ __launch_bounds__(64) void k6_colupdate(int Mn, const int *__restrict
     const int N = *dN;
     const int nblk_cols = (Mn + 63) / 64;
     for (int i = blockIdx.x * 64 + threadIdx.x; i < N; i += gridDim.x * 64) parent[i] = i;
-    for (int blk = blockIdx.x; blk < nblk_cols; blk += gridDim.x) {
-        const int m0 = blk * 64, m1 = min(Mn, m0 + 64);
-        const int m = m0 + threadIdx.x;
-        if (!label) {
-            if (m < m1) collen[m] = coloff[m + 1] - coloff[m];
-            continue;
-        }
-        const int eb = coloff[m0], ee = coloff[m1];
-        if (ee - eb <= kColStage) {
-            for (int x = threadIdx.x; x < ee - eb; x += 64) stage[x] = colnodes[eb + x];
-            wave_sync();
-            if (m < m1) {
-                int *c = stage + coloff[m] - eb;
-                const int n = collen[m];
-                for (int j = 0; j < n; j++) c[j] = label[c[j]];
-                collen[m] = col_sort_unique(c, n);
-            }
-            wave_sync();
-            for (int x = threadIdx.x; x < ee - eb; x += 64) colnodes[eb + x] = stage[x];
-            wave_sync();
-        } else if (m < m1) {
-            int *c = colnodes + coloff[m];
-            const int n = collen[m];
-            for (int j = 0; j < n; j++) c[j] = label[c[j]];
-            collen[m] = col_sort_unique(c, n);
-        }
-    }
+    for (int blk = blockIdx.x; blk < nblk_cols; blk += gridDim.x)
+        col_update_block(blk, Mn, coloff, collen, colnodes, label, stage);
 }
+
+// The next iteration's column update, folded into k6_merge's launch (it needs only this
+// iteration's labels, which k6_merge does not touch): after the K merge items come
+// ceil(ceil(Mn/64)/4) column items of four 64-column groups, one per wave, staged in the
+// merge bitmap's LDS; the union-find parents of the next level are reset too.
+struct ColUpdate {
+    int Mn;
+    const int *dN;  // next level's node count (parents to reset)
+    const int *coloff;
+    int *collen, *colnodes;
+    const int *label;  // this iteration's labels; null: no column update
+    int *parent;
+    int N0;             // level-0 nodes: final_label[i] = level_label[final_label[i]]
+    const int *level_label;
+    int *final_label;
+};
 
 // Edge rule of update_graph (iterative_clustering.py:20-29) in float32, as torch evaluates
 // it: disconnect if O < thr; connect if fl32(S / fl32(O + 1e-7f)) >= fl32(ct); i != j.
@@ -1434,6 +1458,7 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
     if (threadIdx.x == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
 }
 
+// Multi-workgroup K5-K9 (large N: level 0, and every level of very large scenes).
 // K5: root of every node; flag roots (= smallest member of each component).
 // Also clears the row-length accumulator of the next level and the overflow count.
 __global__ __launch_bounds__(256) void k6_compress(const int *__restrict__ dN, int *__restrict__ parent,
@@ -1483,6 +1508,83 @@ __global__ __launch_bounds__(256) void k6_memscatter(const int *__restrict__ dN,
     }
 }
 
+// K5-K9 in one 1024-thread workgroup (one launch instead of five; every step is O(N)):
+// roots and their ranks in index order (the component order of nx.connected_components,
+// iterative_clustering.py:7), labels, member counts and row-length bounds, their scans (member
+// offsets, next-level row offsets, next N and pool capacity) and the member lists.  Every
+// thread owns a contiguous index range, so each scan is one block scan of per-thread totals.
+// memcnt is zero on entry and on exit.  (The level-0 objects are relabelled in k6_merge.)
+__device__ __forceinline__ int2 block_excl_scan2(int a, int b, int *ws, int &ta, int &tb)
+{
+    const int ea = block_excl_scan<1024>(a, ws, ta);
+    const int eb = block_excl_scan<1024>(b, ws, tb);
+    return make_int2(ea, eb);
+}
+
+__global__ __launch_bounds__(1024) void k6_components(
+    const int *__restrict__ dN, int *__restrict__ dNn, int *__restrict__ parent, int *__restrict__ root,
+    int *__restrict__ rank, const int *__restrict__ n_len, int *__restrict__ label, int *__restrict__ level_out,
+    int *__restrict__ memcnt, int *__restrict__ memoff, int *__restrict__ ublen, int *__restrict__ newoff,
+    int *__restrict__ dcap_next, int *__restrict__ members, int *__restrict__ ovf_n)
+{
+    __shared__ int ws[16];
+    const int N = *dN;
+    const int t = threadIdx.x;
+    if (t == 0) *ovf_n = 0;
+    const int per = (N + 1023) / 1024;
+    const int i0 = min(N, t * per), i1 = min(N, i0 + per);
+    // roots (own range), then ranks of the roots in index order
+    int nr = 0;
+    for (int i = i0; i < i1; i++) {
+        const int r = uf_find(parent, i);
+        root[i] = r;
+        ublen[i] = 0;
+        nr += r == i ? 1 : 0;
+    }
+    int K;
+    int rk = block_excl_scan<1024>(nr, ws, K);
+    for (int i = i0; i < i1; i++)
+        if (root[i] == i) rank[i] = rk++;
+    __syncthreads();
+    // labels, member counts, row-length upper bounds
+    for (int i = t; i < N; i += 1024) {
+        const int k = rank[root[i]];
+        label[i] = k;
+        level_out[i] = k;
+        atomicAdd(&memcnt[k], 1);
+        atomicAdd(&ublen[k], n_len[i]);
+    }
+    __syncthreads();
+    // member offsets and next-level row offsets (K + 1 entries each)
+    const int pk = (K + 1023) / 1024;
+    const int k0 = min(K, t * pk), k1 = min(K, k0 + pk);
+    int s0 = 0, s1 = 0;
+    for (int k = k0; k < k1; k++) {
+        s0 += ld_agent(&memcnt[k]);
+        s1 += ld_agent(&ublen[k]);
+    }
+    int T0, T1;
+    int2 e = block_excl_scan2(s0, s1, ws, T0, T1);
+    for (int k = k0; k < k1; k++) {
+        memoff[k] = e.x;
+        newoff[k] = e.y;
+        e.x += ld_agent(&memcnt[k]);
+        e.y += ld_agent(&ublen[k]);
+    }
+    if (t == 0) {
+        memoff[K] = T0;
+        newoff[K] = T1;
+        *dcap_next = T1;
+        *dNn = K;
+    }
+    __syncthreads();
+    // members of every new node (memcnt returns to zero)
+    for (int i = t; i < N; i += 1024) {
+        const int k = label[i];
+        members[memoff[k] + atomicSub(&memcnt[k], 1) - 1] = i;
+    }
+}
+
 // K10: new node k = OR of its members (node.py:33-34): C row as a sorted unique union
 // (LDS bitmap over the members' [lo, hi] mask range), VF as OR of member VF words.
 // Rows are written at upper-bound offsets; the unused tail of every range gets owner -1.
@@ -1495,14 +1597,32 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
                                                 const unsigned long long *__restrict__ nvf, int FW,
                                                 const int *__restrict__ newoff, int *__restrict__ nn_off,
                                                 int *__restrict__ nn_len, int *__restrict__ npool,
-                                                int *__restrict__ nowner, unsigned long long *__restrict__ nnvf)
+                                                int *__restrict__ nowner, unsigned long long *__restrict__ nnvf,
+                                                ColUpdate cu)
 {
+    static_assert(4 * kColStage <= kMergeBitWords, "column stages alias the merge bitmap");
     __shared__ unsigned bits[kMergeBitWords];
     __shared__ unsigned long long vacc[kMaxFW];
     __shared__ int ws[4];
     __shared__ int s_lo, s_hi;
     const int K = *dK;
-    for (int k = blockIdx.x; k < K; k += gridDim.x) {
+    const int ncolblk = cu.label ? (cu.Mn + 63) / 64 : 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < cu.N0; i += gridDim.x * 256)
+        cu.final_label[i] = cu.level_label[cu.final_label[i]];  // object of every level-0 node
+    if (cu.label) {
+        const int Nn = *cu.dN;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < Nn; i += gridDim.x * 256) cu.parent[i] = i;
+    }
+    for (int item = blockIdx.x; item < K + (ncolblk + 3) / 4; item += gridDim.x) {
+        if (item >= K) {  // uniform per block
+            const int blk = 4 * (item - K) + static_cast<int>(threadIdx.x >> 6);
+            if (blk < ncolblk)
+                col_update_block(blk, cu.Mn, cu.coloff, cu.collen, cu.colnodes, cu.label,
+                                 reinterpret_cast<int *>(bits) + (threadIdx.x >> 6) * kColStage);
+            __syncthreads();
+            continue;
+        }
+        const int k = item;
         const int mb = memoff[k], me = memoff[k + 1];
         const int dst = newoff[k], dend = newoff[k + 1];
         if (me - mb == 1) {
