@@ -75,7 +75,7 @@ struct mc_ctx {
     int64_t nnzC0 = 0;
     // ---- S6 ----
     DevBuf d_parent, d_root, d_isroot, d_rank, d_label, d_levels, d_memcnt, d_memoff, d_ublen, d_newoff;
-    DevBuf d_members, d_colcnt, d_coloff, d_colnodes, d_ovf_list, d_ovf_n, d_scratch, d_touched, d_edges;
+    DevBuf d_members, d_colcnt, d_coloff, d_colnodes, d_ovf_n, d_scratch, d_touched, d_edges;
     DevBuf d_spread;  // spread slots of the S2 boundary counter
     DevBuf d_Nlev, d_final_label;
     DevBuf d_poolA, d_poolB, d_offA, d_offB, d_lenA, d_lenB, d_vfA, d_vfB, d_ownA, d_ownB, d_cap;
@@ -212,7 +212,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_n0_ptoff, &ctx->d_n0_ptlen, &ctx->d_n0_vf, &ctx->d_user_cidx, &ctx->d_user_pts,
                       &ctx->d_parent, &ctx->d_root, &ctx->d_isroot, &ctx->d_rank, &ctx->d_label, &ctx->d_levels,
                       &ctx->d_memcnt, &ctx->d_memoff, &ctx->d_ublen, &ctx->d_newoff, &ctx->d_members, &ctx->d_colcnt,
-                      &ctx->d_coloff, &ctx->d_colnodes, &ctx->d_ovf_list, &ctx->d_ovf_n, &ctx->d_scratch,
+                      &ctx->d_coloff, &ctx->d_colnodes, &ctx->d_ovf_n, &ctx->d_scratch,
                       &ctx->d_touched, &ctx->d_edges, &ctx->d_spread, &ctx->d_Nlev, &ctx->d_final_label,
                       &ctx->d_poolA, &ctx->d_poolB, &ctx->d_offA, &ctx->d_offB, &ctx->d_lenA, &ctx->d_lenB,
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
@@ -859,12 +859,11 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         ctx->d_coloff.reserve((Mn + 2) * 4);
         ctx->d_collen.reserve((Mn + 1) * 4);
         ctx->d_colnodes.reserve(cap * 4);
-        ctx->d_ovf_list.reserve(n0 * 4);
         if (!ctx->d_ovf_n.ptr) {
-            ctx->d_ovf_n.reserve(4);
-            MC_HIP(hipMemsetAsync(ctx->d_ovf_n.ptr, 0, 4, s));  // kept zero by K5
+            ctx->d_ovf_n.reserve((1 + mc::kOvfSlots) * 4);  // [0] unused counter (K5 clears it), [1..] slot locks
+            MC_HIP(hipMemsetAsync(ctx->d_ovf_n.ptr, 0, (1 + mc::kOvfSlots) * 4, s));  // locks kept zero
         }
-        constexpr int kOvfBlocks = 64;
+        constexpr int kOvfBlocks = mc::kOvfSlots;
         if (ctx->scratch_n0 < N0) {
             ctx->d_scratch.reserve(static_cast<size_t>(kOvfBlocks) * n0 * 4);
             ctx->d_touched.reserve(static_cast<size_t>(kOvfBlocks) * n0 * 4);
@@ -927,17 +926,11 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
             if (!dense_obs) {
                 TimedScope ts(ctx->timer, s, "s6_pairs");
+                const mc::OvfWork ow{ctx->d_scratch.as<int>(), ctx->d_touched.as<int>(), N0, ctx->d_ovf_n.as<int>() + 1};
                 hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
                                    ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
                                    ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
-                                   ctx->d_edges.as<unsigned long long>(), ctx->d_ovf_list.as<int>(),
-                                   ctx->d_ovf_n.as<int>());
-                hipLaunchKernelGGL(mc::k6_pairs_overflow, dim3(kOvfBlocks), dim3(256), 0, s, ctx->d_ovf_list.as<int>(),
-                                   ctx->d_ovf_n.as<int>(), cur_off, cur_len, cur_pool, ctx->d_coloff.as<int>(),
-                                   ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
-                                   ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
-                                   ctx->d_edges.as<unsigned long long>(), ctx->d_scratch.as<int>(),
-                                   ctx->d_touched.as<int>(), N0);
+                                   ctx->d_edges.as<unsigned long long>(), ow);
             } else {
                 TimedScope ts(ctx->timer, s, "s6_pairs");
                 hipLaunchKernelGGL(mc::k6_parent_init, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>());

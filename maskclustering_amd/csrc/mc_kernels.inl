@@ -1218,6 +1218,19 @@ constexpr int kPairWaves = 4, kPairBatch = 8, kTestBatch = 4, kTestWords = 4;
 #define MC_ABLATE_PAIRS 0
 #endif
 
+struct OvfWork {
+    int *scratch, *touched;  // kOvfSlots dense counters / touched lists of N0 ints (zero at rest)
+    int N0;
+    int *locks;              // kOvfSlots slot locks (zero at rest)
+};
+constexpr int kOvfLocal = 256;  // overflow nodes per workgroup: <= 4 * ceil(N / (4 * 2048)) <= 128 for N <= 2^18
+__device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf, const int *__restrict__ n_off,
+                                     const int *__restrict__ n_len, const int *__restrict__ pool,
+                                     const int *__restrict__ coloff, const int *__restrict__ collen,
+                                     const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
+                                     int FW, EdgeRule er, int *__restrict__ parent,
+                                     unsigned long long *__restrict__ edges_t);
+
 __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, const int *__restrict__ n_off,
                                                 const int *__restrict__ n_len, const int *__restrict__ pool,
                                                 const int *__restrict__ coloff, const int *__restrict__ collen,
@@ -1225,8 +1238,10 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                                                 const unsigned long long *__restrict__ nvf, int FW,
                                                 const float *__restrict__ thr, int t, float ctf,
                                                 int *__restrict__ parent, unsigned long long *__restrict__ edges,
-                                                int *__restrict__ ovf_list, int *__restrict__ ovf_n)
+                                                OvfWork ow)
 {
+    __shared__ int s_ovf[kOvfLocal];
+    __shared__ int s_novf;
     __shared__ int hkey[kPairWaves][kHashSize];
     __shared__ int hcnt[kPairWaves][kHashSize];
     __shared__ short hused[kPairWaves][kHashMaxFill + 64];
@@ -1244,10 +1259,12 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     unsigned long long nedges = 0;
 
     if (blockIdx.x * kPairWaves >= N) return;  // uniform: nothing for this block
+    if (threadIdx.x == 0) s_novf = 0;
     for (int s = lane; s < kHashSize; s += 64) {
         keys[s] = -1;
         cnts[s] = 0;
     }
+    __syncthreads();
     for (int a = blockIdx.x * kPairWaves + wv; a < N; a += gridDim.x * kPairWaves) {
         if (lane == 0) {
             hfill[wv] = 0;
@@ -1316,7 +1333,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
         wave_sync();
         const int fill = min(hfill[wv], kHashMaxFill);
         const bool ovf = hovf[wv] != 0;
-        if (ovf && lane == 0) ovf_list[atomicAdd(ovf_n, 1)] = a;  // redo this node in the overflow kernel
+        if (ovf && lane == 0) s_ovf[atomicAdd(&s_novf, 1)] = a;  // redone by the whole workgroup below
         const unsigned long long *va = nvf + static_cast<size_t>(a) * FW;
         if (ovf) {
             // clear every slot (inserted keys past the used list are not tracked)
@@ -1376,61 +1393,89 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     // wave-reduce the edge count
     int ne = static_cast<int>(nedges);
     ne = wave_sum(ne);
-    if (MC_ABLATE_PAIRS >= 4) return;
-    if (lane == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
+    if (MC_ABLATE_PAIRS < 4 && lane == 0 && ne)
+        spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
+    __syncthreads();
+    if (s_novf > 0)  // uniform
+        pairs_overflow_local(ow, s_ovf, s_novf, n_off, n_len, pool, coloff, collen, colnodes, nvf, FW, er, parent,
+                             edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL);
 }
 
-// K4b: nodes whose partner set overflowed the LDS hash.  Dense global counters per
-// workgroup slot (scr[N0] zero on entry and on exit) and a touched list.
-__global__ __launch_bounds__(256) void k6_pairs_overflow(
-    const int *__restrict__ ovf_list, const int *__restrict__ ovf_n, const int *__restrict__ n_off,
-    const int *__restrict__ n_len, const int *__restrict__ pool, const int *__restrict__ coloff,
-    const int *__restrict__ collen, const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
-    int FW, const float *__restrict__ thr, int t, float ctf, int *__restrict__ parent,
-    unsigned long long *__restrict__ edges, int *__restrict__ scratch, int *__restrict__ touched, int N0)
+// K4b: nodes whose partner set overflowed the LDS hash, by a whole workgroup with dense global
+// counters (scr[N0] zero on entry and on exit) and a touched list.
+__device__ void pairs_overflow_node(int a, const int *__restrict__ n_off, const int *__restrict__ n_len,
+                                    const int *__restrict__ pool, const int *__restrict__ coloff,
+                                    const int *__restrict__ collen, const int *__restrict__ colnodes,
+                                    const unsigned long long *__restrict__ nvf, int FW, EdgeRule er,
+                                    int *__restrict__ parent, int *__restrict__ scr, int *__restrict__ tl,
+                                    int *ntouch, unsigned long long &nedges)
 {
-    __shared__ int ntouch;
-    __shared__ int ws[4];
-    const int n = *ovf_n;
-    if (n == 0) return;
-    const EdgeRule er{thr[t], ctf};
-    int *scr = scratch + static_cast<size_t>(blockIdx.x) * N0;
-    int *tl = touched + static_cast<size_t>(blockIdx.x) * N0;
-    unsigned long long nedges = 0;
-    for (int q = blockIdx.x; q < n; q += gridDim.x) {
-        const int a = ovf_list[q];
-        if (threadIdx.x == 0) ntouch = 0;
-        __syncthreads();
-        const int o = n_off[a], L = n_len[a];
-        for (int e = 0; e < L; e++) {
-            const int m = pool[o + e];
-            const int cb = coloff[m], ce = cb + collen[m];
-            for (int k = cb + threadIdx.x; k < ce; k += 256) {
-                const int bnode = colnodes[k];
-                if (bnode <= a) continue;
-                if (atomicAdd(&scr[bnode], 1) == 0) tl[atomicAdd(&ntouch, 1)] = bnode;
-            }
+    if (threadIdx.x == 0) *ntouch = 0;
+    __syncthreads();
+    const int o = n_off[a], L = n_len[a];
+    for (int e = 0; e < L; e++) {
+        const int m = pool[o + e];
+        const int cb = coloff[m], ce = cb + collen[m];
+        for (int k = cb + threadIdx.x; k < ce; k += 256) {
+            const int bnode = colnodes[k];
+            if (bnode <= a) continue;
+            if (atomicAdd(&scr[bnode], 1) == 0) tl[atomicAdd(ntouch, 1)] = bnode;
         }
-        __syncthreads();
-        const int nt = ntouch;
-        const unsigned long long *va = nvf + static_cast<size_t>(a) * FW;
-        for (int k = threadIdx.x; k < nt; k += 256) {
-            const int bnode = tl[k];
-            const int s = scr[bnode];
-            scr[bnode] = 0;
-            if (!edge_possible(s, er)) continue;
-            const unsigned long long *vb = nvf + static_cast<size_t>(bnode) * FW;
-            int ob = 0;
-            for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
-            if (edge_ok(ob, s, er)) {
-                nedges++;
-                uf_unite(parent, a, bnode);
-            }
-        }
-        __syncthreads();
     }
-    int ne = block_sum<256>(static_cast<int>(nedges), ws);
-    if (threadIdx.x == 0 && ne) spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
+    __syncthreads();
+    const int nt = *ntouch;
+    const unsigned long long *va = nvf + static_cast<size_t>(a) * FW;
+    for (int k = threadIdx.x; k < nt; k += 256) {
+        const int bnode = tl[k];
+        const int sv = ld_agent(&scr[bnode]);
+        st_agent(&scr[bnode], 0);
+        if (!edge_possible(sv, er)) continue;
+        const unsigned long long *vb = nvf + static_cast<size_t>(bnode) * FW;
+        int ob = 0;
+        for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
+        if (edge_ok(ob, sv, er)) {
+            nedges++;
+            uf_unite(parent, a, bnode);
+        }
+    }
+    __syncthreads();
+}
+
+// Overflow nodes are redone inside k6_pairs' launch (no launch of its own) by the workgroup that
+// listed them, once its own nodes are done, with one of kOvfSlots dense counter slots taken under
+// a lock (rare: only workgroups with an overflowed node touch the locks).  The slots are shared by
+// workgroups on different XCDs within one launch, so their counters are read and cleared with
+// device-coherent accesses.
+constexpr int kOvfSlots = 64;
+__device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf, const int *__restrict__ n_off,
+                                     const int *__restrict__ n_len, const int *__restrict__ pool,
+                                     const int *__restrict__ coloff, const int *__restrict__ collen,
+                                     const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
+                                     int FW, EdgeRule er, int *__restrict__ parent,
+                                     unsigned long long *__restrict__ edges_t)
+{
+    __shared__ int s_slot, ntouch;
+    __shared__ int ws[4];
+    if (threadIdx.x == 0) {
+        int slot = static_cast<int>(blockIdx.x % kOvfSlots);
+        while (atomicCAS(&ow.locks[slot], 0, 1) != 0) {  // holders release without waiting on anyone
+            slot = (slot + 1) % kOvfSlots;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        s_slot = slot;
+    }
+    __syncthreads();
+    int *scr = ow.scratch + static_cast<size_t>(s_slot) * ow.N0;
+    int *tl = ow.touched + static_cast<size_t>(s_slot) * ow.N0;
+    unsigned long long nedges = 0;
+    for (int q = 0; q < novf; q++)
+        pairs_overflow_node(ovf_nodes[q], n_off, n_len, pool, coloff, collen, colnodes, nvf, FW, er, parent, scr, tl,
+                            &ntouch, nedges);
+    const int ne = block_sum<256>(static_cast<int>(nedges), ws);  // (its barriers order the clears before the release)
+    if (threadIdx.x == 0) {
+        if (ne) spread_add(edges_t, static_cast<unsigned long long>(ne));
+        atomicExch(&ow.locks[s_slot], 0);
+    }
 }
 
 // Dense observer-only pairs for ct <= 0 (every pair with O >= thr is an edge, S unused).
