@@ -102,18 +102,6 @@ __device__ __forceinline__ double wave_max_d(double v)
     for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));
     return v;
 }
-__device__ __forceinline__ int wave_min_i(int v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max_i(int v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
-    return v;
-}
 
 // block (256) min / max of 3 doubles, broadcast to every thread; red holds 2*3*4 doubles
 __device__ __forceinline__ void block_minmax3(double mn[3], double mx[3], double *red)

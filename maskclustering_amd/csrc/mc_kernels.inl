@@ -47,6 +47,19 @@ __device__ __forceinline__ int wave_sum(int x)
     return x;
 }
 
+__device__ __forceinline__ int wave_min_i(int v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
 // Block-wide exclusive scan for blockDim.x == NT (multiple of 64). `ws` holds NT/64 ints.
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int *ws, int &total)
@@ -1141,11 +1154,56 @@ __device__ __forceinline__ void col_update_block(int blk, int Mn, const int *__r
         wave_sync();
         for (int x = lane; x < ee - eb; x += 64) colnodes[eb + x] = stage[x];
         wave_sync();
-    } else if (m < m1) {
-        int *c = colnodes + coloff[m];
-        const int n = collen[m];
-        for (int j = 0; j < n; j++) c[j] = label[c[j]];
-        collen[m] = col_sort_unique(c, n);
+    } else {
+        // the group does not fit the stage: its columns one at a time, by the whole wave, as a
+        // sorted-unique set through an LDS bitmap over the column's label range (one lane per
+        // column only when that range exceeds the bitmap)
+        unsigned *bm = reinterpret_cast<unsigned *>(stage);
+        for (int mm = m0; mm < m1; mm++) {
+            int *c = colnodes + coloff[mm];
+            const int n = collen[mm];
+            int lo = INT_MAX, hi = -1;
+            for (int j = lane; j < n; j += 64) {
+                const int l = label[c[j]];
+                lo = min(lo, l);
+                hi = max(hi, l);
+            }
+            lo = wave_min_i(lo);
+            hi = wave_max_i(hi);
+            if (n == 0) continue;
+            const int RW = ((hi - lo) >> 5) + 1;
+            if (RW > kColStage) {
+                if (lane == 0) {
+                    for (int j = 0; j < n; j++) c[j] = label[c[j]];
+                    collen[mm] = col_sort_unique(c, n);
+                }
+                wave_sync();
+                continue;
+            }
+            for (int w = lane; w < RW; w += 64) bm[w] = 0u;
+            wave_sync();
+            for (int j = lane; j < n; j += 64) {
+                const int l = label[c[j]] - lo;
+                atomicOr(&bm[l >> 5], 1u << (l & 31));
+            }
+            wave_sync();
+            int pos = 0;
+            for (int w0 = 0; w0 < RW; w0 += 64) {
+                const unsigned v = w0 + lane < RW ? bm[w0 + lane] : 0u;
+                const int cnt = __popc(v);
+                const int incl = wave_incl_scan(cnt);
+                int o = pos + incl - cnt;
+                unsigned x = v;
+                while (x) {
+                    const int bt = __ffs(x) - 1;
+                    x &= x - 1;
+                    c[o++] = lo + ((w0 + lane) << 5) + bt;
+                }
+                pos += __shfl(incl, 63, 64);
+            }
+            if (lane == 0) collen[mm] = pos;
+            wave_sync();
+        }
     }
 }
 
