@@ -1112,6 +1112,7 @@ __global__ __launch_bounds__(256) void k6_colscatter(const int *__restrict__ dca
 // (a column is the set of nodes contained by mask m).  label == nullptr: initialise
 // the lengths after the level-0 transpose.  Also resets the union-find parents.
 constexpr int kColStage = 2048;
+constexpr int kColLaneMax = 64;  // unstaged columns up to this length are sorted by their own lane
 __device__ __forceinline__ int col_sort_unique(int *c, int n)
 {
     for (int i = 1; i < n; i++) {
@@ -1159,7 +1160,17 @@ __device__ __forceinline__ void col_update_block(int blk, int Mn, const int *__r
         // sorted-unique set through an LDS bitmap over the column's label range (one lane per
         // column only when that range exceeds the bitmap)
         unsigned *bm = reinterpret_cast<unsigned *>(stage);
-        for (int mm = m0; mm < m1; mm++) {
+        // short columns in their own lanes (global memory), long ones by the whole wave below
+        const int nl = m < m1 ? collen[m] : 0;
+        if (m < m1 && nl <= kColLaneMax) {
+            int *c = colnodes + coloff[m];
+            for (int j = 0; j < nl; j++) c[j] = label[c[j]];
+            collen[m] = col_sort_unique(c, nl);
+        }
+        unsigned long long longs = __ballot(m < m1 && nl > kColLaneMax);
+        while (longs) {
+            const int mm = m0 + __ffsll(static_cast<long long>(longs)) - 1;
+            longs &= longs - 1;
             int *c = colnodes + coloff[mm];
             const int n = collen[mm];
             int lo = INT_MAX, hi = -1;
@@ -1221,7 +1232,7 @@ __global__ __launch_bounds__(64) void k6_colupdate(int Mn, const int *__restrict
 }
 
 // The next iteration's column update, folded into k6_merge's launch (it needs only this
-// iteration's labels, which k6_merge does not touch): after the K merge items come
+// iteration's labels, which k6_merge does not touch): before the K merge items come
 // ceil(ceil(Mn/64)/4) column items of four 64-column groups, one per wave, staged in the
 // merge bitmap's LDS; the union-find parents of the next level are reset too.
 struct ColUpdate {
@@ -1716,16 +1727,17 @@ __global__ __launch_bounds__(256) void k6_merge(const int *__restrict__ dK, cons
         const int Nn = *cu.dN;
         for (int i = blockIdx.x * 256 + threadIdx.x; i < Nn; i += gridDim.x * 256) cu.parent[i] = i;
     }
-    for (int item = blockIdx.x; item < K + (ncolblk + 3) / 4; item += gridDim.x) {
-        if (item >= K) {  // uniform per block
-            const int blk = 4 * (item - K) + static_cast<int>(threadIdx.x >> 6);
+    const int ncolitems = (ncolblk + 3) / 4;  // first, so that they spread over the first grid round
+    for (int item = blockIdx.x; item < ncolitems + K; item += gridDim.x) {
+        if (item < ncolitems) {  // uniform per block
+            const int blk = 4 * item + static_cast<int>(threadIdx.x >> 6);
             if (blk < ncolblk)
                 col_update_block(blk, cu.Mn, cu.coloff, cu.collen, cu.colnodes, cu.label,
                                  reinterpret_cast<int *>(bits) + (threadIdx.x >> 6) * kColStage);
             __syncthreads();
             continue;
         }
-        const int k = item;
+        const int k = item - ncolitems;
         const int mb = memoff[k], me = memoff[k + 1];
         const int dst = newoff[k], dend = newoff[k + 1];
         if (me - mb == 1) {
