@@ -198,6 +198,45 @@ int mc_cluster_get_objects(mc_ctx *ctx, uint64_t *vf_bits /* K*ceil(F/64) */,
                            int64_t *pt_off /* K+1 */, int32_t *pt_idx,
                            int64_t *mask_off /* K+1 */, int32_t *mask_idx /* level-0 node ids */);
 
+/* ---- post-processing of the clustered objects ----------------------
+ * Replaces the compute of utils/post_process.py:173-194 (post_process up to export):
+ * dbscan_process (:104-123), filter_point (:40-101), merge_overlapping_objects (:7-37).
+ * Inputs are host arrays.  Nodes are the ones post_process keeps (>= 2 masks, :182), their
+ * points in list(node.point_ids) order (graph/node.py:45); node masks are indices into the
+ * mask table (mask_point_clouds entries) in node.mask_list order, with the frame column of
+ * each.  A node mask whose frame is not among the node's visible frames fails with
+ * MC_ERR_INVALID (the reference raises IndexError at :69). */
+typedef struct mc_pp_params {
+    double dbscan_eps;              /* 0.1   post_process.py:104                    */
+    int32_t dbscan_min_points;      /* 4     post_process.py:109                    */
+    double point_filter_threshold;  /* args.point_filter_threshold, :95             */
+    double overlapping_ratio;       /* 0.8   :194                                   */
+} mc_pp_params;
+
+typedef struct mc_pp_info {
+    int32_t num_objects;   /* DBSCAN objects of all nodes, node order then class order */
+    int32_t num_filtered;  /* objects kept by filter_point                            */
+    int32_t num_final;     /* objects left after merge_overlapping_objects            */
+    int64_t num_entries;   /* node points in total                                    */
+    int64_t num_node_masks;
+} mc_pp_info;
+
+int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32_t num_frames,
+              const double *scene_xyz /* P*3 */, const uint64_t *pfm_bits /* P*ceil(F/64) */,
+              int32_t num_masks, const int64_t *mask_off /* num_masks+1 */, const int32_t *mask_pts,
+              int32_t num_nodes, const uint64_t *node_vf_bits /* num_nodes*ceil(F/64) */,
+              const int64_t *node_pt_off /* num_nodes+1 */, const int32_t *node_pts,
+              const int64_t *node_mask_off /* num_nodes+1 */, const int32_t *node_masks,
+              const int32_t *node_mask_col);
+int mc_pp_get_info(mc_ctx *ctx, mc_pp_info *info);
+/* entry_object: object of each node point when the point passes the detection-ratio filter
+ * and its object is final, else -1; mask_object / mask_coverage: the object each node mask
+ * is assigned to (-1: it intersects none) and its coverage;
+ * object_state: 0 dropped by filter_point, 1 merged away, 2 final; object_node; bbox
+ * (min xyz, max xyz) per DBSCAN object.  Object ids are DBSCAN object ids. */
+int mc_pp_get_results(mc_ctx *ctx, int32_t *entry_object, int32_t *mask_object, double *mask_coverage,
+                      uint8_t *object_state, int32_t *object_node, double *object_bbox);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,17 @@ class BpInfo(ctypes.Structure):
                 ("error_frame", ctypes.c_int32), ("num_mask_points", ctypes.c_int64)]
 
 
+class PPParams(ctypes.Structure):
+    """mc_pp_params: utils/post_process.py:104,109 (DBSCAN), :95 (point filter), :194 (overlap)."""
+    _fields_ = [("dbscan_eps", ctypes.c_double), ("dbscan_min_points", ctypes.c_int32),
+                ("point_filter_threshold", ctypes.c_double), ("overlapping_ratio", ctypes.c_double)]
+
+
+class PPInfo(ctypes.Structure):
+    _fields_ = [("num_objects", ctypes.c_int32), ("num_filtered", ctypes.c_int32), ("num_final", ctypes.c_int32),
+                ("num_entries", ctypes.c_int64), ("num_node_masks", ctypes.c_int64)]
+
+
 _lib = None
 
 
@@ -142,6 +153,9 @@ def load():
         "mc_backproject_copy_points_device": (ctypes.c_int, [vp, vp]),
         "mc_backproject_get_candidates": (ctypes.c_int, [vp, vp]),
         "mc_scene_use_backprojection": (ctypes.c_int, [vp]),
+        "mc_pp_run": (ctypes.c_int, [vp, P(PPParams), i64, i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
+        "mc_pp_get_info": (ctypes.c_int, [vp, P(PPInfo)]),
+        "mc_pp_get_results": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -433,3 +447,40 @@ def _bp_methods():
 
 
 _bp_methods()
+
+
+def _pp_methods():
+    def pp_run(self, params: PPParams, scene_xyz, pfm_bits, num_frames, mask_off, mask_pts, node_vf_bits,
+               node_pt_off, node_pts, node_mask_off, node_masks, node_mask_col):
+        a = dict(scene=np.ascontiguousarray(scene_xyz, np.float64), pfm=np.ascontiguousarray(pfm_bits, np.uint64),
+                 moff=np.ascontiguousarray(mask_off, np.int64), mpts=np.ascontiguousarray(mask_pts, np.int32),
+                 vf=np.ascontiguousarray(node_vf_bits, np.uint64), poff=np.ascontiguousarray(node_pt_off, np.int64),
+                 pts=np.ascontiguousarray(node_pts, np.int32), qoff=np.ascontiguousarray(node_mask_off, np.int64),
+                 qm=np.ascontiguousarray(node_masks, np.int32), qc=np.ascontiguousarray(node_mask_col, np.int32))
+        self._check(self.L.mc_pp_run(self.h, ctypes.byref(params), a["scene"].shape[0], int(num_frames), _ptr(a["scene"]),
+                                     _ptr(a["pfm"]), len(a["moff"]) - 1, _ptr(a["moff"]), _ptr(a["mpts"]),
+                                     len(a["poff"]) - 1, _ptr(a["vf"]), _ptr(a["poff"]), _ptr(a["pts"]), _ptr(a["qoff"]),
+                                     _ptr(a["qm"]), _ptr(a["qc"])))
+
+    def pp_info(self) -> PPInfo:
+        info = PPInfo()
+        self._check(self.L.mc_pp_get_info(self.h, ctypes.byref(info)))
+        return info
+
+    def pp_results(self):
+        i = self.pp_info()
+        K, E, Q = i.num_objects, i.num_entries, i.num_node_masks
+        r = dict(entry_object=np.zeros(max(E, 1), np.int32), mask_object=np.zeros(max(Q, 1), np.int32),
+                 mask_coverage=np.zeros(max(Q, 1), np.float64), object_state=np.zeros(max(K, 1), np.uint8),
+                 object_node=np.zeros(max(K, 1), np.int32), object_bbox=np.zeros((max(K, 1), 6), np.float64))
+        self._check(self.L.mc_pp_get_results(self.h, _ptr(r["entry_object"]), _ptr(r["mask_object"]),
+                                             _ptr(r["mask_coverage"]), _ptr(r["object_state"]), _ptr(r["object_node"]),
+                                             _ptr(r["object_bbox"])))
+        n = dict(entry_object=E, mask_object=Q, mask_coverage=Q, object_state=K, object_node=K, object_bbox=K)
+        return {k: v[:n[k]] for k, v in r.items()}
+
+    for f in (pp_run, pp_info, pp_results):
+        setattr(Context, f.__name__, f)
+
+
+_pp_methods()

@@ -10,6 +10,7 @@
 #include "mc_internal.hpp"
 #include "mc_kernels.inl"
 #include "mc_bp_kernels.inl"
+#include "mc_pp_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -110,6 +111,16 @@ struct mc_ctx {
     int64_t bp_nnz = 0;
     std::vector<int32_t> bp_col, bp_label, bp_stats;
     std::vector<int64_t> bp_off;
+
+    // ---- post-processing ----
+    DevBuf d_pp_posmap;  // one P-entry position map per workgroup, -1 at rest
+    int64_t pp_posmap_P = 0;
+    int pp_posmap_slots = 0;
+    bool have_pp = false;
+    mc_pp_info pp_info{};
+    std::vector<int32_t> pp_entry_obj, pp_qobj, pp_obj_node;
+    std::vector<double> pp_qcov, pp_box;
+    std::vector<uint8_t> pp_state;
 };
 
 namespace {
@@ -1632,6 +1643,265 @@ int mc_scene_use_backprojection(mc_ctx *ctx)
     const std::vector<int64_t> off = ctx->bp_off;
     return mc_scene_set_masks(ctx, ctx->P_scene, ctx->bp_F, static_cast<int32_t>(col.size()), col.data(), lab.data(),
                               off.data(), ctx->d_bp_pts.as<int32_t>(), 1);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// post-processing (utils/post_process.py:173-194)
+// ---------------------------------------------------------------------------------------------
+int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32_t num_frames, const double *scene_xyz,
+              const uint64_t *pfm_bits, int32_t num_masks, const int64_t *mask_off, const int32_t *mask_pts,
+              int32_t num_nodes, const uint64_t *node_vf_bits, const int64_t *node_pt_off, const int32_t *node_pts,
+              const int64_t *node_mask_off, const int32_t *node_masks, const int32_t *node_mask_col)
+{
+    return guarded(ctx, [&] {
+        ctx->have_pp = false;
+        MC_REQUIRE(params, MC_ERR_INVALID, "null params");
+        MC_REQUIRE(num_points >= 0 && num_points < (1ll << 31) && num_frames >= 0 && num_masks >= 0 && num_nodes >= 0,
+                   MC_ERR_INVALID, "bad sizes");
+        MC_REQUIRE(num_frames <= 16384, MC_ERR_UNSUPPORTED, "num_frames must be <= 16384");
+        MC_REQUIRE(params->dbscan_eps > 0 && params->dbscan_min_points >= 1, MC_ERR_INVALID, "bad DBSCAN parameters");
+        MC_REQUIRE(mask_off && node_pt_off && node_mask_off, MC_ERR_INVALID, "null offsets");
+        const int N = num_nodes, F = num_frames, FW = (F + 63) / 64, Mt = num_masks;
+        const int64_t P = num_points, E = node_pt_off[N], Q = node_mask_off[N], MP = mask_off[Mt];
+        MC_REQUIRE(node_pt_off[0] == 0 && node_mask_off[0] == 0 && mask_off[0] == 0, MC_ERR_INVALID, "offsets must start at 0");
+        MC_REQUIRE(E < (1ll << 30) && Q < (1ll << 31), MC_ERR_UNSUPPORTED, "too many node points");
+        MC_REQUIRE((P == 0 || (scene_xyz && pfm_bits)) && (E == 0 || node_pts) && (Q == 0 || (node_masks && node_mask_col)) &&
+                       (MP == 0 || mask_pts) && (N == 0 || node_vf_bits),
+                   MC_ERR_INVALID, "null argument");
+        // host checks and per-node layout: the frame position of each node mask among the node's
+        // visible frames (post_process.py:69), hit-bit words per node point
+        std::vector<int32_t> qfpos(static_cast<size_t>(Q));
+        std::vector<int64_t> hit_off(N + 1, 0);
+        std::vector<int32_t> order(N);
+        for (int k = 0; k < N; k++) {
+            const uint64_t *vf = node_vf_bits + static_cast<int64_t>(k) * FW;
+            int nvf = 0;
+            for (int w = 0; w < FW; w++) nvf += __builtin_popcountll(vf[w]);
+            const int64_t n = node_pt_off[k + 1] - node_pt_off[k];
+            MC_REQUIRE(n >= 0 && node_mask_off[k + 1] >= node_mask_off[k], MC_ERR_INVALID, "offsets must be ascending");
+            for (int64_t q = node_mask_off[k]; q < node_mask_off[k + 1]; q++) {
+                const int c = node_mask_col[q], m = node_masks[q];
+                MC_REQUIRE(m >= 0 && m < Mt, MC_ERR_INVALID, "node mask index out of range");
+                MC_REQUIRE(c >= 0 && c < F && ((vf[c >> 6] >> (c & 63)) & 1ull), MC_ERR_INVALID,
+                           "a mask's frame is not among the node's visible frames (post_process.py:69 IndexError)");
+                int pos = 0;
+                for (int w = 0; w < (c >> 6); w++) pos += __builtin_popcountll(vf[w]);
+                pos += __builtin_popcountll(vf[c >> 6] & ((1ull << (c & 63)) - 1));
+                qfpos[q] = pos;
+            }
+            hit_off[k + 1] = hit_off[k] + n * ((nvf + 63) / 64);
+            order[k] = k;
+        }
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+            return node_pt_off[a + 1] - node_pt_off[a] > node_pt_off[b + 1] - node_pt_off[b];
+        });
+        for (int64_t i = 0; i < E; i++) MC_REQUIRE(node_pts[i] >= 0 && node_pts[i] < P, MC_ERR_INVALID, "node point out of range");
+        for (int64_t i = 0; i < MP; i++) MC_REQUIRE(mask_pts[i] >= 0 && mask_pts[i] < P, MC_ERR_INVALID, "mask point out of range");
+
+        hipStream_t s = ctx->stream;
+        auto up = [&](DevBuf &b, const void *h, size_t bytes) {
+            b.reserve(bytes + 8);
+            if (bytes) MC_HIP(hipMemcpyAsync(b.ptr, h, bytes, hipMemcpyHostToDevice, s));
+        };
+        DevBuf scene, pfm, moff, mpts, npoff, npts, nvf, qoff, qm, qfp, hoff, dorder;
+        up(scene, scene_xyz, static_cast<size_t>(P) * 24);
+        up(pfm, pfm_bits, static_cast<size_t>(P) * FW * 8);
+        up(moff, mask_off, static_cast<size_t>(Mt + 1) * 8);
+        up(mpts, mask_pts, static_cast<size_t>(MP) * 4);
+        up(npoff, node_pt_off, static_cast<size_t>(N + 1) * 8);
+        up(npts, node_pts, static_cast<size_t>(E) * 4);
+        up(nvf, node_vf_bits, static_cast<size_t>(N) * FW * 8);
+        up(qoff, node_mask_off, static_cast<size_t>(N + 1) * 8);
+        up(qm, node_masks, static_cast<size_t>(Q) * 4);
+        up(qfp, qfpos.data(), static_cast<size_t>(Q) * 4);
+        up(hoff, hit_off.data(), static_cast<size_t>(N + 1) * 8);
+        up(dorder, order.data(), static_cast<size_t>(N) * 4);
+
+        mc::PPDev pr;
+        pr.eps2 = params->dbscan_eps * params->dbscan_eps;
+        pr.ce = params->dbscan_eps * 1.01;
+        pr.thr = params->point_filter_threshold;
+        pr.ratio = params->overlapping_ratio;
+        pr.minpts = params->dbscan_min_points;
+
+        // ---- DBSCAN split (dbscan_process) ----
+        DevBuf xyz, pcell, pbkt, bcnt, bstart, blist, ncnt, par, root, rnk, lab, ccnt, nob, nsh, tick;
+        xyz.reserve(E * 24 + 8);
+        pcell.reserve(E * 8 + 8);
+        for (DevBuf *b : {&pbkt, &blist, &ncnt, &par, &root, &rnk, &lab}) b->reserve(E * 4 + 8);
+        bcnt.reserve((2 * E + N + 1) * 4);
+        bstart.reserve((2 * E + N + 1) * 4);
+        ccnt.reserve((E + N + 1) * 4);
+        nob.reserve(N * 4 + 8);
+        nsh.reserve(N * 4 + 8);
+        tick.reserve(16);
+        MC_HIP(hipMemsetAsync(bcnt.ptr, 0, (2 * E + N + 1) * 4, s));
+        MC_HIP(hipMemsetAsync(tick.ptr, 0, 16, s));
+        const int wg = std::max(1, std::min(N, ctx->num_cu * 2));
+        {
+            mc::TimedScope ts(ctx->timer, s, "pp_dbscan");
+            if (E) hipLaunchKernelGGL(mc::k_pp_gather, grid_for(3 * E), dim3(256), 0, s, scene.as<double>(), npts.as<int>(), E,
+                                      xyz.as<double>());
+            if (N) hipLaunchKernelGGL(mc::k_pp_dbscan, dim3(wg), dim3(256), 0, s, N, dorder.as<int>(), tick.as<int>(),
+                                      npoff.as<int64_t>(), pr, xyz.as<double>(), pcell.as<unsigned long long>(), pbkt.as<int>(),
+                                      bcnt.as<int>(), bstart.as<int>(), blist.as<int>(), ncnt.as<int>(), par.as<int>(),
+                                      root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), nob.as<int>(), nsh.as<int>());
+            MC_HIP(hipGetLastError());
+        }
+        std::vector<int32_t> h_nob(N), h_base(N + 1, 0);
+        if (N) MC_HIP(hipMemcpyAsync(h_nob.data(), nob.ptr, N * 4, hipMemcpyDeviceToHost, s));
+        MC_HIP(hipStreamSynchronize(s));
+        for (int k = 0; k < N; k++) h_base[k + 1] = h_base[k] + h_nob[k];
+        const int K = h_base[N];
+        DevBuf obase;
+        up(obase, h_base.data(), static_cast<size_t>(N + 1) * 4);
+
+        // ---- filter_point ----
+        const int slots = std::max(1, std::min(N, ctx->num_cu));
+        if (ctx->pp_posmap_P < P || ctx->pp_posmap_slots < slots) {
+            ctx->d_pp_posmap.release();
+            ctx->d_pp_posmap.reserve(static_cast<size_t>(slots) * P * 4 + 8);
+            MC_HIP(hipMemsetAsync(ctx->d_pp_posmap.ptr, 0xFF, static_cast<size_t>(slots) * P * 4, s));
+            ctx->pp_posmap_P = P;
+            ctx->pp_posmap_slots = slots;
+        }
+        const int64_t H = hit_off[N];
+        DevBuf hit, cvid, qobj, qcov, onm, onv, obox, eobj;
+        hit.reserve(H * 8 + 8);
+        cvid.reserve(E * 4 + 8);
+        qobj.reserve(Q * 4 + 8);
+        qcov.reserve(Q * 8 + 8);
+        onm.reserve(K * 4 + 8);
+        onv.reserve(K * 4 + 8);
+        obox.reserve(K * 48 + 8);
+        eobj.reserve(E * 4 + 8);
+        if (H) MC_HIP(hipMemsetAsync(hit.ptr, 0, H * 8, s));
+        if (K) MC_HIP(hipMemsetAsync(onm.ptr, 0, K * 4, s));
+        {
+            mc::TimedScope ts(ctx->timer, s, "pp_filter");
+            if (N) hipLaunchKernelGGL(mc::k_pp_filter, dim3(slots), dim3(256), 0, s, N, dorder.as<int>(), tick.as<int>() + 1, pr,
+                                      FW, P, npoff.as<int64_t>(), npts.as<int>(), nvf.as<unsigned long long>(),
+                                      hoff.as<int64_t>(), qoff.as<int64_t>(), qm.as<int>(), qfp.as<int>(), moff.as<int64_t>(),
+                                      mpts.as<int>(), pfm.as<unsigned long long>(), xyz.as<double>(), lab.as<int>(),
+                                      ccnt.as<int>(), nob.as<int>(), nsh.as<int>(), obase.as<int>(), ctx->d_pp_posmap.as<int>(),
+                                      hit.as<unsigned long long>(), cvid.as<int>(), qobj.as<int>(), qcov.as<double>(),
+                                      onm.as<int>(), onv.as<int>(), obox.as<double>(), eobj.as<int>());
+            MC_HIP(hipGetLastError());
+        }
+        std::vector<int32_t> h_nm(K), h_nv(K);
+        std::vector<double> h_box(static_cast<size_t>(K) * 6);
+        if (K) {
+            MC_HIP(hipMemcpyAsync(h_nm.data(), onm.ptr, K * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(h_nv.data(), onv.ptr, K * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(h_box.data(), obox.ptr, K * 48, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        // objects kept by filter_point (:96): a kept point and >= 2 masks
+        std::vector<int32_t> kidx(K, -1), kept;
+        std::vector<double> kbox;
+        std::vector<int32_t> klen;
+        for (int o = 0; o < K; o++)
+            if (h_nv[o] > 0 && h_nm[o] >= 2) {
+                kidx[o] = static_cast<int32_t>(kept.size());
+                kept.push_back(o);
+                kbox.insert(kbox.end(), h_box.begin() + 6 * o, h_box.begin() + 6 * o + 6);
+                klen.push_back(h_nv[o]);
+            }
+        const int Kk = static_cast<int>(kept.size());
+        MC_REQUIRE(Kk <= 46340, MC_ERR_UNSUPPORTED, "more than 46340 objects after filter_point");
+
+        // ---- merge_overlapping_objects ----
+        std::vector<uint8_t> h_inv(Kk, 0);
+        if (Kk > 1) {
+            mc::TimedScope ts(ctx->timer, s, "pp_merge");
+            DevBuf dk, pcnt, plist, mxc, inter, dbox, dlen, dec, inv;
+            up(dk, kidx.data(), static_cast<size_t>(K) * 4);
+            up(dbox, kbox.data(), static_cast<size_t>(Kk) * 48);
+            up(dlen, klen.data(), static_cast<size_t>(Kk) * 4);
+            pcnt.reserve(P * 4 + 8);
+            mxc.reserve(8);
+            int sl = mc::kPPSlots;
+            for (int pass = 0; pass < 2; pass++) {
+                plist.reserve(static_cast<size_t>(P) * sl * 4 + 8);
+                MC_HIP(hipMemsetAsync(pcnt.ptr, 0, P * 4, s));
+                MC_HIP(hipMemsetAsync(mxc.ptr, 0, 4, s));
+                hipLaunchKernelGGL(mc::k_pp_index, grid_for(E), dim3(256), 0, s, E, npts.as<int>(), eobj.as<int>(), dk.as<int>(),
+                                   sl, pcnt.as<int>(), plist.as<int>(), mxc.as<int>());
+                int mx = 0;
+                MC_HIP(hipMemcpyAsync(&mx, mxc.ptr, 4, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipStreamSynchronize(s));
+                if (mx <= sl) break;
+                sl = mx;
+            }
+            inter.reserve(static_cast<size_t>(Kk) * Kk * 4);
+            dec.reserve(static_cast<size_t>(Kk) * Kk);
+            inv.reserve(Kk + 8);
+            MC_HIP(hipMemsetAsync(inter.ptr, 0, static_cast<size_t>(Kk) * Kk * 4, s));
+            hipLaunchKernelGGL(mc::k_pp_pairs, grid_for(P), dim3(256), 0, s, P, sl, pcnt.as<int>(), plist.as<int>(), Kk,
+                               inter.as<int>());
+            hipLaunchKernelGGL(mc::k_pp_decide, grid_for(static_cast<int64_t>(Kk) * Kk), dim3(256), 0, s, Kk, pr,
+                               dbox.as<double>(), dlen.as<int>(), inter.as<int>(), dec.as<unsigned char>());
+            hipLaunchKernelGGL(mc::k_pp_greedy, dim3(1), dim3(1024), 0, s, Kk, dec.as<unsigned char>(), inv.as<unsigned char>());
+            MC_HIP(hipGetLastError());
+            MC_HIP(hipMemcpyAsync(h_inv.data(), inv.ptr, Kk, hipMemcpyDeviceToHost, s));
+        }
+        // ---- results ----
+        ctx->pp_state.assign(K, 0);
+        int nfin = 0;
+        for (int i = 0; i < Kk; i++) {
+            ctx->pp_state[kept[i]] = h_inv[i] ? 1 : 2;
+            nfin += h_inv[i] ? 0 : 1;
+        }
+        ctx->pp_entry_obj.resize(E);
+        ctx->pp_qobj.resize(Q);
+        ctx->pp_qcov.resize(Q);
+        if (E) MC_HIP(hipMemcpyAsync(ctx->pp_entry_obj.data(), eobj.ptr, E * 4, hipMemcpyDeviceToHost, s));
+        if (Q) {
+            MC_HIP(hipMemcpyAsync(ctx->pp_qobj.data(), qobj.ptr, Q * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(ctx->pp_qcov.data(), qcov.ptr, Q * 8, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        ctx->timer.collect();
+        for (auto &o : ctx->pp_entry_obj)
+            if (o >= 0 && ctx->pp_state[o] != 2) o = -1;
+        ctx->pp_obj_node.resize(K);
+        for (int k = 0; k < N; k++)
+            for (int o = h_base[k]; o < h_base[k + 1]; o++) ctx->pp_obj_node[o] = k;
+        ctx->pp_box = std::move(h_box);
+        ctx->pp_info.num_objects = K;
+        ctx->pp_info.num_filtered = Kk;
+        ctx->pp_info.num_final = nfin;
+        ctx->pp_info.num_entries = E;
+        ctx->pp_info.num_node_masks = Q;
+        ctx->have_pp = true;
+    });
+}
+
+int mc_pp_get_info(mc_ctx *ctx, mc_pp_info *info)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_pp, MC_ERR_STATE, "no post-processing result");
+        MC_REQUIRE(info, MC_ERR_INVALID, "null argument");
+        *info = ctx->pp_info;
+    });
+}
+
+int mc_pp_get_results(mc_ctx *ctx, int32_t *entry_object, int32_t *mask_object, double *mask_coverage,
+                      uint8_t *object_state, int32_t *object_node, double *object_bbox)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_pp, MC_ERR_STATE, "no post-processing result");
+        auto cp = [](void *dst, const void *src, size_t bytes) {
+            if (dst && bytes) std::memcpy(dst, src, bytes);
+        };
+        cp(entry_object, ctx->pp_entry_obj.data(), ctx->pp_entry_obj.size() * 4);
+        cp(mask_object, ctx->pp_qobj.data(), ctx->pp_qobj.size() * 4);
+        cp(mask_coverage, ctx->pp_qcov.data(), ctx->pp_qcov.size() * 8);
+        cp(object_state, ctx->pp_state.data(), ctx->pp_state.size());
+        cp(object_node, ctx->pp_obj_node.data(), ctx->pp_obj_node.size() * 4);
+        cp(object_bbox, ctx->pp_box.data(), ctx->pp_box.size() * 8);
+    });
 }
 
 }  // extern "C"

@@ -5,8 +5,9 @@ reference's ``main.py`` / ``run.py`` run unchanged on the device path:
     graph.iterative_clustering  -> maskclustering_amd.graph.iterative_clustering
     graph.node                  -> maskclustering_amd.graph.node
     utils.mask_backprojection   -> maskclustering_amd.utils.mask_backprojection
+    utils.post_process          -> maskclustering_amd.utils.post_process
 
-Every other reference module (utils.config, utils.post_process, dataset.*, ...)
+Every other reference module (utils.config, dataset.*, ...)
 is imported from the reference as usual.  ``integration/sitecustomize.py`` calls
 ``install()`` at interpreter start-up.
 """
@@ -20,6 +21,7 @@ ALIASES = {
     "graph.iterative_clustering": "maskclustering_amd.graph.iterative_clustering",
     "graph.node": "maskclustering_amd.graph.node",
     "utils.mask_backprojection": "maskclustering_amd.utils.mask_backprojection",
+    "utils.post_process": "maskclustering_amd.utils.post_process",
 }
 
 

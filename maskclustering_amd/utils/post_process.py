@@ -1,0 +1,149 @@
+"""Drop-in for the reference's ``utils/post_process.py``.
+
+``post_process(dataset, node_list, mask_point_clouds, scene_points, point_frame_matrix,
+frame_list, args)`` keeps the reference's signature and files (post_process.py:173-195).
+Its compute runs on the device in one C-ABI call (``mc_pp_run``, include/mcgraph.h):
+
+* ``dbscan_process`` (:104-123): DBSCAN(eps 0.1, min_points 4) of every node's points at once,
+  one workgroup per node on a hashed grid, in ``list(node.point_ids)`` order (graph/node.py:45),
+  which is what fixes Open3D's label numbering;
+* ``filter_point`` (:40-101): detection ratios from the packed point-frame bits and the node's
+  masks, mask -> object assignment and coverage, per-object kept points and bboxes;
+* ``merge_overlapping_objects`` (:7-37): pairwise intersections from a point -> object index,
+  the bbox / ratio decision of every pair, and the greedy pass in one workgroup.
+
+The host packs the inputs (mask table from ``mask_point_clouds``, point orders, bit rows) and
+rebuilds the reference's lists; ``export`` (:148-170) writes the same files as the reference.
+Errors follow the reference: a mask missing from ``mask_point_clouds`` raises KeyError (:70), a
+mask whose frame is not among its node's visible frames raises IndexError (:69).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from .. import _device
+from .._native import PPParams
+
+
+def _host(x):
+    if hasattr(x, "detach"):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _bits(rows_bool: np.ndarray, F: int) -> np.ndarray:
+    """bool [R, F] -> little-endian u64 words [R, ceil(F/64)] (bit c of word c // 64 = column c)."""
+    FW = (F + 63) // 64
+    b = np.packbits(np.asarray(rows_bool, bool).reshape(-1, F), axis=1, bitorder="little")
+    out = np.zeros((b.shape[0], FW * 8), np.uint8)
+    out[:, :b.shape[1]] = b
+    return out.view("<u8")
+
+
+def _visible(node) -> np.ndarray:
+    if hasattr(node, "visible_bool"):
+        return np.asarray(node.visible_bool(), bool)
+    return _host(node.visible_frame) > 0
+
+
+def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list,
+                         point_filter_threshold, dbscan_eps=0.1, dbscan_min_points=4, overlapping_ratio=0.8):
+    """post_process.py:180-194 on the device: returns (total_point_ids_list, total_mask_list) as the
+    reference hands them to export (object point ids int64 in list order; [(frame_id, mask_id,
+    coverage)] per object)."""
+    nodes = [n for n in node_list if len(n.mask_list) >= 2]   # :182
+    frame_arr = np.array(frame_list)
+    F = len(frame_list)
+    table, mask_arrays = {}, []
+    q_mask, q_col, q_key, vf_rows, orders = [], [], [], [], []
+    for n in nodes:
+        vf = _visible(n)
+        vcols = np.nonzero(vf)[0]
+        node_fids = frame_arr[vcols]
+        for f, m in n.mask_list:
+            pos = np.nonzero(node_fids == f)[0]
+            if len(pos) == 0:                                     # :69
+                raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+            key = f"{f}_{m}"
+            idx = table.get(key)
+            if idx is None:
+                pts = mask_point_clouds[key]                      # KeyError as at :70
+                idx = table[key] = len(mask_arrays)
+                mask_arrays.append(np.fromiter(pts, np.int64, count=len(pts)))
+            q_mask.append(idx)
+            q_col.append(int(vcols[pos[0]]))
+            q_key.append((f, m))
+        vf_rows.append(vf)
+        orders.append(np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))  # list(point_ids), node.py:45
+    if not nodes:
+        return [], []
+    scene = np.ascontiguousarray(_host(scene_points), np.float64).reshape(-1, 3)
+    pfm = _bits(_host(point_frame_matrix), F)
+    mask_off = np.zeros(len(mask_arrays) + 1, np.int64)
+    np.cumsum([len(a) for a in mask_arrays], out=mask_off[1:])
+    pt_off = np.zeros(len(nodes) + 1, np.int64)
+    np.cumsum([len(o) for o in orders], out=pt_off[1:])
+    q_off = np.zeros(len(nodes) + 1, np.int64)
+    np.cumsum([len(n.mask_list) for n in nodes], out=q_off[1:])
+    pts_all = np.concatenate(orders)
+    prm = PPParams(float(dbscan_eps), int(dbscan_min_points), float(point_filter_threshold), float(overlapping_ratio))
+    ctx = _device.context()
+    ctx.pp_run(prm, scene, pfm, F, mask_off, np.concatenate(mask_arrays) if mask_arrays else np.zeros(0, np.int64),
+               _bits(np.stack(vf_rows), F), pt_off, pts_all, q_off, np.array(q_mask, np.int32), np.array(q_col, np.int32))
+    r = ctx.pp_results()
+    final = np.nonzero(r["object_state"] == 2)[0]
+    ent, onode = r["entry_object"], r["object_node"]
+    out_pts = []
+    for o in final:
+        a, b = pt_off[onode[o]], pt_off[onode[o] + 1]
+        out_pts.append(pts_all[a:b][ent[a:b] == o])
+    slot = {int(o): i for i, o in enumerate(final)}
+    out_masks = [[] for _ in final]
+    qobj, qcov = r["mask_object"], r["mask_coverage"]
+    for q in np.nonzero(np.isin(qobj, final))[0]:                 # node order, then mask_list order
+        f, m = q_key[q]
+        out_masks[slot[int(qobj[q])]].append((f, m, float(qcov[q])))
+    return out_pts, out_masks
+
+
+def find_represent_mask(mask_info_list):
+    """post_process.py:126-128: the five masks of largest coverage (sorts the list in place)."""
+    mask_info_list.sort(key=lambda x: x[2], reverse=True)
+    return mask_info_list[:5]
+
+
+def export_class_agnostic_mask(args, class_agnostic_mask_list):
+    """post_process.py:131-145: data/prediction/<config>_class_agnostic/<seq_name>.npz."""
+    os.makedirs(os.path.join("data/prediction", args.config), exist_ok=True)
+    n = len(class_agnostic_mask_list)
+    out_dir = os.path.join("data/prediction", args.config + "_class_agnostic")
+    os.makedirs(out_dir, exist_ok=True)
+    np.savez(os.path.join(out_dir, f"{args.seq_name}.npz"), pred_masks=np.stack(class_agnostic_mask_list, axis=1),
+             pred_score=np.ones(n), pred_classes=np.zeros(n, dtype=np.int32))
+
+
+def export(dataset, total_point_ids_list, total_mask_list, args):
+    """post_process.py:148-170: binary masks over the scene points + the object dict."""
+    P = dataset.get_scene_points().shape[0]
+    masks, object_dict = [], {}
+    for i, (point_ids, mask_list) in enumerate(zip(total_point_ids_list, total_mask_list)):
+        object_dict[i] = {"point_ids": point_ids, "mask_list": mask_list,
+                          "repre_mask_list": find_represent_mask(mask_list)}
+        m = np.zeros(P, dtype=bool)
+        m[list(point_ids)] = True
+        masks.append(m)
+    export_class_agnostic_mask(args, masks)
+    out_dir = os.path.join(dataset.object_dict_dir, args.config)
+    os.makedirs(out_dir, exist_ok=True)
+    np.save(os.path.join(out_dir, "object_dict.npy"), object_dict, allow_pickle=True)
+
+
+def post_process(dataset, node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list, args):
+    """post_process.py:173-195."""
+    if args.debug:
+        print('start exporting')
+    pts, masks = post_process_objects(node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list,
+                                      args.point_filter_threshold)
+    export(dataset, pts, masks, args)

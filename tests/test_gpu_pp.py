@@ -1,0 +1,124 @@
+"""Post-processing on the GPU (maskclustering_amd.utils.post_process, mc_pp_run) against the
+reference's own post_process outputs (tests/golden/pp_small.npz) and the CPU restatement
+(oracle/pp_oracle.py) on seeded synthetic scenes.  Bit-exact: point ids, mask assignment,
+coverage (float64), object order."""
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from oracle import pp_oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "pp_small.npz")
+
+
+def _pp():
+    from maskclustering_amd.utils import post_process
+    return post_process
+
+
+def _node(mask_list, vf, order):
+    # point_ids iterates in the recorded list(point_ids) order of the reference process
+    return SimpleNamespace(mask_list=list(mask_list), visible_frame=np.asarray(vf, np.float32),
+                           point_ids=dict.fromkeys(int(x) for x in order).keys())
+
+
+def _check(got, want_pts, want_masks):
+    gp, gm = got
+    assert len(gp) == len(want_pts)
+    for k in range(len(want_pts)):
+        np.testing.assert_array_equal(np.asarray(gp[k]), np.asarray(want_pts[k], np.int64), err_msg=f"object {k}")
+        assert gp[k].dtype == np.int64
+        assert gm[k] == want_masks[k], f"object {k} masks"
+
+
+@pytest.mark.parametrize("case", ["a", "b"])
+def test_pp_matches_reference_golden(case):
+    z = np.load(GOLD)
+    fids = z["frame_ids"].tolist()
+    keys = [(fids[c], int(l)) for c, l in zip(z["mpc_col"], z["mpc_label"])]
+    mpc = {f"{f}_{m}": set(z["mpc_idx"][z["mpc_off"][i]:z["mpc_off"][i + 1]].tolist()) for i, (f, m) in enumerate(keys)}
+    mo, mi = z[case + "_node_mask_off"], z[case + "_node_mask_idx"]
+    po, pi_ = z[case + "_node_pt_off"], z[case + "_node_pt_idx"]
+    nodes = [_node([keys[q] for q in mi[mo[k]:mo[k + 1]]], z[case + "_node_vf"][k], pi_[po[k]:po[k + 1]])
+             for k in range(len(mo) - 1)]
+    got = _pp().post_process_objects(nodes, mpc, z["scene"], z["pfm"], fids, float(z[case + "_thr"]))
+    oo, oi = z[case + "_obj_pt_off"], z[case + "_obj_pt_idx"]
+    qo, qi, qc = z[case + "_obj_mask_off"], z[case + "_obj_mask_idx"], z[case + "_obj_mask_cov"]
+    want_pts = [oi[oo[k]:oo[k + 1]] for k in range(len(oo) - 1)]
+    want_masks = [[(keys[q][0], keys[q][1], float(c)) for q, c in zip(qi[qo[k]:qo[k + 1]], qc[qo[k]:qo[k + 1]])]
+                  for k in range(len(qo) - 1)]
+    _check(got, want_pts, want_masks)
+
+
+def synthetic_pp(seed, P=6000, F=40, n_nodes=30, blob=0.05):
+    """Blobs of points (some far apart, some touching, isolated noise), nodes over random blob
+    subsets in shuffled order, masks over random point subsets in the node's frames, random pfm,
+    duplicated nodes (overlap merge) and near-duplicates."""
+    rng = np.random.default_rng(seed)
+    nb = 60
+    centers = rng.uniform(0, 4, (nb, 3))
+    centers[1::7] = centers[0::7][: len(centers[1::7])] + 0.12        # touching pairs (border ties)
+    owner = rng.integers(0, nb, P)
+    scene = centers[owner] + rng.normal(0, blob, (P, 3))
+    scene[rng.random(P) < 0.02] += rng.uniform(-0.5, 0.5, (1, 3))     # stray points (noise class)
+    scene = np.round(scene, 3)                                        # exact-distance ties on a grid
+    pfm = rng.random((P, F)) < 0.35
+    frame_ids = [int(x) for x in np.arange(F) * 10]
+    mpc, nodes = {}, []
+    lab = 1
+    for k in range(n_nodes):
+        bl = rng.choice(nb, size=rng.integers(1, 4), replace=False)
+        pts = np.nonzero(np.isin(owner, bl))[0]
+        pts = rng.permutation(pts)
+        vf = rng.random(F) < 0.4
+        vcols = np.nonzero(vf)[0]
+        if len(vcols) == 0:
+            vf[0] = True
+            vcols = np.array([0])
+        ml = []
+        for _ in range(rng.integers(1, 7)):
+            c = int(rng.choice(vcols))
+            sel = pts[rng.random(len(pts)) < rng.uniform(0.1, 0.9)]
+            extra = rng.integers(0, P, 20)                              # points outside the node
+            mpc[f"{frame_ids[c]}_{lab}"] = set(np.concatenate([sel, extra]).tolist())
+            ml.append((frame_ids[c], lab))
+            lab += 1
+        nodes.append((ml, vf, pts))
+    nodes += [nodes[i] for i in range(0, n_nodes, 5)]                  # exact duplicates
+    return scene, pfm, frame_ids, mpc, nodes
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pp_matches_oracle_synthetic(seed):
+    scene, pfm, fids, mpc, nodes = synthetic_pp(seed)
+    thr = [0.5, 0.7, 0.2][seed]
+    got = _pp().post_process_objects([_node(*n) for n in nodes], mpc, scene, pfm, fids, thr)
+    keys = list(mpc.keys())
+    kidx = {k: i for i, k in enumerate(keys)}
+    col = {f: c for c, f in enumerate(fids)}
+    mask_pts = [np.array(sorted(mpc[k]), np.int64) for k in keys]
+    mask_col = np.array([col[int(k.rsplit("_", 1)[0])] for k in keys])
+    onodes = [([kidx[f"{f}_{m}"] for f, m in ml], vf, pts) for ml, vf, pts in nodes]
+    wp, wm = pp_oracle.post_process_objects(scene, pfm, mask_pts, mask_col, onodes, thr)
+    want_masks = [[(int(keys[q].rsplit("_", 1)[0]), int(keys[q].rsplit("_", 1)[1]), c) for q, c in ml] for ml in wm]
+    assert len(wp) > 3
+    _check(got, wp, want_masks)
+
+
+def test_pp_errors_and_empty():
+    pp = _pp()
+    scene = np.zeros((10, 3))
+    pfm = np.zeros((10, 4), bool)
+    assert pp.post_process_objects([], {}, scene, pfm, [0, 1, 2, 3], 0.5) == ([], [])
+    one = _node([(0, 1)], [1, 0, 0, 0], [0, 1])                       # < 2 masks: ignored (:182)
+    assert pp.post_process_objects([one], {}, scene, pfm, [0, 1, 2, 3], 0.5) == ([], [])
+    bad = _node([(0, 1), (1, 2)], [1, 0, 0, 0], [0, 1])               # frame 1 not visible (:69)
+    with pytest.raises(IndexError):
+        pp.post_process_objects([bad], {"0_1": {0}, "1_2": {1}}, scene, pfm, [0, 1, 2, 3], 0.5)
+    missing = _node([(0, 1), (0, 2)], [1, 0, 0, 0], [0, 1])           # no such mask (:70)
+    with pytest.raises(KeyError):
+        pp.post_process_objects([missing], {"0_1": {0}}, scene, pfm, [0, 1, 2, 3], 0.5)
