@@ -9,7 +9,10 @@ A step = one pass of the hot path over one synthetic ScanNet-shaped scene
                 per-object point sets, from per-frame mask sets resident in
                 HBM to final components + merged bitsets in HBM;
   --variant e2e the same preceded by S1 back-projection of every frame from
-                depth / segmentation / poses resident in HBM (640x480 frames).
+                depth / segmentation / poses resident in HBM (640x480 frames);
+  --variant pp  the post-processing row (utils/post_process.py:173-194): the
+                drop-in post_process over the scene's clustered objects
+                (own JSON line: ms per scene, per-kernel device times).
 
 metric: mask-pair consensus counts/sec = Σ_t N_t² (the ordered node pairs whose
 view consensus the reference evaluates, graph/iterative_clustering.py:20-29)
@@ -19,7 +22,7 @@ first metric).  Multi-GPU: one process per GPU, each rank its own scene
 (scene-parallel, the reference's run.py:33-50 pattern): weak scaling, no
 data-path collective.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant g|e2e] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant g|e2e|pp] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -28,6 +31,7 @@ import json
 import os
 import sys
 import time
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -238,12 +242,131 @@ class ShardedEndToEndStep(EndToEndStep):
         return w
 
 
+class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic the path reads
+    def __init__(self, fx, fy, cx, cy):
+        self.f, self.c = (fx, fy), (cx, cy)
+
+    def get_focal_length(self):
+        return self.f
+
+    def get_principal_point(self):
+        return self.c
+
+
+class FrameDataset:  # dataset/scannet.py:34-73 over arrays
+    def __init__(self, fr, frame_ids):
+        self.fr, self.col = fr, {f: c for c, f in enumerate(frame_ids)}
+
+    def get_intrinsics(self, f):
+        return PinholeIntrinsic(*self.fr.intrinsics[self.col[f]])
+
+    def get_extrinsic(self, f):
+        return self.fr.poses[self.col[f]].copy()
+
+    def get_depth(self, f):
+        return self.fr.depth[self.col[f]].copy()
+
+    def get_segmentation(self, f, align_with_depth=False):
+        return self.fr.seg[self.col[f]].copy()
+
+
+def run_post_process(a):
+    """--variant pp: the post-processing row on the c2 RGB-D scene.  The
+    drop-in graph path (S1-S6) makes the scene's objects once; each step is one drop-in
+    post_process_objects call over them (utils/post_process.py:180-194: host packing, mc_pp_run,
+    host lists).  cpu_baseline: oracle/pp_oracle.py (1 thread) on a bounded sample of nodes, the
+    GPU run on the same sample checked bit for bit against it."""
+    import torch
+    from maskclustering_amd import _device
+    from maskclustering_amd.graph import construction, iterative_clustering
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    from maskclustering_amd.utils import post_process as pp
+
+    t0 = time.perf_counter()
+    fr = make_frames_shape(a.shape, seed=0, device="cuda:0")
+    fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
+    log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
+    args = SimpleNamespace(debug=False, mask_visible_threshold=0.3, undersegment_filter_threshold=0.3,
+                           view_consensus_threshold=0.9, contained_threshold=0.8, point_filter_threshold=0.5)
+    t0 = time.perf_counter()
+    nodes, thr, mpc, pfm = construction.mask_graph_construction(args, fr.scene_points, fids, FrameDataset(fr, fids))
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+    log(f"graph path: {len(nodes)} nodes -> {len(objects)} objects in {time.perf_counter() - t0:.1f} s")
+    pfm = np.asarray(pfm)
+    ctx = _device.context()
+    run = lambda nl: pp.post_process_objects(nl, mpc, fr.scene_points, pfm, fids, args.point_filter_threshold)
+    for _ in range(max(a.warmup, 1)):
+        run(objects)
+    groups = ("pp_dbscan", "pp_filter", "pp_merge")
+    ctx.set_timing(True)
+    ctx.reset_kernel_times()
+    walls = []
+    for _ in range(a.steps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        pts, masks = run(objects)
+        walls.append(time.perf_counter() - t)
+    kern = {g: ctx.kernel_time(g)[0] / max(ctx.kernel_time(g)[1], 1) for g in groups}
+    ctx.set_timing(False)
+    info = ctx.pp_info()
+    kept = [o for o in objects if len(o.mask_list) >= 2]
+    E = sum(len(o.point_ids) for o in kept)
+    ms = 1e3 * float(np.sum(walls)) / a.steps
+    res = {"metric": "post_process ms per scene (DBSCAN split + point filter + overlap merge)",
+           "value": round(ms, 3), "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(ms, 3), "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f64", "config": {"workload": f"{a.shape}: objects of the synthetic RGB-D scene, "
+                                                 f"P={fr.num_points} F={fr.num_frames}", "variant": "pp"},
+           "device_ms": {g: round(v, 4) for g, v in kern.items()},
+           "device_total_ms": round(sum(kern.values()), 4),
+           "nodes": len(kept), "node_points": E, "dbscan_objects": info.num_objects,
+           "filtered_objects": info.num_filtered, "final_objects": info.num_final,
+           "output_points": int(sum(len(p) for p in pts)), "data": "synthetic"}
+    budget = 15.0
+    if not a.no_cpu_baseline:
+        from oracle import pp_oracle
+        keys = list(mpc.keys())
+        kidx = {k: i for i, k in enumerate(keys)}
+        col = {f: c for c, f in enumerate(fids)}
+        mask_pts = [np.fromiter(mpc[k], np.int64) for k in keys]
+        mask_col = np.array([col[int(k.rsplit("_", 1)[0])] for k in keys])
+        sample, spent, n_pts = [], 0.0, 0
+        t_cpu = 0.0
+        for o in kept:                     # bounded sample, in scene order
+            one = [([kidx[f"{f}_{m}"] for f, m in o.mask_list], o.visible_bool(), np.fromiter(o.point_ids, np.int64))]
+            t = time.perf_counter()
+            pp_oracle.post_process_objects(fr.scene_points, pfm, mask_pts, mask_col, one, args.point_filter_threshold)
+            t_cpu += time.perf_counter() - t
+            sample.append(o)
+            n_pts += len(o.point_ids)
+            if t_cpu > budget:
+                break
+        onodes = [([kidx[f"{f}_{m}"] for f, m in o.mask_list], o.visible_bool(), np.fromiter(o.point_ids, np.int64))
+                  for o in sample]
+        t = time.perf_counter()
+        wp, wm = pp_oracle.post_process_objects(fr.scene_points, pfm, mask_pts, mask_col, onodes,
+                                                args.point_filter_threshold)
+        t_cpu_all = time.perf_counter() - t
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        gp, gm = run(sample)
+        t_gpu = time.perf_counter() - t
+        same = len(gp) == len(wp) and all(np.array_equal(x, y) for x, y in zip(gp, wp)) and \
+            [[(f, m, c) for f, m, c in x] for x in gm] == \
+            [[(int(keys[q].rsplit("_", 1)[0]), int(keys[q].rsplit("_", 1)[1]), c) for q, c in x] for x in wm]
+        res["cpu_baseline"] = {"kind": "port", "cores": 1, "sample": f"{len(sample)} of {len(kept)} nodes, "
+                               f"{n_pts} of {E} node points (oracle/pp_oracle.py incl. the merge over the sample)",
+                               "cpu_ms": round(1e3 * t_cpu_all, 1), "gpu_ms_same_sample": round(1e3 * t_gpu, 3),
+                               "bit_exact_on_sample": bool(same)}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--variant", choices=["g", "e2e"], default="g")
+    ap.add_argument("--variant", choices=["g", "e2e", "pp"], default="g")
     ap.add_argument("--shape", default="c2")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -251,6 +374,8 @@ def main():
                     help="scene: every rank its own scene (weak scaling); frames: one scene, frames split "
                          "over the ranks (e2e only, strong scaling)")
     args = ap.parse_args()
+    if args.variant == "pp":
+        return run_post_process(args)
 
     import torch
     import torch.distributed as dist

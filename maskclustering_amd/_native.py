@@ -35,6 +35,7 @@ EXPORTED = [
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
+    "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results",
 ]
 
 MC_BP_NSTAT = 10

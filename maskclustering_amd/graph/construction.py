@@ -76,12 +76,51 @@ def _backproject_all(scene_points, frame_list, dataset):
     return ctx
 
 
+class MaskPointClouds(dict):
+    """``{f"{frame_id}_{mask_id}": set}`` exactly as the reference builds it (:57), which also
+    keeps the CSR it was made from (``csr``: key -> row, offsets, point ids) so that
+    utils.post_process can hand the device the rows instead of re-reading every set.  Any
+    assignment or deletion drops the CSR; post_process also checks the set sizes."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.csr = None
+
+    def _drop(self):
+        self.csr = None
+
+    def __setitem__(self, k, v):
+        self._drop()
+        super().__setitem__(k, v)
+
+    def __delitem__(self, k):
+        self._drop()
+        super().__delitem__(k)
+
+
+
+def _dropping(name):
+    def f(self, *a, **kw):
+        self._drop()
+        return getattr(dict, name)(self, *a, **kw)
+    f.__name__ = name
+    return f
+
+
+for _n in ("update", "pop", "popitem", "clear", "setdefault"):
+    setattr(MaskPointClouds, _n, _dropping(_n))
+
+
 def _mask_sets(ctx, frame_list):
     col, lab, off, pts = ctx.bp_masks()
     gl = [(frame_list[c], np.uint8(m)) for c, m in zip(col.tolist(), lab.tolist())]
-    mpc = {}
+    mpc = MaskPointClouds()
+    row = {}
     for g, (fid, mid) in enumerate(gl):
-        mpc[f"{fid}_{mid}"] = set(pts[off[g]:off[g + 1]].tolist())
+        key = f"{fid}_{mid}"
+        dict.__setitem__(mpc, key, set(pts[off[g]:off[g + 1]].tolist()))
+        row[key] = g
+    mpc.csr = (row, np.asarray(off, np.int64), np.asarray(pts))
     return gl, mpc
 
 

@@ -13,7 +13,9 @@ Its compute runs on the device in one C-ABI call (``mc_pp_run``, include/mcgraph
   the bbox / ratio decision of every pair, and the greedy pass in one workgroup.
 
 The host packs the inputs (mask table from ``mask_point_clouds``, point orders, bit rows) and
-rebuilds the reference's lists; ``export`` (:148-170) writes the same files as the reference.
+rebuilds the reference's lists.  When ``mask_point_clouds`` is the one this package's
+``mask_graph_construction`` returned (graph.construction.MaskPointClouds, unmodified), the
+device gets the CSR rows the sets were made from instead of a re-read of every set; ``export`` (:148-170) writes the same files as the reference.
 Errors follow the reference: a mask missing from ``mask_point_clouds`` raises KeyError (:70), a
 mask whose frame is not among its node's visible frames raises IndexError (:69).
 """
@@ -58,22 +60,29 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     F = len(frame_list)
     table, mask_arrays = {}, []
     q_mask, q_col, q_key, vf_rows, orders = [], [], [], [], []
+    csr = getattr(mask_point_clouds, "csr", None)   # rows the drop-in construction made the sets from
     for n in nodes:
         vf = _visible(n)
         vcols = np.nonzero(vf)[0]
-        node_fids = frame_arr[vcols]
+        first = {}                                                # frame id -> first visible column (:69)
+        for c, fid in zip(vcols.tolist(), frame_arr[vcols].tolist()):
+            first.setdefault(fid, c)
         for f, m in n.mask_list:
-            pos = np.nonzero(node_fids == f)[0]
-            if len(pos) == 0:                                     # :69
+            c = first.get(f.item() if hasattr(f, "item") else f)
+            if c is None:                                         # :69
                 raise IndexError("index 0 is out of bounds for axis 0 with size 0")
             key = f"{f}_{m}"
             idx = table.get(key)
             if idx is None:
                 pts = mask_point_clouds[key]                      # KeyError as at :70
+                if csr is not None:
+                    g = csr[0][key]
+                    if csr[1][g + 1] - csr[1][g] != len(pts):     # a set changed in place
+                        csr = None
                 idx = table[key] = len(mask_arrays)
-                mask_arrays.append(np.fromiter(pts, np.int64, count=len(pts)))
+                mask_arrays.append(pts)
             q_mask.append(idx)
-            q_col.append(int(vcols[pos[0]]))
+            q_col.append(c)
             q_key.append((f, m))
         vf_rows.append(vf)
         orders.append(np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))  # list(point_ids), node.py:45
@@ -81,8 +90,16 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
         return [], []
     scene = np.ascontiguousarray(_host(scene_points), np.float64).reshape(-1, 3)
     pfm = _bits(_host(point_frame_matrix), F)
-    mask_off = np.zeros(len(mask_arrays) + 1, np.int64)
-    np.cumsum([len(a) for a in mask_arrays], out=mask_off[1:])
+    if csr is not None:      # the construction's rows: table entry -> CSR row, no set is re-read
+        rows = np.fromiter((csr[0][k] for k in table), np.int64, count=len(table))
+        q_dev = rows[np.asarray(q_mask, np.int64)]
+        mask_off, mask_pts = csr[1], csr[2]
+    else:
+        q_dev = np.asarray(q_mask, np.int64)
+        arrs = [np.fromiter(p, np.int64, count=len(p)) for p in mask_arrays]
+        mask_off = np.zeros(len(arrs) + 1, np.int64)
+        np.cumsum([len(a) for a in arrs], out=mask_off[1:])
+        mask_pts = np.concatenate(arrs) if arrs else np.zeros(0, np.int64)
     pt_off = np.zeros(len(nodes) + 1, np.int64)
     np.cumsum([len(o) for o in orders], out=pt_off[1:])
     q_off = np.zeros(len(nodes) + 1, np.int64)
@@ -90,21 +107,23 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     pts_all = np.concatenate(orders)
     prm = PPParams(float(dbscan_eps), int(dbscan_min_points), float(point_filter_threshold), float(overlapping_ratio))
     ctx = _device.context()
-    ctx.pp_run(prm, scene, pfm, F, mask_off, np.concatenate(mask_arrays) if mask_arrays else np.zeros(0, np.int64),
-               _bits(np.stack(vf_rows), F), pt_off, pts_all, q_off, np.array(q_mask, np.int32), np.array(q_col, np.int32))
+    ctx.pp_run(prm, scene, pfm, F, mask_off, mask_pts, _bits(np.stack(vf_rows), F), pt_off, pts_all, q_off, q_dev,
+               np.array(q_col, np.int32))
     r = ctx.pp_results()
     final = np.nonzero(r["object_state"] == 2)[0]
     ent, onode = r["entry_object"], r["object_node"]
     out_pts = []
-    for o in final:
-        a, b = pt_off[onode[o]], pt_off[onode[o] + 1]
+    for o, k in zip(final.tolist(), onode[final].tolist()):
+        a, b = pt_off[k], pt_off[k + 1]
         out_pts.append(pts_all[a:b][ent[a:b] == o])
-    slot = {int(o): i for i, o in enumerate(final)}
+    slot = np.full(len(r["object_state"]) + 1, -1, np.int64)
+    slot[final] = np.arange(len(final))
+    qslot = slot[r["mask_object"]]                                # mask_object -1 -> slot[-1] = -1
     out_masks = [[] for _ in final]
-    qobj, qcov = r["mask_object"], r["mask_coverage"]
-    for q in np.nonzero(np.isin(qobj, final))[0]:                 # node order, then mask_list order
+    sel = np.nonzero(qslot >= 0)[0]                               # node order, then mask_list order
+    for q, sl, cov in zip(sel.tolist(), qslot[sel].tolist(), r["mask_coverage"][sel].tolist()):
         f, m = q_key[q]
-        out_masks[slot[int(qobj[q])]].append((f, m, float(qcov[q])))
+        out_masks[sl].append((f, m, cov))
     return out_pts, out_masks
 
 

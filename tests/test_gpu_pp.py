@@ -122,3 +122,36 @@ def test_pp_errors_and_empty():
     missing = _node([(0, 1), (0, 2)], [1, 0, 0, 0], [0, 1])           # no such mask (:70)
     with pytest.raises(KeyError):
         pp.post_process_objects([missing], {"0_1": {0}}, scene, pfm, [0, 1, 2, 3], 0.5)
+
+
+def test_pp_after_dropin_graph_path():
+    """The drop-in graph path's own outputs: the CSR fast path (MaskPointClouds) and a plain dict
+    of the same sets give the same objects, equal to the oracle's on the same point orders."""
+    import sys
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import make_api_golden as ag
+    from test_gpu_api import PinholeIntrinsic, _load
+    from maskclustering_amd.graph import construction, iterative_clustering
+    z, frames, fids, args = _load("api_small_scannet")
+    nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
+                                                                ag.FrameDataset(frames, fids, PinholeIntrinsic))
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+    assert getattr(mpc, "csr", None) is not None
+    fast = _pp().post_process_objects(objects, mpc, frames.scene_points, pfm, fids, 0.5)
+    plain = _pp().post_process_objects(objects, dict(mpc), frames.scene_points, pfm, fids, 0.5)
+    keys = list(mpc.keys())
+    kidx = {k: i for i, k in enumerate(keys)}
+    col = {f: c for c, f in enumerate(fids)}
+    onodes = [([kidx[f"{f}_{m}"] for f, m in o.mask_list], o.visible_bool(), np.fromiter(o.point_ids, np.int64))
+              for o in objects]
+    wp, wm = pp_oracle.post_process_objects(np.asarray(frames.scene_points, np.float64), np.asarray(pfm),
+                                            [np.fromiter(mpc[k], np.int64) for k in keys],
+                                            np.array([col[int(k.rsplit("_", 1)[0])] for k in keys]), onodes, 0.5)
+    want_masks = [[(int(keys[q].rsplit("_", 1)[0]), int(keys[q].rsplit("_", 1)[1]), c) for q, c in ml] for ml in wm]
+    assert len(wp) > 5
+    for got in (fast, plain):
+        gm = [[(int(f), int(m), c) for f, m, c in ml] for ml in got[1]]
+        _check((got[0], gm), wp, want_masks)
+    mpc[keys[0]] = set()                       # any assignment drops the CSR fast path
+    assert mpc.csr is None
