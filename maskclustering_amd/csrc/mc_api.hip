@@ -1738,12 +1738,12 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
         tick.reserve(16);
         MC_HIP(hipMemsetAsync(bcnt.ptr, 0, (2 * E + N + 1) * 4, s));
         MC_HIP(hipMemsetAsync(tick.ptr, 0, 16, s));
-        const int wg = std::max(1, std::min(N, ctx->num_cu * 2));
+        const int wg = std::max(1, std::min(N, ctx->num_cu * 2));  // 512-thread workgroups (1024 spills the neighbour walks)
         {
             mc::TimedScope ts(ctx->timer, s, "pp_dbscan");
             if (E) hipLaunchKernelGGL(mc::k_pp_gather, grid_for(3 * E), dim3(256), 0, s, scene.as<double>(), npts.as<int>(), E,
                                       xyz.as<double>());
-            if (N) hipLaunchKernelGGL(mc::k_pp_dbscan, dim3(wg), dim3(256), 0, s, N, dorder.as<int>(), tick.as<int>(),
+            if (N) hipLaunchKernelGGL(mc::k_pp_dbscan<512>, dim3(wg), dim3(512), 0, s, N, dorder.as<int>(), tick.as<int>(),
                                       npoff.as<int64_t>(), pr, xyz.as<double>(), pcell.as<unsigned long long>(), pbkt.as<int>(),
                                       bcnt.as<int>(), bstart.as<int>(), blist.as<int>(), ncnt.as<int>(), par.as<int>(),
                                       root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), nob.as<int>(), nsh.as<int>());
@@ -1840,11 +1840,43 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
             MC_HIP(hipMemsetAsync(inter.ptr, 0, static_cast<size_t>(Kk) * Kk * 4, s));
             hipLaunchKernelGGL(mc::k_pp_pairs, grid_for(P), dim3(256), 0, s, P, sl, pcnt.as<int>(), plist.as<int>(), Kk,
                                inter.as<int>());
+            constexpr int kCap = 1 << 16;
+            DevBuf nl, lst;
+            nl.reserve(8);
+            lst.reserve(static_cast<size_t>(kCap) * sizeof(int2));
+            MC_HIP(hipMemsetAsync(nl.ptr, 0, 4, s));
             hipLaunchKernelGGL(mc::k_pp_decide, grid_for(static_cast<int64_t>(Kk) * Kk), dim3(256), 0, s, Kk, pr,
-                               dbox.as<double>(), dlen.as<int>(), inter.as<int>(), dec.as<unsigned char>());
-            hipLaunchKernelGGL(mc::k_pp_greedy, dim3(1), dim3(1024), 0, s, Kk, dec.as<unsigned char>(), inv.as<unsigned char>());
+                               dbox.as<double>(), dlen.as<int>(), inter.as<int>(), dec.as<unsigned char>(), kCap,
+                               nl.as<int>(), lst.as<int2>());
             MC_HIP(hipGetLastError());
-            MC_HIP(hipMemcpyAsync(h_inv.data(), inv.ptr, Kk, hipMemcpyDeviceToHost, s));
+            int nd = 0;
+            MC_HIP(hipMemcpyAsync(&nd, nl.ptr, 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipStreamSynchronize(s));
+            if (nd <= kCap) {
+                // the greedy pass (post_process.py:14-29) over the non-zero decisions only: zero
+                // decisions change nothing, so visiting (i, j) ascending is the reference's loop
+                std::vector<int2> d(nd);
+                if (nd) MC_HIP(hipMemcpy(d.data(), lst.ptr, static_cast<size_t>(nd) * sizeof(int2), hipMemcpyDeviceToHost));
+                auto jj = [](const int2 &v) { return v.y < 0 ? -1 - v.y : v.y; };
+                std::sort(d.begin(), d.end(), [&](const int2 &a, const int2 &b) {
+                    return a.x != b.x ? a.x < b.x : jj(a) < jj(b);
+                });
+                int row = -1;
+                bool skip = false;
+                for (const int2 &v : d) {
+                    if (v.x != row) {  // "if invalid_object[i]: continue" is read once per row (:15)
+                        row = v.x;
+                        skip = h_inv[row] != 0;
+                    }
+                    if (skip || h_inv[jj(v)]) continue;
+                    if (v.y < 0) h_inv[v.x] = 1;
+                    else h_inv[v.y] = 1;
+                }
+            } else {
+                hipLaunchKernelGGL(mc::k_pp_greedy, dim3(1), dim3(1024), 0, s, Kk, dec.as<unsigned char>(), inv.as<unsigned char>());
+                MC_HIP(hipGetLastError());
+                MC_HIP(hipMemcpyAsync(h_inv.data(), inv.ptr, Kk, hipMemcpyDeviceToHost, s));
+            }
         }
         // ---- results ----
         ctx->pp_state.assign(K, 0);

@@ -42,17 +42,45 @@ __global__ __launch_bounds__(256) void k_pp_gather(const double *__restrict__ sc
         xyz[i] = scene[3 * static_cast<int64_t>(pts[i / 3]) + i % 3];
 }
 
+// block min / max of 3 doubles over NT threads, broadcast; red holds 6 * NT/64 doubles
+template <int NT>
+__device__ __forceinline__ void pp_block_minmax3(double mn[3], double mx[3], double *red)
+{
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const double lo = wave_min_d(mn[c]), hi = wave_max_d(mx[c]);
+        if (lane == 0) {
+            red[c * NW + wv] = lo;
+            red[(3 + c) * NW + wv] = hi;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        mn[c] = red[c * NW];
+        mx[c] = red[(3 + c) * NW];
+        for (int w = 1; w < NW; w++) {
+            mn[c] = fmin(mn[c], red[c * NW + w]);
+            mx[c] = fmax(mx[c], red[(3 + c) * NW + w]);
+        }
+    }
+    __syncthreads();
+}
+
 // DBSCAN of every node (utils/post_process.py:109): labels -> object index within the node
 // (class order: noise first when present, then clusters by smallest core point), object sizes.
-__global__ __launch_bounds__(256) void k_pp_dbscan(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pp_dbscan(
     int N, const int *__restrict__ order, int *__restrict__ ticket, const int64_t *__restrict__ pt_off, PPDev pr,
     const double *__restrict__ xyz, unsigned long long *__restrict__ pcell, int *__restrict__ pbkt,
     int *__restrict__ bcnt, int *__restrict__ bstart, int *__restrict__ blist, int *__restrict__ ncnt,
     int *__restrict__ par, int *__restrict__ root, int *__restrict__ rnk, int *__restrict__ lab,
     int *__restrict__ ccnt, int *__restrict__ nob, int *__restrict__ nsh)
 {
-    __shared__ double red[24];
-    __shared__ int ws[4];
+    __shared__ double red[6 * (NT / 64)];
+    __shared__ int ws[NT / 64];
     __shared__ int s_k;
     const int t = threadIdx.x;
     while (true) {
@@ -71,13 +99,13 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
         const unsigned nb = 2u * static_cast<unsigned>(n);
         // 1. bounding box -> grid origin (cells of 1.01 eps: every eps-neighbour is in the 27 cells)
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        for (int i = t; i < n; i += 256)
+        for (int i = t; i < n; i += NT)
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 mn[c] = fmin(mn[c], P[3 * i + c]);
                 mx[c] = fmax(mx[c], P[3 * i + c]);
             }
-        block_minmax3(mn, mx, red);
+        pp_block_minmax3<NT>(mn, mx, red);
         BpCells g;
         g.pc = pc;
         g.bs = bs;
@@ -86,7 +114,7 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
 #pragma unroll
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
         // 2. cells + bucket counts (bucket counters are zero at rest)
-        for (int i = t; i < n; i += 256) {
+        for (int i = t; i < n; i += NT) {
             int cxyz[3];
 #pragma unroll
             for (int c = 0; c < 3; c++) cxyz[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
@@ -95,16 +123,16 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
             pb[i] = static_cast<int>(b);
             atomicAdd(&bc[b], 1);
         }
-        for (int i = t; i <= n; i += 256) cc[i] = 0;
+        for (int i = t; i <= n; i += NT) cc[i] = 0;
         __syncthreads();
         // 3. bucket starts
         {
             int carry = 0;
-            for (int b0 = 0; b0 < static_cast<int>(nb); b0 += 256) {
+            for (int b0 = 0; b0 < static_cast<int>(nb); b0 += NT) {
                 const int b = b0 + t;
                 const int v = b < static_cast<int>(nb) ? ld_agent(&bc[b]) : 0;
                 int tot;
-                const int ex = block_excl_scan<256>(v, ws, tot);
+                const int ex = block_excl_scan<NT>(v, ws, tot);
                 if (b < static_cast<int>(nb)) bs[b] = carry + ex;
                 carry += tot;
             }
@@ -112,14 +140,14 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
         }
         __syncthreads();
         // 4. counting-sort scatter (bucket counters return to zero)
-        for (int i = t; i < n; i += 256) {
+        for (int i = t; i < n; i += NT) {
             const int b = pb[i];
             bl[bs[b] + atomicSub(&bc[b], 1) - 1] = i;
         }
         __syncthreads();
         auto cell_of = [&](int i, int &x, int &y, int &z) { unpack3(pc[i], x, y, z); };
         // 5. eps-neighbour counts, self included (nanoflann radius search: d2 < eps^2)
-        for (int i = t; i < n; i += 256) {
+        for (int i = t; i < n; i += NT) {
             int x, y, z;
             cell_of(i, x, y, z);
             int cnt = 0;
@@ -131,7 +159,7 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
         }
         __syncthreads();
         // 6. core points connected within eps: union-find, root = smallest index
-        for (int i = t; i < n; i += 256) {
+        for (int i = t; i < n; i += NT) {
             if (nc[i] < pr.minpts) continue;
             int x, y, z;
             cell_of(i, x, y, z);
@@ -146,7 +174,7 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
         int ncl;
         {
             int carry = 0;
-            for (int i0 = 0; i0 < n; i0 += 256) {
+            for (int i0 = 0; i0 < n; i0 += NT) {
                 const int i = i0 + t;
                 int isr = 0;
                 if (i < n && nc[i] >= pr.minpts) {
@@ -155,7 +183,7 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
                     isr = r == i ? 1 : 0;
                 }
                 int tot;
-                const int ex = block_excl_scan<256>(isr, ws, tot);
+                const int ex = block_excl_scan<NT>(isr, ws, tot);
                 if (isr) rk[i] = carry + ex;
                 carry += tot;
             }
@@ -164,7 +192,7 @@ __global__ __launch_bounds__(256) void k_pp_dbscan(
         __syncthreads();
         // 8. labels: a border point joins the first cluster that reaches it = the adjacent cluster
         //    of smallest number; class = label + 1 (post_process.py:109)
-        for (int i = t; i < n; i += 256) {
+        for (int i = t; i < n; i += NT) {
             int l;
             if (nc[i] >= pr.minpts) {
                 l = rk[ro[i]];
@@ -369,9 +397,12 @@ __global__ __launch_bounds__(256) void k_pp_pairs(int64_t P, int slots, const in
 }
 
 // decision of every pair i < j (post_process.py:24-29): 1 = i merged away, 2 = j merged away
+// The non-zero decisions are also appended to a list (order-free; capacity cap) so that the host
+// can run the greedy pass over them alone when they fit.
 __global__ __launch_bounds__(256) void k_pp_decide(int K, PPDev pr, const double *__restrict__ box,
                                                    const int *__restrict__ len, const int *__restrict__ inter,
-                                                   unsigned char *__restrict__ dec)
+                                                   unsigned char *__restrict__ dec, int cap, int *__restrict__ nlist,
+                                                   int2 *__restrict__ list)
 {
     const int64_t tot = static_cast<int64_t>(K) * K;
     for (int64_t x = blockIdx.x * 256ll + threadIdx.x; x < tot; x += gridDim.x * 256ll) {
@@ -389,6 +420,10 @@ __global__ __launch_bounds__(256) void k_pp_decide(int K, PPDev pr, const double
             else if (in / static_cast<double>(len[j]) > pr.ratio) r = 2;
         }
         dec[x] = r;
+        if (r) {
+            const int at = atomicAdd(nlist, 1);
+            if (at < cap) list[at] = make_int2(i, r == 1 ? -1 - j : j);
+        }
     }
 }
 

@@ -61,29 +61,43 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     table, mask_arrays = {}, []
     q_mask, q_col, q_key, vf_rows, orders = [], [], [], [], []
     csr = getattr(mask_point_clouds, "csr", None)   # rows the drop-in construction made the sets from
+    fcol = {}
+    for c, fid in enumerate(frame_arr.tolist()):
+        fcol.setdefault(fid, c)
+    unique_frames = len(fcol) == F
+
+    def add(key):
+        pts = mask_point_clouds[key]                              # KeyError as at :70
+        table[key] = len(mask_arrays)
+        mask_arrays.append(pts)
+
     for n in nodes:
         vf = _visible(n)
-        vcols = np.nonzero(vf)[0]
-        first = {}                                                # frame id -> first visible column (:69)
-        for c, fid in zip(vcols.tolist(), frame_arr[vcols].tolist()):
-            first.setdefault(fid, c)
-        for f, m in n.mask_list:
-            c = first.get(f.item() if hasattr(f, "item") else f)
-            if c is None:                                         # :69
-                raise IndexError("index 0 is out of bounds for axis 0 with size 0")
-            key = f"{f}_{m}"
-            idx = table.get(key)
-            if idx is None:
-                pts = mask_point_clouds[key]                      # KeyError as at :70
-                if csr is not None:
-                    g = csr[0][key]
-                    if csr[1][g + 1] - csr[1][g] != len(pts):     # a set changed in place
-                        csr = None
-                idx = table[key] = len(mask_arrays)
-                mask_arrays.append(pts)
-            q_mask.append(idx)
-            q_col.append(c)
-            q_key.append((f, m))
+        ml = n.mask_list
+        cols = np.array([fcol.get(f, -1) for f, _ in ml], np.int64) if unique_frames else None
+        if cols is not None and (cols >= 0).all() and vf[cols].all():
+            keys = [f"{f}_{m}" for f, m in ml]
+            for key in keys:
+                if key not in table:
+                    add(key)
+            q_mask.extend([table[k] for k in keys])
+            q_col.extend(cols.tolist())
+            q_key.extend(ml)
+        else:                                                     # per mask, in the reference's order
+            vcols = np.nonzero(vf)[0]
+            first = {}                                            # frame id -> first visible column (:69)
+            for c, fid in zip(vcols.tolist(), frame_arr[vcols].tolist()):
+                first.setdefault(fid, c)
+            for f, m in ml:
+                c = first.get(f)
+                if c is None:                                     # :69
+                    raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+                key = f"{f}_{m}"
+                if key not in table:
+                    add(key)
+                q_mask.append(table[key])
+                q_col.append(c)
+                q_key.append((f, m))
         vf_rows.append(vf)
         orders.append(np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))  # list(point_ids), node.py:45
     if not nodes:
@@ -92,6 +106,10 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     pfm = _bits(_host(point_frame_matrix), F)
     if csr is not None:      # the construction's rows: table entry -> CSR row, no set is re-read
         rows = np.fromiter((csr[0][k] for k in table), np.int64, count=len(table))
+        lens = np.fromiter((len(p) for p in mask_arrays), np.int64, count=len(mask_arrays))
+        if not np.array_equal(np.diff(csr[1])[rows], lens):       # a set changed in place
+            csr = None
+    if csr is not None:
         q_dev = rows[np.asarray(q_mask, np.int64)]
         mask_off, mask_pts = csr[1], csr[2]
     else:
