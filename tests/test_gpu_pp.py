@@ -156,3 +156,41 @@ def test_pp_after_dropin_graph_path():
         _check((got[0], gm), wp, want_masks)
     mpc[keys[0]] = set()                       # any assignment drops the CSR fast path
     assert mpc.csr is None
+
+
+def _oracle_vs_gpu(scene, pfm, fids, mpc, nodes, thr):
+    got = _pp().post_process_objects([_node(*n) for n in nodes], mpc, scene, pfm, fids, thr)
+    keys = list(mpc.keys())
+    kidx = {k: i for i, k in enumerate(keys)}
+    col = {f: c for c, f in enumerate(fids)}
+    onodes = [([kidx[f"{f}_{m}"] for f, m in ml], vf, np.asarray(pts, np.int64)) for ml, vf, pts in nodes]
+    wp, wm = pp_oracle.post_process_objects(scene, pfm, [np.array(sorted(mpc[k]), np.int64) for k in keys],
+                                            np.array([col[k.rsplit("_", 1)[0]] if isinstance(fids[0], str)
+                                                      else col[int(k.rsplit("_", 1)[0])] for k in keys]), onodes, thr)
+    want = [[(keys[q].rsplit("_", 1)[0] if isinstance(fids[0], str) else int(keys[q].rsplit("_", 1)[0]),
+              int(keys[q].rsplit("_", 1)[1]), c) for q, c in ml] for ml in wm]
+    _check(got, wp, want)
+    return got
+
+
+def test_pp_edge_cases():
+    """Empty node, all-noise node, masks that hold none of the node's points, a single final
+    object, string frame ids (TASMap, dataset/tasmap.py:26-34), thresholds 0 and 1."""
+    rng = np.random.default_rng(7)
+    P, F = 400, 6
+    scene = np.round(np.concatenate([rng.normal(0, 0.03, (200, 3)),          # one dense blob
+                                     rng.uniform(5, 50, (200, 3))]), 4)     # sparse: all noise
+    pfm = rng.random((P, F)) < 0.5
+    fids = [f"{i:05d}" for i in range(F)]
+    mpc = {f"{fids[0]}_1": set(range(0, 150)), f"{fids[1]}_2": set(range(50, 200)),
+           f"{fids[2]}_3": set(range(300, 320)), f"{fids[3]}_4": set(range(390, 400)),
+           f"{fids[4]}_5": {0}, f"{fids[5]}_6": set(range(200, 400))}
+    vf = np.ones(F, bool)
+    nodes = [([(fids[0], 1), (fids[1], 2)], vf, []),                               # empty node
+             ([(fids[2], 3), (fids[5], 6)], vf, rng.permutation(np.arange(200, 400))),  # all noise
+             ([(fids[3], 4), (fids[4], 5)], vf, rng.permutation(np.arange(0, 200))),  # masks barely touch
+             ([(fids[0], 1), (fids[1], 2), (fids[4], 5)], vf, rng.permutation(np.arange(0, 200)))]
+    for thr in (0.0, 0.5, 1.0):
+        _oracle_vs_gpu(scene, pfm, fids, mpc, nodes, thr)
+    got = _oracle_vs_gpu(scene, pfm, fids, mpc, nodes[3:], 0.0)
+    assert len(got[0]) == 1 and len(got[1][0]) == 3
