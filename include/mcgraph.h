@@ -237,6 +237,17 @@ int mc_pp_get_info(mc_ctx *ctx, mc_pp_info *info);
 int mc_pp_get_results(mc_ctx *ctx, int32_t *entry_object, int32_t *mask_object, double *mask_coverage,
                       uint8_t *object_state, int32_t *object_node, double *object_bbox);
 
+/* ---- instance-evaluation match counts -------------------------------
+ * Replaces the device part of evaluation/evaluate.py:254-329 (assign_instances_for_scan): per
+ * predicted mask k (column k of the [P, K] pred_masks matrix of the prediction npz, non-zero =
+ * in the mask, :289): pred_verts[k] = np.count_nonzero (:290), void_intersection[k] (:303) and
+ * intersection[k * num_gt + g] = |pred_k ∩ gt instance g| (:308).  gt_instance[p] = index of
+ * the ground-truth instance holding point p, or -1. */
+int mc_eval_match_counts(mc_ctx *ctx, int64_t num_points, int32_t num_pred, const uint8_t *pred_masks /* P*K */,
+                         const int32_t *gt_instance /* P */, int32_t num_gt, const uint8_t *void_flags /* P */,
+                         int64_t *pred_verts /* K */, int64_t *void_intersection /* K */,
+                         int64_t *intersection /* K*num_gt */);
+
 #ifdef __cplusplus
 }
 #endif

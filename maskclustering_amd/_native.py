@@ -35,7 +35,7 @@ EXPORTED = [
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
-    "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results",
+    "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts",
 ]
 
 MC_BP_NSTAT = 10
@@ -157,6 +157,7 @@ def load():
         "mc_pp_run": (ctypes.c_int, [vp, P(PPParams), i64, i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
         "mc_pp_get_info": (ctypes.c_int, [vp, P(PPInfo)]),
         "mc_pp_get_results": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+        "mc_eval_match_counts": (ctypes.c_int, [vp, i64, i32, vp, vp, i32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -485,3 +486,23 @@ def _pp_methods():
 
 
 _pp_methods()
+
+
+def _eval_methods():
+    def eval_match_counts(self, pred_masks, gt_instance, num_gt, void_flags):
+        """evaluation/evaluate.py:289-308 on the device: (vert counts [K], void intersections [K],
+        intersections [K, num_gt]) of the columns of pred_masks [P, K]."""
+        pm = np.ascontiguousarray(np.asarray(pred_masks) != 0, np.uint8)
+        P, K = pm.shape
+        g = np.ascontiguousarray(gt_instance, np.int32)
+        v = np.ascontiguousarray(void_flags, np.uint8)
+        verts, vint = np.zeros(max(K, 1), np.int64), np.zeros(max(K, 1), np.int64)
+        inter = np.zeros((max(K, 1), max(int(num_gt), 1)), np.int64)
+        self._check(self.L.mc_eval_match_counts(self.h, P, K, _ptr(pm), _ptr(g), int(num_gt), _ptr(v), _ptr(verts),
+                                                _ptr(vint), _ptr(inter)))
+        return verts[:K], vint[:K], inter[:K, :int(num_gt)]
+
+    Context.eval_match_counts = eval_match_counts
+
+
+_eval_methods()

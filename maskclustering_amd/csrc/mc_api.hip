@@ -11,6 +11,7 @@
 #include "mc_kernels.inl"
 #include "mc_bp_kernels.inl"
 #include "mc_pp_kernels.inl"
+#include "mc_eval_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -1933,6 +1934,57 @@ int mc_pp_get_results(mc_ctx *ctx, int32_t *entry_object, int32_t *mask_object, 
         cp(object_state, ctx->pp_state.data(), ctx->pp_state.size());
         cp(object_node, ctx->pp_obj_node.data(), ctx->pp_obj_node.size() * 4);
         cp(object_bbox, ctx->pp_box.data(), ctx->pp_box.size() * 8);
+    });
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// instance-evaluation match counts (evaluation/evaluate.py:254-329)
+// ---------------------------------------------------------------------------------------------
+int mc_eval_match_counts(mc_ctx *ctx, int64_t num_points, int32_t num_pred, const uint8_t *pred_masks,
+                         const int32_t *gt_instance, int32_t num_gt, const uint8_t *void_flags, int64_t *pred_verts,
+                         int64_t *void_intersection, int64_t *intersection)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_points >= 0 && num_pred >= 0 && num_gt >= 0, MC_ERR_INVALID, "negative size");
+        MC_REQUIRE((num_points == 0 || (gt_instance && void_flags && (num_pred == 0 || pred_masks))) &&
+                       (num_pred == 0 || (pred_verts && void_intersection && (num_gt == 0 || intersection))),
+                   MC_ERR_INVALID, "null argument");
+        const int64_t P = num_points;
+        const int K = num_pred, G = num_gt;
+        for (int64_t p = 0; p < P; p++)
+            MC_REQUIRE(gt_instance[p] >= -1 && gt_instance[p] < G, MC_ERR_INVALID, "gt instance index out of range");
+        hipStream_t s = ctx->stream;
+        DevBuf dpred, dg, dv, dverts, dvi, dint;
+        dpred.reserve(static_cast<size_t>(P) * K + 8);
+        dg.reserve(P * 4 + 8);
+        dv.reserve(P + 8);
+        dverts.reserve(K * 8 + 8);
+        dvi.reserve(K * 8 + 8);
+        dint.reserve(static_cast<size_t>(K) * G * 8 + 8);
+        if (P && K) MC_HIP(hipMemcpyAsync(dpred.ptr, pred_masks, static_cast<size_t>(P) * K, hipMemcpyHostToDevice, s));
+        if (P) {
+            MC_HIP(hipMemcpyAsync(dg.ptr, gt_instance, P * 4, hipMemcpyHostToDevice, s));
+            MC_HIP(hipMemcpyAsync(dv.ptr, void_flags, P, hipMemcpyHostToDevice, s));
+        }
+        MC_HIP(hipMemsetAsync(dverts.ptr, 0, K * 8 + 8, s));
+        MC_HIP(hipMemsetAsync(dvi.ptr, 0, K * 8 + 8, s));
+        MC_HIP(hipMemsetAsync(dint.ptr, 0, static_cast<size_t>(K) * G * 8 + 8, s));
+        {
+            mc::TimedScope ts(ctx->timer, s, "eval_counts");
+            if (P && K)
+                hipLaunchKernelGGL(mc::k_eval_counts, grid_for(P, 256, 8192), dim3(256), 0, s, P, K, G, dpred.as<unsigned char>(),
+                                   dg.as<int>(), dv.as<unsigned char>(), dverts.as<unsigned long long>(),
+                                   dvi.as<unsigned long long>(), dint.as<unsigned long long>());
+            MC_HIP(hipGetLastError());
+        }
+        if (K) {
+            MC_HIP(hipMemcpyAsync(pred_verts, dverts.ptr, K * 8, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(void_intersection, dvi.ptr, K * 8, hipMemcpyDeviceToHost, s));
+            if (G) MC_HIP(hipMemcpyAsync(intersection, dint.ptr, static_cast<size_t>(K) * G * 8, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        ctx->timer.collect();
     });
 }
 
