@@ -9,7 +9,7 @@ OUT=${OUT:-gpurun_out/round}
 mkdir -p "$OUT"
 STEPS=${STEPS:-20}
 BENCH_ARGS=${BENCH_ARGS:-}
-run() { echo "== $*"; "$@"; local rc=$?; echo "rc=$rc"; return $rc; }
+run() { echo "== $*" >&2; "$@"; local rc=$?; echo "rc=$rc" >&2; return $rc; }
 
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   run timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
