@@ -248,6 +248,17 @@ int mc_eval_match_counts(mc_ctx *ctx, int64_t num_points, int32_t num_pred, cons
                          int64_t *pred_verts /* K */, int64_t *void_intersection /* K */,
                          int64_t *intersection /* K*num_gt */);
 
+/* ---- frame decode -------------------------------------------------------
+ * Replaces the per-frame host work of dataset/scannet.py:49-54 (get_depth: uint16 / depth_scale
+ * as float64, stored float32; matterport.py:92 and scannetpp.py:169 alike) and :68-73
+ * (get_segmentation(align_with_depth=True): cv2.resize(seg, (W, H), INTER_NEAREST)) for a batch of
+ * frames.  Inputs are host arrays, or device pointers when inputs_on_device; outputs are device
+ * pointers (e.g. the depth / seg arrays mc_backproject reads).  depth or seg may be NULL. */
+int mc_frames_decode(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                     const uint16_t *depth /* F*H*W */, double depth_scale, int32_t seg_height, int32_t seg_width,
+                     const uint8_t *seg /* F*seg_height*seg_width */, int inputs_on_device,
+                     float *depth_out /* device, F*H*W */, uint8_t *seg_out /* device, F*H*W */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,7 @@ EXPORTED = [
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
-    "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts",
+    "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
 ]
 
 MC_BP_NSTAT = 10
@@ -158,6 +158,7 @@ def load():
         "mc_pp_get_info": (ctypes.c_int, [vp, P(PPInfo)]),
         "mc_pp_get_results": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
         "mc_eval_match_counts": (ctypes.c_int, [vp, i64, i32, vp, vp, i32, vp, vp, vp, vp]),
+        "mc_frames_decode": (ctypes.c_int, [vp, i32, i32, i32, vp, dbl, i32, i32, vp, ctypes.c_int, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -506,3 +507,19 @@ def _eval_methods():
 
 
 _eval_methods()
+
+
+def _io_methods():
+    def frames_decode(self, num_frames, height, width, depth_ptr, depth_scale, seg_shape, seg_ptr, on_device,
+                      depth_out_ptr, seg_out_ptr):
+        """mc_frames_decode (dataset/scannet.py:49-54, :68-73); pointers as ints (None = skip)."""
+        c = lambda x: None if x is None else ctypes.c_void_p(int(x))
+        hs, ws = seg_shape
+        self._check(self.L.mc_frames_decode(self.h, int(num_frames), int(height), int(width), c(depth_ptr),
+                                            float(depth_scale), int(hs), int(ws), c(seg_ptr), 1 if on_device else 0,
+                                            c(depth_out_ptr), c(seg_out_ptr)))
+
+    Context.frames_decode = frames_decode
+
+
+_io_methods()

@@ -12,6 +12,7 @@
 #include "mc_bp_kernels.inl"
 #include "mc_pp_kernels.inl"
 #include "mc_eval_kernels.inl"
+#include "mc_io_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -1982,6 +1983,59 @@ int mc_eval_match_counts(mc_ctx *ctx, int64_t num_points, int32_t num_pred, cons
             MC_HIP(hipMemcpyAsync(pred_verts, dverts.ptr, K * 8, hipMemcpyDeviceToHost, s));
             MC_HIP(hipMemcpyAsync(void_intersection, dvi.ptr, K * 8, hipMemcpyDeviceToHost, s));
             if (G) MC_HIP(hipMemcpyAsync(intersection, dint.ptr, static_cast<size_t>(K) * G * 8, hipMemcpyDeviceToHost, s));
+        }
+        MC_HIP(hipStreamSynchronize(s));
+        ctx->timer.collect();
+    });
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// frame decode (dataset/scannet.py:49-54, :68-73)
+// ---------------------------------------------------------------------------------------------
+int mc_frames_decode(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const uint16_t *depth,
+                     double depth_scale, int32_t seg_height, int32_t seg_width, const uint8_t *seg, int inputs_on_device,
+                     float *depth_out, uint8_t *seg_out)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_frames >= 0 && height >= 0 && width >= 0 && seg_height >= 0 && seg_width >= 0, MC_ERR_INVALID,
+                   "negative size");
+        MC_REQUIRE((!depth || (depth_out && depth_scale != 0.0)) && (!seg || (seg_out && seg_height > 0 && seg_width > 0)),
+                   MC_ERR_INVALID, "missing output or bad scale");
+        const int64_t total = static_cast<int64_t>(num_frames) * height * width;
+        const int64_t stotal = static_cast<int64_t>(num_frames) * seg_height * seg_width;
+        // cv2.resize(..., INTER_NEAREST) tables (OpenCV resizeNN): src = min(floor(dst * (1 / (dsize / ssize))), ssize - 1)
+        std::vector<int> yo(std::max(height, 1)), xo(std::max(width, 1));
+        const double ify = 1.0 / (static_cast<double>(height) / seg_height), ifx = 1.0 / (static_cast<double>(width) / seg_width);
+        for (int y = 0; y < height; y++) yo[y] = std::min(static_cast<int>(std::floor(y * ify)), seg_height - 1);
+        for (int x = 0; x < width; x++) xo[x] = std::min(static_cast<int>(std::floor(x * ifx)), seg_width - 1);
+        hipStream_t s = ctx->stream;
+        DevBuf dd, ds, dyo, dxo;
+        const unsigned short *din = reinterpret_cast<const unsigned short *>(depth);
+        const unsigned char *sin = seg;
+        if (!inputs_on_device) {
+            if (depth) {
+                dd.reserve(total * 2 + 8);
+                if (total) MC_HIP(hipMemcpyAsync(dd.ptr, depth, total * 2, hipMemcpyHostToDevice, s));
+                din = dd.as<unsigned short>();
+            }
+            if (seg) {
+                ds.reserve(stotal + 8);
+                if (stotal) MC_HIP(hipMemcpyAsync(ds.ptr, seg, stotal, hipMemcpyHostToDevice, s));
+                sin = ds.as<unsigned char>();
+            }
+        }
+        dyo.reserve(yo.size() * 4);
+        dxo.reserve(xo.size() * 4);
+        MC_HIP(hipMemcpyAsync(dyo.ptr, yo.data(), yo.size() * 4, hipMemcpyHostToDevice, s));
+        MC_HIP(hipMemcpyAsync(dxo.ptr, xo.data(), xo.size() * 4, hipMemcpyHostToDevice, s));
+        {
+            mc::TimedScope ts(ctx->timer, s, "frames_decode");
+            if (total && (depth || seg))
+                hipLaunchKernelGGL(mc::k_frames_decode, grid_for(total, 256, 16384), dim3(256), 0, s, total, height, width,
+                                   seg_height, seg_width, depth ? din : nullptr, depth_scale, seg ? sin : nullptr,
+                                   dyo.as<int>(), dxo.as<int>(), depth_out, seg_out);
+            MC_HIP(hipGetLastError());
         }
         MC_HIP(hipStreamSynchronize(s));
         ctx->timer.collect();
