@@ -1740,12 +1740,41 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
         tick.reserve(16);
         MC_HIP(hipMemsetAsync(bcnt.ptr, 0, (2 * E + N + 1) * 4, s));
         MC_HIP(hipMemsetAsync(tick.ptr, 0, 16, s));
-        const int wg = std::max(1, std::min(N, ctx->num_cu * 2));  // 512-thread workgroups (1024 spills the neighbour walks)
         {
             mc::TimedScope ts(ctx->timer, s, "pp_dbscan");
             if (E) hipLaunchKernelGGL(mc::k_pp_gather, grid_for(3 * E), dim3(256), 0, s, scene.as<double>(), npts.as<int>(), E,
                                       xyz.as<double>());
-            if (N) hipLaunchKernelGGL(mc::k_pp_dbscan<512>, dim3(wg), dim3(512), 0, s, N, dorder.as<int>(), tick.as<int>(),
+            // nodes above big_min points (the first nbig of the size order) are split over the chip
+            int big_min = mc::kPPLdsUF;
+            if (const char *e = getenv("MC_PP_BIG_MIN")) big_min = std::max(1, atoi(e));
+            int nbig = 0;
+            std::vector<int2> items;
+            while (nbig < N && node_pt_off[order[nbig] + 1] - node_pt_off[order[nbig]] > big_min) {
+                const int k = order[nbig++];
+                const int n = static_cast<int>(node_pt_off[k + 1] - node_pt_off[k]);
+                for (int c = 0; c < n; c += 512) items.push_back(make_int2(k, c));
+            }
+            if (nbig) {
+                DevBuf ditems, gcm;
+                up(ditems, items.data(), items.size() * sizeof(int2));
+                gcm.reserve(static_cast<size_t>(N) * 12 + 8);
+                const mc::PPBig b{npoff.as<int64_t>(), xyz.as<double>(), pcell.as<unsigned long long>(), pbkt.as<int>(),
+                                  bcnt.as<int>(), bstart.as<int>(), blist.as<int>(), ncnt.as<int>(), par.as<int>(),
+                                  root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), gcm.as<int>()};
+                const int ni = static_cast<int>(items.size());
+                hipLaunchKernelGGL(mc::k_pp_big_grid<512>, dim3(nbig), dim3(512), 0, s, nbig, dorder.as<int>(), pr, b);
+                hipLaunchKernelGGL((mc::k_pp_big_walk<512, 0>), dim3(std::min(ni, 65536)), dim3(512), 0, s, ni,
+                                   ditems.as<int2>(), pr, b);
+                hipLaunchKernelGGL((mc::k_pp_big_walk<512, 1>), dim3(std::min(ni, 65536)), dim3(512), 0, s, ni,
+                                   ditems.as<int2>(), pr, b);
+                hipLaunchKernelGGL(mc::k_pp_big_label<512>, dim3(nbig), dim3(512), 0, s, nbig, dorder.as<int>(), pr, b,
+                                   nob.as<int>(), nsh.as<int>());
+                MC_HIP(hipGetLastError());
+                MC_HIP(hipStreamSynchronize(s));  // ditems / gcm are freed at scope exit
+            }
+            if (N > nbig)  // 512-thread workgroups (1024 spills the neighbour walks)
+                hipLaunchKernelGGL(mc::k_pp_dbscan<512>, dim3(std::max(1, std::min(N - nbig, ctx->num_cu * 2))), dim3(512), 0, s,
+                                   N - nbig, dorder.as<int>() + nbig, tick.as<int>(),
                                       npoff.as<int64_t>(), pr, xyz.as<double>(), pcell.as<unsigned long long>(), pbkt.as<int>(),
                                       bcnt.as<int>(), bstart.as<int>(), blist.as<int>(), ncnt.as<int>(), par.as<int>(),
                                       root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), nob.as<int>(), nsh.as<int>());

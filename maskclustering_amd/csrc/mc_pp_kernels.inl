@@ -18,6 +18,7 @@ namespace mc {
 constexpr int kPPObjChunk = 1024;  // per-wave LDS counters of mask ∩ object
 constexpr int kPPBoxChunk = 256;   // per-workgroup LDS bbox / kept-point accumulators
 constexpr int kPPSlots = 16;       // objects per point in the intersection index (grown on demand)
+constexpr int kPPLdsUF = 8192;     // nodes up to this many points keep their union-find in LDS
 
 struct PPDev {
     double eps2, ce, thr, ratio;
@@ -82,6 +83,8 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
     __shared__ double red[6 * (NT / 64)];
     __shared__ int ws[NT / 64];
     __shared__ int s_k;
+    __shared__ int s_par[kPPLdsUF];  // union-find in LDS when the node fits: global-memory find chains
+                                     // (a dependent load per step) made the unions the whole cost
     const int t = threadIdx.x;
     while (true) {
         if (t == 0) s_k = atomicAdd(ticket, 1);
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             for (int R = 0; R <= 1; R++)
                 bp_shell(g, x, y, z, R, [&](int j) { cnt += bp_d2(pi, P + 3 * j) < pr.eps2 ? 1 : 0; });
             nc[i] = cnt;
-            pa[i] = i;
+            if (n <= kPPLdsUF) s_par[i] = i;
+            else pa[i] = i;
         }
         __syncthreads();
         // 6. core points connected within eps: union-find, root = smallest index
@@ -166,7 +170,10 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             const double *pi = P + 3 * i;
             for (int R = 0; R <= 1; R++)
                 bp_shell(g, x, y, z, R, [&](int j) {
-                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) uf_unite(pa, i, j);
+                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) {
+                        if (n <= kPPLdsUF) uf_unite_s(s_par, i, j);
+                        else uf_unite(pa, i, j);
+                    }
                 });
         }
         __syncthreads();
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
                 const int i = i0 + t;
                 int isr = 0;
                 if (i < n && nc[i] >= pr.minpts) {
-                    const int r = uf_find(pa, i);
+                    const int r = n <= kPPLdsUF ? uf_find_s(s_par, i) : uf_find(pa, i);
                     ro[i] = r;
                     isr = r == i ? 1 : 0;
                 }
@@ -213,6 +220,178 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
         __syncthreads();
         // 9. objects = non-empty classes (:115-118): the noise class only when it is non-empty;
         //    object = class - shift
+        if (t == 0) {
+            const int noise = ld_agent(&cc[0]) > 0 ? 1 : 0;
+            nob[k] = ncl + noise;
+            nsh[k] = 1 - noise;
+        }
+        __syncthreads();
+    }
+}
+
+// Large nodes (more than a threshold of points, e.g. a floor of ScanNet++ size) are split over
+// many workgroups: the grid of a node is built by one workgroup (k_pp_big_grid), the neighbour
+// counts and the core-point unions run on (node, 512-point chunk) items over the whole chip
+// (k_pp_big_walk), and ranks / labels / objects again per node (k_pp_big_label).  Same steps and
+// results as k_pp_dbscan.
+struct PPBig {
+    const int64_t *pt_off;
+    const double *xyz;
+    unsigned long long *pcell;
+    int *pbkt, *bcnt, *bstart, *blist, *ncnt, *par, *root, *rnk, *lab, *ccnt;
+    int *gcm;  // per node: cmax[3]
+};
+
+__device__ __forceinline__ BpCells pp_cells(const PPBig &b, int k, int64_t e0, int n)
+{
+    BpCells g;
+    g.pc = b.pcell + e0;
+    g.bs = b.bstart + 2 * e0 + k;
+    g.bl = b.blist + e0;
+    g.nb = 2u * static_cast<unsigned>(n);
+#pragma unroll
+    for (int c = 0; c < 3; c++) g.cmax[c] = b.gcm[3 * k + c];
+    return g;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pp_big_grid(int nbig, const int *__restrict__ big, PPDev pr, PPBig b)
+{
+    __shared__ double red[6 * (NT / 64)];
+    __shared__ int ws[NT / 64];
+    const int t = threadIdx.x;
+    for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
+        const int k = big[q];
+        const int64_t e0 = b.pt_off[k];
+        const int n = static_cast<int>(b.pt_off[k + 1] - e0);
+        const double *P = b.xyz + 3 * e0;
+        unsigned long long *pc = b.pcell + e0;
+        int *pb = b.pbkt + e0, *bc = b.bcnt + 2 * e0 + k, *bs = b.bstart + 2 * e0 + k, *bl = b.blist + e0;
+        int *pa = b.par + e0, *cc = b.ccnt + e0 + k;
+        const unsigned nb = 2u * static_cast<unsigned>(n);
+        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int i = t; i < n; i += NT)
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                mn[c] = fmin(mn[c], P[3 * i + c]);
+                mx[c] = fmax(mx[c], P[3 * i + c]);
+            }
+        pp_block_minmax3<NT>(mn, mx, red);
+        if (t == 0)
+#pragma unroll
+            for (int c = 0; c < 3; c++) b.gcm[3 * k + c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
+        for (int i = t; i < n; i += NT) {
+            int cxyz[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) cxyz[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
+            pc[i] = pack3(cxyz[0], cxyz[1], cxyz[2]);
+            const unsigned h = mod_mul(bp_hash3(cxyz[0], cxyz[1], cxyz[2]), nb);
+            pb[i] = static_cast<int>(h);
+            atomicAdd(&bc[h], 1);
+            pa[i] = i;
+        }
+        for (int i = t; i <= n; i += NT) cc[i] = 0;
+        __syncthreads();
+        int carry = 0;
+        for (int b0 = 0; b0 < static_cast<int>(nb); b0 += NT) {
+            const int h = b0 + t;
+            const int v = h < static_cast<int>(nb) ? ld_agent(&bc[h]) : 0;
+            int tot;
+            const int ex = block_excl_scan<NT>(v, ws, tot);
+            if (h < static_cast<int>(nb)) bs[h] = carry + ex;
+            carry += tot;
+        }
+        if (t == 0) bs[nb] = carry;
+        __syncthreads();
+        for (int i = t; i < n; i += NT) {
+            const int h = pb[i];
+            bl[bs[h] + atomicSub(&bc[h], 1) - 1] = i;
+        }
+        __syncthreads();
+    }
+}
+
+// PASS 0: eps-neighbour counts; PASS 1: unions of core points (root = smallest index)
+template <int NT, int PASS>
+__global__ __launch_bounds__(NT) void k_pp_big_walk(int nitems, const int2 *__restrict__ items, PPDev pr, PPBig b)
+{
+    for (int q = blockIdx.x; q < nitems; q += gridDim.x) {
+        const int k = items[q].x;
+        const int64_t e0 = b.pt_off[k];
+        const int n = static_cast<int>(b.pt_off[k + 1] - e0);
+        const int i = items[q].y + static_cast<int>(threadIdx.x);
+        if (i >= n) continue;
+        const BpCells g = pp_cells(b, k, e0, n);
+        const double *P = b.xyz + 3 * e0;
+        int *nc = b.ncnt + e0;
+        int x, y, z;
+        unpack3(g.pc[i], x, y, z);
+        const double *pi = P + 3 * i;
+        if (PASS == 0) {
+            int cnt = 0;
+            for (int R = 0; R <= 1; R++)
+                bp_shell(g, x, y, z, R, [&](int j) { cnt += bp_d2(pi, P + 3 * j) < pr.eps2 ? 1 : 0; });
+            nc[i] = cnt;
+        } else {
+            if (nc[i] < pr.minpts) continue;
+            int *pa = b.par + e0;
+            for (int R = 0; R <= 1; R++)
+                bp_shell(g, x, y, z, R, [&](int j) {
+                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) uf_unite(pa, i, j);
+                });
+        }
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pp_big_label(int nbig, const int *__restrict__ big, PPDev pr, PPBig b,
+                                                     int *__restrict__ nob, int *__restrict__ nsh)
+{
+    __shared__ int ws[NT / 64];
+    const int t = threadIdx.x;
+    for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
+        const int k = big[q];
+        const int64_t e0 = b.pt_off[k];
+        const int n = static_cast<int>(b.pt_off[k + 1] - e0);
+        const BpCells g = pp_cells(b, k, e0, n);
+        const double *P = b.xyz + 3 * e0;
+        int *nc = b.ncnt + e0, *pa = b.par + e0, *ro = b.root + e0, *rk = b.rnk + e0, *lb = b.lab + e0;
+        int *cc = b.ccnt + e0 + k;
+        int carry = 0;
+        for (int i0 = 0; i0 < n; i0 += NT) {
+            const int i = i0 + t;
+            int isr = 0;
+            if (i < n && nc[i] >= pr.minpts) {
+                const int r = uf_find(pa, i);
+                ro[i] = r;
+                isr = r == i ? 1 : 0;
+            }
+            int tot;
+            const int ex = block_excl_scan<NT>(isr, ws, tot);
+            if (isr) rk[i] = carry + ex;
+            carry += tot;
+        }
+        const int ncl = carry;
+        __syncthreads();
+        for (int i = t; i < n; i += NT) {
+            int l;
+            if (nc[i] >= pr.minpts) {
+                l = rk[ro[i]];
+            } else {
+                int x, y, z;
+                unpack3(g.pc[i], x, y, z);
+                const double *pi = P + 3 * i;
+                int mr = INT_MAX;
+                for (int R = 0; R <= 1; R++)
+                    bp_shell(g, x, y, z, R, [&](int j) {
+                        if (nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) mr = min(mr, ro[j]);
+                    });
+                l = mr == INT_MAX ? -1 : rk[mr];
+            }
+            lb[i] = l + 1;
+            atomicAdd(&cc[l + 1], 1);
+        }
+        __syncthreads();
         if (t == 0) {
             const int noise = ld_agent(&cc[0]) > 0 ? 1 : 0;
             nob[k] = ncl + noise;

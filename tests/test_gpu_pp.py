@@ -194,3 +194,25 @@ def test_pp_edge_cases():
         _oracle_vs_gpu(scene, pfm, fids, mpc, nodes, thr)
     got = _oracle_vs_gpu(scene, pfm, fids, mpc, nodes[3:], 0.0)
     assert len(got[0]) == 1 and len(got[1][0]) == 3
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_pp_split_dbscan_path(seed, monkeypatch):
+    """Nodes above MC_PP_BIG_MIN points take the split DBSCAN (grid per node, neighbour counts and
+    unions on 512-point chunks over the chip, labels per node): same objects as the oracle."""
+    monkeypatch.setenv("MC_PP_BIG_MIN", "60")
+    scene, pfm, fids, mpc, nodes = synthetic_pp(seed, **(dict(nb=12, n_nodes=50) if seed == 3 else {}))
+    _oracle_vs_gpu(scene, pfm, fids, mpc, nodes, 0.5)
+    z = np.load(GOLD)
+    fids = z["frame_ids"].tolist()
+    keys = [(fids[c], int(l)) for c, l in zip(z["mpc_col"], z["mpc_label"])]
+    mpc = {f"{f}_{m}": set(z["mpc_idx"][z["mpc_off"][i]:z["mpc_off"][i + 1]].tolist()) for i, (f, m) in enumerate(keys)}
+    mo, mi = z["b_node_mask_off"], z["b_node_mask_idx"]
+    po, pi_ = z["b_node_pt_off"], z["b_node_pt_idx"]
+    nodes = [_node([keys[q] for q in mi[mo[k]:mo[k + 1]]], z["b_node_vf"][k], pi_[po[k]:po[k + 1]])
+             for k in range(len(mo) - 1)]
+    got = _pp().post_process_objects(nodes, mpc, z["scene"], z["pfm"], fids, float(z["b_thr"]))
+    oo, oi = z["b_obj_pt_off"], z["b_obj_pt_idx"]
+    assert len(got[0]) == len(oo) - 1
+    for k in range(len(oo) - 1):
+        np.testing.assert_array_equal(got[0][k], oi[oo[k]:oo[k + 1]].astype(np.int64))
