@@ -1728,7 +1728,10 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
         pr.minpts = params->dbscan_min_points;
 
         // ---- DBSCAN split (dbscan_process) ----
-        DevBuf xyz, pcell, pbkt, bcnt, bstart, blist, ncnt, par, root, rnk, lab, ccnt, nob, nsh, tick;
+        DevBuf xyz, pcell, pbkt, bcnt, bstart, blist, ncnt, par, root, rnk, lab, ccnt, nob, nsh, tick, skey, sxyz, sidx;
+        skey.reserve(E * 8 + 8);  // bucket-ordered copies of the cell keys, points and indices
+        sxyz.reserve(E * 24 + 8);
+        sidx.reserve(E * 4 + 8);
         xyz.reserve(E * 24 + 8);
         pcell.reserve(E * 8 + 8);
         for (DevBuf *b : {&pbkt, &blist, &ncnt, &par, &root, &rnk, &lab}) b->reserve(E * 4 + 8);
@@ -1777,7 +1780,8 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
                                    N - nbig, dorder.as<int>() + nbig, tick.as<int>(),
                                       npoff.as<int64_t>(), pr, xyz.as<double>(), pcell.as<unsigned long long>(), pbkt.as<int>(),
                                       bcnt.as<int>(), bstart.as<int>(), blist.as<int>(), ncnt.as<int>(), par.as<int>(),
-                                      root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), nob.as<int>(), nsh.as<int>());
+                                      root.as<int>(), rnk.as<int>(), lab.as<int>(), ccnt.as<int>(), nob.as<int>(), nsh.as<int>(),
+                                      skey.as<unsigned long long>(), sxyz.as<double>(), sidx.as<int>());
             MC_HIP(hipGetLastError());
         }
         std::vector<int32_t> h_nob(N), h_base(N + 1, 0);

@@ -72,13 +72,33 @@ __device__ __forceinline__ void pp_block_minmax3(double mn[3], double mx[3], dou
 
 // DBSCAN of every node (utils/post_process.py:109): labels -> object index within the node
 // (class order: noise first when present, then clusters by smallest core point), object sizes.
+// the 27 cells around (cx, cy, cz) over the bucket-ordered copies (key, xyz, index): the loads of
+// one bucket are independent of each other, not a cell -> point -> coordinate chain
+template <typename Fn>
+__device__ __forceinline__ void pp_walk27(const BpCells &g, const unsigned long long *__restrict__ sk,
+                                          const double *__restrict__ sx, const int *__restrict__ si, int cx, int cy,
+                                          int cz, Fn &&fn)
+{
+    for (int z = cz - 1; z <= cz + 1; z++)
+        for (int y = cy - 1; y <= cy + 1; y++)
+            for (int x = cx - 1; x <= cx + 1; x++) {
+                if (x < 0 || y < 0 || z < 0 || x > g.cmax[0] || y > g.cmax[1] || z > g.cmax[2]) continue;
+                const unsigned long long key = pack3(x, y, z);
+                const unsigned bk = mod_mul(bp_hash3(x, y, z), g.nb);
+                const int k1 = g.bs[bk + 1];
+                for (int q = g.bs[bk]; q < k1; q++)
+                    if (sk[q] == key) fn(si[q], sx + 3 * static_cast<int64_t>(q));
+            }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_pp_dbscan(
     int N, const int *__restrict__ order, int *__restrict__ ticket, const int64_t *__restrict__ pt_off, PPDev pr,
     const double *__restrict__ xyz, unsigned long long *__restrict__ pcell, int *__restrict__ pbkt,
     int *__restrict__ bcnt, int *__restrict__ bstart, int *__restrict__ blist, int *__restrict__ ncnt,
     int *__restrict__ par, int *__restrict__ root, int *__restrict__ rnk, int *__restrict__ lab,
-    int *__restrict__ ccnt, int *__restrict__ nob, int *__restrict__ nsh)
+    int *__restrict__ ccnt, int *__restrict__ nob, int *__restrict__ nsh, unsigned long long *__restrict__ skey,
+    double *__restrict__ sxyz, int *__restrict__ sidx)
 {
     __shared__ double red[6 * (NT / 64)];
     __shared__ int ws[NT / 64];
@@ -143,9 +163,17 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
         }
         __syncthreads();
         // 4. counting-sort scatter (bucket counters return to zero)
+        unsigned long long *sk = skey + e0;
+        double *sx = sxyz + 3 * e0;
+        int *si = sidx + e0;
         for (int i = t; i < n; i += NT) {
             const int b = pb[i];
-            bl[bs[b] + atomicSub(&bc[b], 1) - 1] = i;
+            const int q = bs[b] + atomicSub(&bc[b], 1) - 1;
+            bl[q] = i;
+            sk[q] = pc[i];
+            si[q] = i;
+#pragma unroll
+            for (int c = 0; c < 3; c++) sx[3 * q + c] = P[3 * i + c];
         }
         __syncthreads();
         auto cell_of = [&](int i, int &x, int &y, int &z) { unpack3(pc[i], x, y, z); };
@@ -155,8 +183,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             cell_of(i, x, y, z);
             int cnt = 0;
             const double *pi = P + 3 * i;
-            for (int R = 0; R <= 1; R++)
-                bp_shell(g, x, y, z, R, [&](int j) { cnt += bp_d2(pi, P + 3 * j) < pr.eps2 ? 1 : 0; });
+            pp_walk27(g, sk, sx, si, x, y, z, [&](int, const double *pj) { cnt += bp_d2(pi, pj) < pr.eps2 ? 1 : 0; });
             nc[i] = cnt;
             if (n <= kPPLdsUF) s_par[i] = i;
             else pa[i] = i;
@@ -168,13 +195,12 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             int x, y, z;
             cell_of(i, x, y, z);
             const double *pi = P + 3 * i;
-            for (int R = 0; R <= 1; R++)
-                bp_shell(g, x, y, z, R, [&](int j) {
-                    if (j < i && nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) {
-                        if (n <= kPPLdsUF) uf_unite_s(s_par, i, j);
-                        else uf_unite(pa, i, j);
-                    }
-                });
+            pp_walk27(g, sk, sx, si, x, y, z, [&](int j, const double *pj) {
+                if (j < i && nc[j] >= pr.minpts && bp_d2(pi, pj) < pr.eps2) {
+                    if (n <= kPPLdsUF) uf_unite_s(s_par, i, j);
+                    else uf_unite(pa, i, j);
+                }
+            });
         }
         __syncthreads();
         // 7. clusters numbered by their smallest core point (Open3D seeds in index order)
@@ -208,10 +234,9 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
                 cell_of(i, x, y, z);
                 const double *pi = P + 3 * i;
                 int mr = INT_MAX;
-                for (int R = 0; R <= 1; R++)
-                    bp_shell(g, x, y, z, R, [&](int j) {
-                        if (nc[j] >= pr.minpts && bp_d2(pi, P + 3 * j) < pr.eps2) mr = min(mr, ro[j]);
-                    });
+                pp_walk27(g, sk, sx, si, x, y, z, [&](int j, const double *pj) {
+                    if (nc[j] >= pr.minpts && bp_d2(pi, pj) < pr.eps2) mr = min(mr, ro[j]);
+                });
                 l = mr == INT_MAX ? -1 : rk[mr];
             }
             lb[i] = l + 1;
