@@ -52,27 +52,80 @@ def log(*a):
 
 
 def graph_work(ctx, mask_pts, P, F):
-    """Per-launch algorithmic bytes / ops of the graph kernel groups."""
+    """Per-launch algorithmic work of every graph kernel group.
+
+    Returns {group: (bound, per_launch, model, alt)}: the primary model is SURVEY.md §8(d)'s
+    where it defines one (S2, S3: dense-equivalent bytes of the reference's point-in-mask
+    matrix; S4, S6: dense-equivalent int8 MFMA ops 2·N²·K), so a sparse kernel can exceed 1;
+    ``alt`` is the builder's minimal-bytes model of what the sparse kernel must touch."""
     gi = ctx.graph_info()
+    ci = ctx.cluster_info()
     M, nnz = gi.num_masks, len(mask_pts)
     FW = (F + 63) // 64
     deg = np.bincount(mask_pts, minlength=P).astype(np.int64)
     bnd = ctx.boundary(P).astype(bool)
     nb = ~bnd[mask_pts]
-    # S3: every mask reads its ids (4 B) + boundary flag (1 B); every non-boundary point its
-    # offsets (8 B) and list entries (4 B each); writes its contained row + flags.
-    s3_bytes = 8 * M + 5 * nnz + int(np.sum(8 + 4 * deg[mask_pts[nb]])) + 4 * gi.num_contained + 5 * M
-    # S2: read mask ids, write + sort point lists (r/w), offsets, boundary, point-frame bits
-    s2_bytes = 4 * nnz + 2 * 4 * nnz + 2 * 4 * nnz + 8 * P + P + 8 * P * FW
-    # S4: dense-equivalent observer GEMM VF·VFᵀ (construction.py:84) — 2·M²·F int8 ops
-    s4_ops = 2.0 * M * M * F
-    s7_bytes = 2 * 4 * nnz + 4 * int(ctx.cluster_info().num_object_points)
-    return {
-        "s2_point_lists": ("hbm", float(s2_bytes)),
-        "s3_masks": ("hbm", float(s3_bytes)),
-        "s4_observer_hist": ("mfma", s4_ops),
-        "s7_points": ("hbm", float(s7_bytes)),
-    }
+    nvalid = int(nb.sum())
+    nnzC = int(gi.num_contained)
+    T = int(ci.num_iterations)
+    N = ctx.level_sizes(T).astype(np.float64)
+    cap = ctx.level_caps(T).astype(np.float64)
+    w = {}
+    # S2 (§8(d)): 2·P·F + P·F/8 + 4·Σ|m|  |  alt: read ids, write + sort point lists, offsets,
+    # boundary, point-frame bits
+    w["s2_point_lists"] = ("hbm", float(2 * P * F + P * F / 8 + 4 * nnz), "SURVEY §8(d) S2 dense-equivalent bytes",
+                           float(4 * nnz + 16 * nnz + 9 * P + 8 * P * FW))
+    # S3 (§8(d)): 2·F·Σ|valid_m| + 4·Σ|m| + M·F/8  |  alt: ids + boundary flags of every mask point,
+    # offsets + list entries of every non-boundary point, contained rows + flags
+    w["s3_masks"] = ("hbm", float(2 * F * nvalid + 4 * nnz + M * F / 8), "SURVEY §8(d) S3 dense-equivalent bytes",
+                     float(8 * M + 5 * nnz + int(np.sum(8 + 4 * deg[mask_pts[nb]])) + 4 * nnzC + 5 * M))
+    # undo + S5: contained rows read twice and written once, VF rows, node arrays
+    w["s3_undo_s5"] = ("hbm", float(12 * nnzC + 16 * FW * M + 40 * M), "contained rows r/w, VF, node arrays", None)
+    # S4: observer GEMM VF·VFᵀ over all M masks (construction.py:84) as int8 MFMA ops
+    w["s4_observer_hist"] = ("mfma", 2.0 * M * M * F, "SURVEY §8(d) 2·M²·F dense-equivalent int8 ops", None)
+    if T:
+        # S6 per iteration t (§8(d)): 2·N_t²·(F+M) dense-equivalent int8 ops, averaged over the T launches
+        w["s6_pairs"] = ("mfma", float(np.sum(2.0 * N[:T] ** 2 * (F + M)) / T),
+                         "SURVEY §8(d) Σ_t 2·N_t²·(F+M) / T dense-equivalent int8 ops", None)
+        # components: parents read, roots / labels / level labels / member lists written, member
+        # counts; offsets of the next level
+        w["s6_components"] = ("hbm", float(np.sum(24 * N[:T] + 8 * N[1:T + 1]) / T),
+                              "24·N_t + 8·N_(t+1) bytes per iteration", None)
+        # merge: members' contained rows (<= cap_t slots) + VF rows read, new rows + owners + VF
+        # written, plus the next level's column lists (read, relabel, write) on all but the last
+        col = np.array([12.0 * nnzC if t + 1 < T else 0.0 for t in range(T)])
+        w["s6_merge"] = ("hbm", float(np.sum(4 * cap[:T] + (8 * FW + 4) * N[:T] + 8 * cap[1:T + 1]
+                                             + (8 * FW + 8) * N[1:T + 1] + col) / T),
+                         "4·cap_t + (8·FW+4)·N_t + 8·cap_(t+1) + (8·FW+8)·N_(t+1) + 12·nnzC bytes per iteration",
+                         None)
+        w["s6_columns"] = ("hbm", float(20 * cap[0]), "level-0 transpose: 20·nnzC0 bytes", None)
+    w["s7_points"] = ("hbm", float(2 * 4 * nnz + 4 * int(ci.num_object_points)), "8·nnz + 4·Σ|object points|", None)
+    return w
+
+
+def roofline_entry(w, avg_s, pmc_group=None):
+    """Roofline of one kernel group: algorithmic work per launch (w = graph_work / bp_work
+    entry) over its average launch duration avg_s; traffic = PMC HBM bytes per launch."""
+    bound, per_launch, model, alt = w
+    if bound == "hbm":
+        achieved, peak, unit = per_launch / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved, peak, unit = per_launch / avg_s / 1e12, INT8_MFMA_PEAK_TOPS, "TFLOP/s"
+    e = {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+         "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 5), "algorithmic_per_launch": per_launch, "model": model}
+    if bound == "mfma":
+        e["note"] = ("dense-equivalent int8 ops of the reference's fp32 GEMMs; the kernel is sparse (it never "
+                     "evaluates pairs with no shared contained mask), so frac can exceed 1 and says nothing "
+                     "about efficiency: see traffic_frac_hbm")
+    if alt is not None:
+        e["alt_model_bytes"] = alt
+        e["alt_frac"] = round(alt / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+    if pmc_group:
+        t = float(pmc_group["bytes_per_launch"])
+        e["traffic"] = round(t, 0)
+        e["traffic_gbs"] = round(t / avg_s / 1e9, 2)
+        e["traffic_frac_hbm"] = round(t / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+    return e
 
 
 def bp_work(ctx, F, H, W):
@@ -84,10 +137,10 @@ def bp_work(ctx, F, H, W):
     npx, nvox, nsor = int(st[:, 2].sum()), int(st[:, 3].sum()), int(st[:, 5].sum())
     nnbr = int(ctx.bp_info().num_mask_points)
     return {
-        "bp_pixels": ("hbm", float(5 * F * H * W + 4 * npx)),
-        "bp_voxel": ("hbm", float(8 * npx + 24 * nvox)),
-        "bp_denoise": ("hbm", float(24 * nvox + 12 * nsor)),
-        "bp_query": ("hbm", float(12 * nsor + 4 * nnbr)),
+        "bp_pixels": ("hbm", float(5 * F * H * W + 4 * npx), "5·F·H·W + 4·Σ mask pixels", None),
+        "bp_voxel": ("hbm", float(8 * npx + 24 * nvox), "8·Σ mask pixels + 24·Σ voxels", None),
+        "bp_denoise": ("hbm", float(24 * nvox + 12 * nsor), "24·Σ voxels + 12·Σ surviving points", None),
+        "bp_query": ("hbm", float(12 * nsor + 4 * nnbr), "12·Σ mask points + 4·Σ neighbour ids", None),
     }
 
 
@@ -408,14 +461,14 @@ def main():
     ctx.set_timing(True)
     runner.step()
     ctx.synchronize()
-    calib = {g: ctx.kernel_time(g)[0] for g in runner.groups}
+    calib = {g: ctx.kernel_time(g) for g in runner.groups}
     ctx.set_timing(False)
     work = runner.work()
-    dominant = max((g for g in calib if g in work), key=lambda g: calib[g])
-    log("calibration (ms):", json.dumps({k: round(v, 4) for k, v in calib.items()}), "dominant:", dominant)
+    dominant = max((g for g in calib if g in work), key=lambda g: calib[g][0])
+    log("calibration (ms):", json.dumps({k: round(v[0], 4) for k, v in calib.items()}), "dominant:", dominant)
 
     # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant
-    # group only (one event pair per step)
+    # group only (one event pair per launch of the group, on the context stream)
     ctx.reset_kernel_times()
     ctx.set_timing_filter(dominant)
     ctx.set_timing(True)
@@ -441,31 +494,38 @@ def main():
     value = total_pairs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    bound, per_launch = work[dominant]
-    avg_s = (dom_ms / max(dom_n, 1)) / 1e3
-    if bound == "hbm":
-        achieved = per_launch / avg_s / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
-    else:
-        achieved = per_launch / avg_s / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": INT8_MFMA_PEAK_TOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / INT8_MFMA_PEAK_TOPS, 4), "traffic": None}
+    # HBM bytes per launch of every kernel group from the committed rocprofv3 PMC passes of the
+    # same workload (scripts/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note in
+    # MI355X_MICROARCH.md)
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.variant}_{args.shape}.json")
+    pmc = json.load(open(pmc_path)).get("groups", {}) if os.path.exists(pmc_path) else {}
+    roof = roofline_entry(work[dominant], (dom_ms / max(dom_n, 1)) / 1e3, pmc.get(dominant))
     roof["kernel"] = dominant
-    roof["avg_launch_ms"] = round(avg_s * 1e3, 5)
-    roof["algorithmic_per_launch"] = per_launch
-    # HBM bytes per launch of the same kernel group from the committed rocprofv3 PMC passes
-    # (scripts/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md)
-    pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.variant}_{args.shape}.json")  # same workload only
-    if bound == "hbm" and os.path.exists(pmc_path):
-        g = json.load(open(pmc_path)).get("groups", {}).get(dominant)
-        if g:
-            roof["traffic"] = round(g["bytes_per_launch"], 0)
-            roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
+    roof["launches_timed"] = int(dom_n)
+    if pmc.get(dominant):
+        roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
+    stages = {}
+    for g, (ms, n) in calib.items():
+        if g in work and n:
+            e = roofline_entry(work[g], ms / n / 1e3, pmc.get(g))
+            stages[g] = {k: e[k] for k in ("bound", "achieved", "unit", "frac", "avg_launch_ms", "model")
+                         if k in e}
+            for k in ("alt_frac", "traffic_frac_hbm"):
+                if k in e:
+                    stages[g][k] = e[k]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames:
         cpu = runner.cpu_baseline()
+        ratio_path = os.path.join(REPO, "profiles", f"cpu_ratio_{args.shape}.json")
+        if os.path.exists(ratio_path) and args.variant == "g":
+            r = json.load(open(ratio_path))
+            cpu["reference_context"] = {
+                "source": os.path.relpath(ratio_path, REPO),
+                "note": "the reference's own S2-S6 (imported unmodified, Appendix B harness) and this C port "
+                        "on the same synthetic scene, both on the 8-core build container (scripts/cpu_ratio.py)",
+                "reference_s": r["reference_s"], "port_s_container": r["port_s"],
+                "port_threads_container": r["port_threads"], "reference_over_port": r["reference_over_port"]}
 
     if rank == 0:
         line = {
@@ -484,9 +544,10 @@ def main():
             "config": {"workload": runner.workload + f" M={gi.num_masks}", "variant": args.variant,
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
-                       "stage_ms": {k: round(v, 4) for k, v in calib.items()},
+                       "stage_ms": {k: round(v[0], 4) for k, v in calib.items()},
                        "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}"},
             "roofline": roof,
+            "stage_roofline": stages,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

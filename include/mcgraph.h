@@ -190,6 +190,9 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
 int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double connect_threshold);
 int mc_cluster_get_info(mc_ctx *ctx, mc_cluster_info *info);
 int mc_cluster_get_level_sizes(mc_ctx *ctx, int32_t *sizes /* num_iterations+1 */);
+/* contained-pool slots of every level (sum of the members' row lengths: the merge's row
+ * upper bounds), level 0 = nnz of the initial rows; used for the S6 byte models of bench.py */
+int mc_cluster_get_level_caps(mc_ctx *ctx, int32_t *caps /* num_iterations+1 */);
 int mc_cluster_get_partition(mc_ctx *ctx, int32_t iteration, int32_t *labels /* N_iteration */);
 int mc_cluster_get_edge_counts(mc_ctx *ctx, int64_t *edges /* num_iterations */);
 int mc_cluster_get_final_labels(mc_ctx *ctx, int32_t *labels /* N0: object of each level-0 node */);

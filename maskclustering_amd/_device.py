@@ -36,16 +36,28 @@ def as_numpy(x) -> np.ndarray:
     return np.asarray(x)
 
 
+def seg_u8(seg) -> np.ndarray:
+    """A segmentation image as uint8 (mask ids <= 255: mask_predict.py:102 writes uint8 PNGs).  Ids
+    outside [0, 255] would wrap and merge distinct masks, so they raise instead."""
+    a = as_numpy(seg)
+    if a.dtype == np.uint8:
+        return a
+    if a.size and (a.min() < 0 or a.max() > 255 or not np.issubdtype(a.dtype, np.integer)):
+        raise ValueError(f"segmentation ids must be integers in [0, 255] (uint8 mask images); got dtype {a.dtype} "
+                         f"range [{a.min()}, {a.max()}]")
+    return a.astype(np.uint8)
+
+
 def set_scene_points(scene_points) -> int:
     """Upload the scene points as float32 (construction.py:37) once per distinct array."""
     global _points_key
     ctx = context()
     if hasattr(scene_points, "data_ptr") and getattr(scene_points, "is_cuda", False) \
             and scene_points.dtype.__str__() == "torch.float32" and scene_points.is_contiguous():
-        key = ("dev", scene_points.data_ptr(), tuple(scene_points.shape), scene_points._version)
-        if key != _points_key:
-            ctx.set_points(device_ptr=scene_points.data_ptr(), num_points=int(scene_points.shape[0]))
-            _points_key = key
+        # always copied (device to device, cheap): a new tensor can reuse a freed tensor's block
+        # with the same shape and version, so the address is no key
+        ctx.set_points(device_ptr=scene_points.data_ptr(), num_points=int(scene_points.shape[0]))
+        _points_key = None
         return int(scene_points.shape[0])
     pts = np.ascontiguousarray(as_numpy(scene_points), dtype=np.float32).reshape(-1, 3)
     key = ("host", pts.shape, hash(pts.tobytes()))

@@ -30,7 +30,7 @@ EXPORTED = [
     "mc_graph_get_visible_frame_bits", "mc_graph_get_contained", "mc_graph_get_undersegment",
     "mc_graph_get_nodes0", "mc_graph_get_observer_hist", "mc_graph_get_thresholds", "mc_observer_thresholds",
     "mc_nodes_set",
-    "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_partition",
+    "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_level_caps", "mc_cluster_get_partition",
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
@@ -142,6 +142,7 @@ def load():
         "mc_cluster_run": (ctypes.c_int, [vp, vp, i32, dbl]),
         "mc_cluster_get_info": (ctypes.c_int, [vp, P(ClusterInfo)]),
         "mc_cluster_get_level_sizes": (ctypes.c_int, [vp, vp]),
+        "mc_cluster_get_level_caps": (ctypes.c_int, [vp, vp]),
         "mc_cluster_get_partition": (ctypes.c_int, [vp, i32, vp]),
         "mc_cluster_get_edge_counts": (ctypes.c_int, [vp, vp]),
         "mc_cluster_get_final_labels": (ctypes.c_int, [vp, vp]),
@@ -337,6 +338,11 @@ class Context:
     def level_sizes(self, n_iter):
         out = np.zeros(n_iter + 1, np.int32)
         self._check(self.L.mc_cluster_get_level_sizes(self.h, _ptr(out)))
+        return out
+
+    def level_caps(self, n_iter):
+        out = np.zeros(n_iter + 1, np.int32)
+        self._check(self.L.mc_cluster_get_level_caps(self.h, _ptr(out)))
         return out
 
     def partition(self, t, n):

@@ -1090,6 +1090,15 @@ int mc_cluster_get_level_sizes(mc_ctx *ctx, int32_t *sizes)
     });
 }
 
+int mc_cluster_get_level_caps(mc_ctx *ctx, int32_t *caps)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster, MC_ERR_STATE, "no clustering result");
+        MC_HIP(hipMemcpyAsync(caps, ctx->d_cap.ptr, (ctx->n_iter + 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
 int mc_cluster_get_partition(mc_ctx *ctx, int32_t iteration, int32_t *labels)
 {
     return guarded(ctx, [&] {
@@ -1699,6 +1708,22 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
             return node_pt_off[a + 1] - node_pt_off[a] > node_pt_off[b + 1] - node_pt_off[b];
         });
         for (int64_t i = 0; i < E; i++) MC_REQUIRE(node_pts[i] >= 0 && node_pts[i] < P, MC_ERR_INVALID, "node point out of range");
+        {  // the DBSCAN grid packs cell coordinates in 21 bits per axis (pack3): every node's extent
+           // must stay below 2^21 cells of 1.01 eps, or neighbours would be missed silently
+            const double ce = params->dbscan_eps * 1.01;
+            for (int k = 0; k < N; k++) {
+                double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+                for (int64_t i = node_pt_off[k]; i < node_pt_off[k + 1]; i++)
+                    for (int c = 0; c < 3; c++) {
+                        const double v = scene_xyz[3 * static_cast<int64_t>(node_pts[i]) + c];
+                        mn[c] = std::min(mn[c], v);
+                        mx[c] = std::max(mx[c], v);
+                    }
+                for (int c = 0; c < 3; c++)
+                    MC_REQUIRE(!(mx[c] >= mn[c]) || std::floor((mx[c] - mn[c]) / ce) < double((1 << 21) - 1),
+                               MC_ERR_UNSUPPORTED, "a node spans more than 2^21 DBSCAN cells per axis (eps too small)");
+            }
+        }
         for (int64_t i = 0; i < MP; i++) MC_REQUIRE(mask_pts[i] >= 0 && mask_pts[i] < P, MC_ERR_INVALID, "mask point out of range");
 
         hipStream_t s = ctx->stream;
@@ -1875,10 +1900,11 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
             MC_HIP(hipMemsetAsync(inter.ptr, 0, static_cast<size_t>(Kk) * Kk * 4, s));
             hipLaunchKernelGGL(mc::k_pp_pairs, grid_for(P), dim3(256), 0, s, P, sl, pcnt.as<int>(), plist.as<int>(), Kk,
                                inter.as<int>());
-            constexpr int kCap = 1 << 16;
+            int kCap = 1 << 16;  // non-zero decisions handled by the host pass; more: k_pp_greedy
+            if (const char *e = getenv("MC_PP_GREEDY_CAP")) kCap = std::max(0, atoi(e));  // tests force the device pass
             DevBuf nl, lst;
             nl.reserve(8);
-            lst.reserve(static_cast<size_t>(kCap) * sizeof(int2));
+            lst.reserve(static_cast<size_t>(std::max(kCap, 1)) * sizeof(int2));
             MC_HIP(hipMemsetAsync(nl.ptr, 0, 4, s));
             hipLaunchKernelGGL(mc::k_pp_decide, grid_for(static_cast<int64_t>(Kk) * Kk), dim3(256), 0, s, Kk, pr,
                                dbox.as<double>(), dlen.as<int>(), inter.as<int>(), dec.as<unsigned char>(), kCap,
@@ -1911,6 +1937,7 @@ int mc_pp_run(mc_ctx *ctx, const mc_pp_params *params, int64_t num_points, int32
                 hipLaunchKernelGGL(mc::k_pp_greedy, dim3(1), dim3(1024), 0, s, Kk, dec.as<unsigned char>(), inv.as<unsigned char>());
                 MC_HIP(hipGetLastError());
                 MC_HIP(hipMemcpyAsync(h_inv.data(), inv.ptr, Kk, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipStreamSynchronize(s));  // h_inv is pageable host memory read just below
             }
         }
         // ---- results ----

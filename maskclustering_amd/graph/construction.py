@@ -53,7 +53,7 @@ def _stack_frames(frame_list, dataset):
     depth, seg, K, T = [], [], [], []
     for frame_id in frame_list:
         depth.append(np.asarray(dataset.get_depth(frame_id), np.float32))
-        seg.append(_device.as_numpy(dataset.get_segmentation(frame_id, align_with_depth=True)).astype(np.uint8))
+        seg.append(_device.seg_u8(dataset.get_segmentation(frame_id, align_with_depth=True)))
         K.append(_device.intrinsics_tuple(dataset.get_intrinsics(frame_id)))
         T.append(np.asarray(dataset.get_extrinsic(frame_id), np.float64).reshape(4, 4))
     return np.stack(depth), np.stack(seg), np.stack(K), np.stack(T)

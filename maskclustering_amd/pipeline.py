@@ -47,7 +47,9 @@ class GraphRun:
         self.cluster(view_consensus_threshold)
 
     # ---- results --------------------------------------------------------------------
-    def canonical(self) -> dict:
+    def canonical(self, dense: bool = True) -> dict:
+        """dense=False skips the point-in-mask and point-frame matrices (P×F: 3 GB / 0.2 GB at
+        C3), for the large-scene parity tests."""
         c = self.ctx
         gi = c.graph_info()
         P, F, M = gi.num_points, gi.num_frames, gi.num_masks
@@ -57,10 +59,12 @@ class GraphRun:
         out["gl_col"], out["gl_label"] = self.mask_col[gidx], self.mask_label[gidx]
         bnd = c.boundary(P)
         out["boundary"] = np.nonzero(bnd)[0].astype(np.int32)
-        pim = c.point_in_mask(P, F)
-        nzp, nzc = np.nonzero(pim)
-        out["pim_p"], out["pim_c"], out["pim_v"] = nzp.astype(np.int32), nzc.astype(np.int32), pim[nzp, nzc].astype(np.int32)
-        out["pfm_bits"] = np.packbits(bits_to_bool(c.point_frame_bits(P, F), F), axis=1)
+        if dense:
+            pim = c.point_in_mask(P, F)
+            nzp, nzc = np.nonzero(pim)
+            out["pim_p"], out["pim_c"], out["pim_v"] = nzp.astype(np.int32), nzc.astype(np.int32), \
+                pim[nzp, nzc].astype(np.int32)
+            out["pfm_bits"] = np.packbits(bits_to_bool(c.point_frame_bits(P, F), F), axis=1)
         out["vf_bits"] = np.packbits(bits_to_bool(c.visible_frame_bits(M, F), F), axis=1)
         off, idx = c.contained(M, gi.num_contained)
         rows = np.repeat(np.arange(M, dtype=np.int32), np.diff(off))

@@ -48,16 +48,19 @@ FRAME_SHAPES = {
     # tests: seconds on the CPU oracle
     "tiny": dict(num_objects=10, num_frames=8, H=60, W=80, length=2.5, spacing=0.02, size=(0.12, 0.3)),
     "small": dict(num_objects=30, num_frames=16, H=120, W=160, length=5.0, spacing=0.02, size=(0.12, 0.3)),
-    # ScanNet-shaped (BASELINE configs[1]): 640x480, ~250 frames, ~60 masks per frame
-    "c2": dict(num_objects=600, num_frames=250, H=480, W=640, length=50.0, spacing=0.025, size=(0.1, 0.3)),
+    # ScanNet-shaped (BASELINE configs[1]): 640x480, 250 frames, ~240k points, ~60 masks per frame (~15k)
+    "c2": dict(num_objects=760, num_frames=250, H=480, W=640, length=50.0, spacing=0.025, size=(0.1, 0.3),
+               frame_rng=True),
+    # the round-1 ScanNet-shaped stand-in (P 194k, M 11.8k), kept for comparisons with its profiles
+    "c2_r1": dict(num_objects=600, num_frames=250, H=480, W=640, length=50.0, spacing=0.025, size=(0.1, 0.3)),
+    # ScanNet++-shaped (BASELINE configs[2], dataset/scannetpp.py:126): 1920x1440, 1500 frames, ~1M points,
+    # ~80k masks
+    "c3": dict(num_objects=3100, num_frames=1500, H=1440, W=1920, length=230.0, spacing=0.025, size=(0.1, 0.3),
+               frame_rng=True),
 }
 
 
-def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_split=0.06, p_merge=0.04,
-                device="cpu", yaw=0.12):
-    import torch
-
-    rng = np.random.default_rng(seed)
+def _scene(num_objects, length, spacing, size, rng):
     K = int(num_objects)
     lo_s, hi_s = size
     ext = rng.uniform(lo_s, hi_s, size=(K, 3))
@@ -66,7 +69,6 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
     centers = np.stack([cx, cy, ext[:, 2] / 2], axis=1)
     bmin = centers - ext / 2
     bmax = centers + ext / 2
-
     # ---- scene points: jittered grid on the five visible faces of every box ----
     pts = []
     for o in range(K):
@@ -89,10 +91,10 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
     scene = np.concatenate(pts, axis=0)
     # mesh-vertex-like order: sorted along the trajectory axis in coarse slabs
     order = np.lexsort((scene[:, 1], np.floor(scene[:, 0] / 0.25)))
-    scene = scene[order]
+    return scene[order], cx, bmin, bmax
 
-    # ---- cameras -------------------------------------------------------------------
-    F = int(num_frames)
+
+def _cameras(F, H, W, length, yaw):
     fx = fy = 577.87 * W / 640.0
     ccx, ccy = (W - 1) / 2.0, (H - 1) / 2.0
     intr = np.tile(np.array([fx, fy, ccx, ccy]), (F, 1))
@@ -106,6 +108,25 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
         poses[f, :3, 0], poses[f, :3, 1], poses[f, :3, 2] = right, down, fwd
         poses[f, :3, 3] = [length * (f + 0.5) / F, -2.0, 1.3]
         poses[f, 3, 3] = 1.0
+    return intr, poses
+
+
+def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_split=0.06, p_merge=0.04,
+                device="cpu", yaw=0.12, frame_rng=False, frames=None, out="numpy"):
+    """Render the scene.  frames: the frame indices to render (default all; the scene points,
+    intrinsics and poses always cover every frame).  frame_rng: the split / merge noise of frame f
+    is drawn from its own generator (seed, f), so that any frame slice renders the same frames as
+    the whole scene (the frame-sharded bench renders only each rank's slice).  out="torch": depth
+    and seg stay on ``device`` as torch tensors (no host copy; the C3 frames are 21 GB)."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    K = int(num_objects)
+    scene, cx, bmin, bmax = _scene(num_objects, length, spacing, size, rng)
+    F = int(num_frames)
+    intr, poses = _cameras(F, H, W, length, yaw)
+    fx, fy, ccx, ccy = intr[0]
+    sel = list(range(F)) if frames is None else list(frames)
 
     dev = torch.device(device)
     tb0 = torch.tensor(bmin, dtype=torch.float64, device=dev)
@@ -114,9 +135,15 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
     v = torch.arange(H, dtype=torch.float64, device=dev)
     vv, uu = torch.meshgrid(v, u, indexing="ij")
     dirs_cam = torch.stack([(uu - ccx) / fx, (vv - ccy) / fy, torch.ones_like(uu)], dim=-1).reshape(-1, 3)
-    depth = np.zeros((F, H, W), np.float32)
-    seg = np.zeros((F, H, W), np.uint8)
-    for f in range(F):
+    ucol = torch.arange(W, device=dev)[None, :]
+    if out == "torch":
+        depth = torch.zeros((len(sel), H, W), dtype=torch.float32, device=dev)
+        seg = torch.zeros((len(sel), H, W), dtype=torch.uint8, device=dev)
+    else:
+        depth = np.zeros((len(sel), H, W), np.float32)
+        seg = np.zeros((len(sel), H, W), np.uint8)
+    chunk = 32 if H * W <= 400_000 else 8
+    for i, f in enumerate(sel):
         R = torch.tensor(poses[f, :3, :3], dtype=torch.float64, device=dev)
         c = torch.tensor(poses[f, :3, 3], dtype=torch.float64, device=dev)
         d = dirs_cam @ R.T                       # world direction per unit camera depth
@@ -129,8 +156,8 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
             tw = torch.where(d[:, 1] > 1e-9, (3.2 - c[1]) / d[:, 1], torch.full_like(best_t, float("inf")))
             bg = torch.minimum(tf, tw)
             inv = 1.0 / torch.where(d.abs() < 1e-12, torch.full_like(d, 1e-12), d)
-            for k0 in range(0, len(near), 32):
-                idx = torch.as_tensor(near[k0:k0 + 32], device=dev)
+            for k0 in range(0, len(near), chunk):
+                idx = torch.as_tensor(near[k0:k0 + chunk], device=dev)
                 t0 = (tb0[idx][None] - c) * inv[:, None]     # [R, B, 3]
                 t1 = (tb1[idx][None] - c) * inv[:, None]
                 tn = torch.minimum(t0, t1).amax(-1)
@@ -142,38 +169,45 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
                 best_t = torch.where(better, tmin, best_t)
                 best_o = torch.where(better, idx[arg], best_o)
             use_obj = best_t < bg
-            t = torch.where(use_obj, best_t, bg)
-            obj = torch.where(use_obj, best_o, torch.full_like(best_o, -1))
-        t = t.cpu().numpy().reshape(H, W)
-        obj = obj.cpu().numpy().reshape(H, W)
-        dq = np.where(np.isfinite(t) & (t < 60.0), np.round(t * 1000.0), 0.0).astype(np.uint16)
-        depth[f] = dq.astype(np.float32) / np.float32(1000.0)
-        # per-frame instance ids: visible objects in object order, with split / merge noise
-        vis = np.unique(obj[obj >= 0])
-        lab = np.zeros(K + 1, np.int64)
-        nxt, i = 1, 0
-        split_of = {}
-        while i < len(vis) and nxt < 255:
-            o = vis[i]
-            lab[o + 1] = nxt
-            if rng.random() < p_merge and i + 1 < len(vis):
-                lab[vis[i + 1] + 1] = nxt
-                i += 1
-            elif rng.random() < p_split and nxt + 1 < 255:
-                split_of[o] = nxt + 1
+            t = torch.where(use_obj, best_t, bg).reshape(H, W)
+            obj = torch.where(use_obj, best_o, torch.full_like(best_o, -1)).reshape(H, W)
+            # depth quantised like ScanNet's uint16 millimetres (round half to even, as numpy)
+            dq = torch.where(torch.isfinite(t) & (t < 60.0), torch.round(t * 1000.0), torch.zeros_like(t))
+            dz = dq.to(torch.int32).to(torch.float32) / np.float32(1000.0)
+            # per-frame instance ids: visible objects in object order, with split / merge noise
+            vis = torch.unique(obj[obj >= 0]).cpu().numpy()
+            r = np.random.default_rng([seed, f]) if frame_rng else rng
+            lab = np.zeros(K + 1, np.int64)
+            nxt, j = 1, 0
+            split_of = {}
+            while j < len(vis) and nxt < 255:
+                o = vis[j]
+                lab[o + 1] = nxt
+                if r.random() < p_merge and j + 1 < len(vis):
+                    lab[vis[j + 1] + 1] = nxt
+                    j += 1
+                elif r.random() < p_split and nxt + 1 < 255:
+                    split_of[o] = nxt + 1
+                    nxt += 1
                 nxt += 1
-            nxt += 1
-            i += 1
-        s = lab[obj + 1]
-        for o, second in split_of.items():
-            m = obj == o
-            cols = np.nonzero(m.any(axis=0))[0]
-            if len(cols) >= 2:
-                mid = cols[len(cols) // 2]
-                s[m & (np.arange(W)[None, :] >= mid)] = second
-        seg[f] = s.astype(np.uint8)
-    return SceneFrames(scene, depth, seg, intr, poses,
-                       meta=dict(seed=seed, num_objects=K, length=length, spacing=spacing))
+                j += 1
+            s_ = torch.as_tensor(lab, device=dev)[obj + 1]
+            for o, second in split_of.items():
+                m = obj == int(o)
+                cols = torch.nonzero(m.any(dim=0)).flatten()
+                if len(cols) >= 2:
+                    mid = int(cols[len(cols) // 2])
+                    s_[m & (ucol >= mid)] = second
+            s_ = s_.to(torch.uint8)
+        if out == "torch":
+            depth[i] = dz
+            seg[i] = s_
+        else:
+            depth[i] = dz.cpu().numpy()
+            seg[i] = s_.cpu().numpy()
+    return SceneFrames(scene, depth, seg, intr[sel], poses[sel],
+                       meta=dict(seed=seed, num_objects=K, length=length, spacing=spacing, frames=sel,
+                                 num_frames_total=F))
 
 
 def make_frames_shape(name: str, seed: int = 0, device: str = "cpu", **kw) -> SceneFrames:

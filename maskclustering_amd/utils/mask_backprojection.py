@@ -73,7 +73,7 @@ def turn_mask_to_point(dataset, scene_points, mask_image, frame_id):
     if np.sum(np.isinf(T)) > 0:
         return {}, [], set()
     depth = np.asarray(dataset.get_depth(frame_id), np.float32)
-    seg = _device.as_numpy(mask_image).astype(np.uint8, copy=False).reshape(depth.shape)
+    seg = _device.seg_u8(mask_image).reshape(depth.shape)
     _, lab, off, pts = _run_frames(scene_points, depth[None], seg[None], K[None], T[None])
     if len(lab) == 0:
         return {}, [], []

@@ -135,6 +135,19 @@ def lib():
         L.orc_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p, ctypes.c_int, _f32p,
                                   ctypes.c_double, _i32p, _i32p, _i32p, _u8p, _u8p]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orcs_s2.restype = ctypes.c_int
+        L.orcs_s2.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _i32p, _i64p, _i32p, _u8p, _u8p, _i64p, _i32p]
+        L.orcs_s3.restype = ctypes.c_int
+        L.orcs_s3.argtypes = [ctypes.c_int, _i32p, _i32p, _i64p, _i32p, _u8p, _i32p, _u8p, _i64p, _i32p,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, _i32p, _i32p, _i32p,
+                              _u8p]
+        L.orcs_undo.restype = None
+        L.orcs_undo.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i32p, _u8p]
+        L.orcs_observer_hist.restype = None
+        L.orcs_observer_hist.argtypes = [ctypes.c_int, ctypes.c_int, _u64p, _u64p, ctypes.c_int]
+        L.orcs_cluster.restype = ctypes.c_int
+        L.orcs_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _i64p, _i32p, ctypes.c_int, _f32p,
+                                   ctypes.c_double, _i32p, _i32p, _i32p, _i64p, _u64p, _i64p, _i32p]
         _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
         L.orc_s1_frame.restype = ctypes.c_int
         L.orc_s1_frame.argtypes = [ctypes.c_int64, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _u8p, _f64p, _f64p,
@@ -276,3 +289,141 @@ def run(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     out["obj_son_off"] = so
     out["obj_son_idx"] = np.concatenate(sons).astype(np.int32) if K else np.zeros(0, np.int32)
     return out
+
+
+def _bits_rows(cols_per_row, n_rows, F):
+    """rows of frame indices -> (n_rows, ceil(F/64)) uint64 little-endian bits"""
+    FW = max((F + 63) // 64, 1)
+    out = np.zeros((max(n_rows, 1), FW), np.uint64)
+    for r, cs in enumerate(cols_per_row):
+        if len(cs):
+            np.bitwise_or.at(out[r], np.asarray(cs) // 64, np.left_shift(np.uint64(1), (np.asarray(cs) % 64).astype(np.uint64)))
+    return out[:n_rows]
+
+
+def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
+               mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
+               contained_threshold, timings: dict | None = None):
+    """Whole S2-S6 path on the CPU with sparse rows (oracle/graph_sparse.c): the golden-fixture
+    dictionary of run() without the dense point-in-mask entries (pim_*), for C3/C4-sized scenes."""
+    L = lib()
+    P, F = int(num_points), int(num_frames)
+    col = np.ascontiguousarray(mask_col, np.int32)
+    label = np.ascontiguousarray(mask_label, np.int32)
+    off = np.ascontiguousarray(mask_off, np.int64)
+    pts = np.ascontiguousarray(mask_pts, np.int32)
+    M_in = len(col)
+    t0 = time.perf_counter()
+    kept = np.zeros(max(M_in, 1), np.uint8)
+    bnd = np.zeros(max(P, 1), np.uint8)
+    pt_off = np.zeros(P + 1, np.int64)
+    pt_ent = np.zeros(max(int(off[-1]) if M_in else 0, 1), np.int32)
+    M = L.orcs_s2(P, F, M_in, col, off, pts, kept, bnd, pt_off, pt_ent)
+    kept = kept[:M_in]
+    gidx = np.where(kept > 0, np.cumsum(kept) - 1, -1).astype(np.int32)
+    t1 = time.perf_counter()
+    Fc = max(F, 1)
+    ct_frame = np.zeros(max(M, 1) * Fc, np.int32)
+    ct_tgt = np.zeros(max(M, 1) * Fc, np.int32)
+    ct_len = np.zeros(max(M, 1), np.int32)
+    useg = np.zeros(max(M, 1), np.uint8)
+    L.orcs_s3(M_in, col, label, off, pts, np.ascontiguousarray(kept), gidx, bnd, pt_off, pt_ent,
+              float(mask_visible_threshold), float(contained_threshold), float(undersegment_filter_threshold), Fc,
+              ct_frame, ct_tgt, ct_len, useg)
+    L.orcs_undo(M, Fc, ct_frame, ct_tgt, ct_len, useg)
+    ct_frame, ct_tgt = ct_frame.reshape(-1, Fc), ct_tgt.reshape(-1, Fc)
+    ct_len, useg = ct_len[:M], useg[:M]
+    FW = max((F + 63) // 64, 1)
+    rr = np.repeat(np.arange(M), ct_len)
+    cc = np.concatenate([ct_frame[r, :ct_len[r]] for r in range(M)]) if M else np.zeros(0, np.int32)
+    tt = np.concatenate([ct_tgt[r, :ct_len[r]] for r in range(M)]) if M else np.zeros(0, np.int32)
+    vfw = np.zeros((max(M, 1), FW), np.uint64)
+    if len(rr):
+        np.bitwise_or.at(vfw, (rr, cc // 64), np.left_shift(np.uint64(1), (cc % 64).astype(np.uint64)))
+    vfw = np.ascontiguousarray(vfw[:M] if M else vfw)
+    t2 = time.perf_counter()
+    hist = np.zeros(F + 1, np.uint64)
+    L.orcs_observer_hist(M, FW, vfw, hist, F)
+    thr, thr_isint = thresholds_from_hist(hist)
+    t3 = time.perf_counter()
+    if thr is None:
+        raise IndexError("no positive observer count (np.percentile of an empty array)")
+    node0 = np.nonzero(useg == 0)[0].astype(np.int32)
+    order = np.lexsort((tt, rr))
+    rr_s, tt_s = rr[order], tt[order]
+    c_off_all = np.zeros(M + 1, np.int64)
+    np.cumsum(ct_len, out=c_off_all[1:])
+    lens0 = ct_len[node0].astype(np.int64)
+    c_off0 = np.zeros(len(node0) + 1, np.int64)
+    np.cumsum(lens0, out=c_off0[1:])
+    c_idx0 = np.concatenate([tt_s[c_off_all[g]:c_off_all[g + 1]] for g in node0]).astype(np.int32) \
+        if len(node0) and c_off0[-1] else np.zeros(1, np.int32)
+    N0 = len(node0)
+    T = len(thr)
+    labels = np.full((max(T, 1), max(N0, 1)), -1, np.int32)
+    sizes = np.zeros(T + 1, np.int32)
+    final = np.zeros(max(N0, 1), np.int32)
+    edges = np.zeros(max(T, 1), np.int64)
+    vf_out = np.zeros((max(N0, 1), FW), np.uint64)
+    co_out = np.zeros(max(N0, 1) + 1, np.int64)
+    ci_out = np.zeros(max(int(c_off0[-1]), 1), np.int32)
+    t4 = time.perf_counter()
+    K = L.orcs_cluster(N0, FW, M, np.ascontiguousarray(vfw[node0]) if N0 else np.zeros((1, FW), np.uint64), c_off0,
+                       np.ascontiguousarray(c_idx0), T, np.ascontiguousarray(thr, np.float32),
+                       float(view_consensus_threshold), labels, sizes, final, edges, vf_out, co_out, ci_out)
+    t5 = time.perf_counter()
+    if timings is not None:
+        timings.update(s2=t1 - t0, s3=t2 - t1, s4=t3 - t2, s6=t5 - t4,
+                       pairs=int(sum(int(s) ** 2 for s in sizes[:-1])) if T else 0, threads=L.orc_num_threads())
+    out = {}
+    keep_idx = np.nonzero(kept)[0]
+    out["gl_col"], out["gl_label"] = col[keep_idx].copy(), label[keep_idx].copy()
+    out["boundary"] = np.nonzero(bnd[:P])[0].astype(np.int32)
+    out["vf_bits"] = np.packbits(_bits_to_bool(vfw, F), axis=1) if M else np.zeros((0, (F + 7) // 8), np.uint8)
+    out["c_row"], out["c_col"] = rr_s.astype(np.int32), tt_s.astype(np.int32)
+    out["undersegment"] = np.nonzero(useg)[0].astype(np.int32)
+    out["thr_value"], out["thr_is_int"] = thr, thr_isint
+    out["node0_g"] = node0
+    out["observer_hist"] = hist
+    out["num_iters"] = np.array(T, np.int32)
+    out["level_sizes"] = sizes
+    out["edge_counts"] = edges[:T].copy()
+    for t in range(T):
+        out[f"part_{t}"] = labels[t, :sizes[t]].copy()
+    fin = final[:N0]
+    order = np.argsort(fin, kind="stable")
+    mo = np.zeros(K + 1, np.int64)
+    np.cumsum(np.bincount(fin, minlength=K), out=mo[1:])
+    out["obj_mask_off"], out["obj_mask_idx"] = mo, node0[order].astype(np.int32)
+    # object points: union of the member masks' point sets (node.py:35), ascending
+    goff = np.zeros(M + 1, np.int64)
+    np.cumsum((off[1:] - off[:-1])[keep_idx], out=goff[1:])
+    obj_of_g = np.full(M, -1, np.int64)
+    obj_of_g[node0] = fin
+    gl_pts = np.concatenate([pts[off[g]:off[g + 1]] for g in keep_idx]).astype(np.int64) if M else np.zeros(0, np.int64)
+    og = np.repeat(obj_of_g, np.diff(goff))
+    sel = og >= 0
+    key = np.unique(og[sel] * max(P, 1) + gl_pts[sel])
+    ko = key // max(P, 1)
+    po = np.zeros(K + 1, np.int64)
+    np.cumsum(np.bincount(ko, minlength=K), out=po[1:])
+    out["obj_pt_off"], out["obj_pt_idx"] = po, (key % max(P, 1)).astype(np.int32)
+    out["obj_vf_bits"] = np.packbits(_bits_to_bool(vf_out[:K], F), axis=1) if K else np.zeros((0, (F + 7) // 8), np.uint8)
+    out["obj_c_off"], out["obj_c_idx"] = co_out[:K + 1].copy(), ci_out[:co_out[K]].copy()
+    out["obj_node_info"] = np.array([(T, k) if T else (0, k) for k in range(K)], np.int32).reshape(-1, 2)
+    if T:
+        last = labels[T - 1, :sizes[T - 1]]
+        so = np.zeros(K + 1, np.int64)
+        np.cumsum(np.bincount(last, minlength=K), out=so[1:])
+        out["obj_son_off"], out["obj_son_idx"] = so, np.argsort(last, kind="stable").astype(np.int32)
+    else:
+        out["obj_son_off"], out["obj_son_idx"] = np.zeros(K + 1, np.int64), np.zeros(0, np.int32)
+    return out
+
+
+def _bits_to_bool(words, n):
+    words = np.ascontiguousarray(words, dtype="<u8")
+    if words.size == 0:
+        return np.zeros((words.shape[0], n), bool)
+    b = np.unpackbits(words.view(np.uint8).reshape(words.shape[0], -1), axis=1, bitorder="little")
+    return b[:, :n].astype(bool)

@@ -13,16 +13,24 @@ import json
 import os
 import sys
 
-# kernel-name prefix -> timed group of mc_api.hip (TimedScope names)
+# timed group of mc_api.hip (TimedScope names) -> (kernel-name prefixes, anchor prefixes): a group
+# launch is one launch of an anchor kernel (TimedScope count), and its bytes are the total bytes of
+# all the group's kernels over the anchor launches
 GROUPS = {
-    "s3_masks": ["mc::k_s3_masks"],
-    "s2_point_lists": ["mc::k_s2_degree", "mc::k_s2_scatter", "mc::k_s2_points", "mc::k_scan_reduce", "mc::k_scan_down"],
-    "s4_observer_hist": ["mc::k_s4_hist", "mc::k_s4_thresholds"],
-    "s7_points": ["mc::k7"],
-    "s6_pairs": ["mc::k6_pairs"],
-    "bp_voxel": ["mc::k_bp_voxel"],
-    "bp_denoise": ["mc::k_bp_denoise"],
-    "bp_query": ["mc::k_bp_query"],
+    "s3_masks": (["mc::k_s3_masks"], ["mc::k_s3_masks<1>"]),
+    "s2_point_lists": (["mc::k_s2_degree", "mc::k_s2_scatter", "mc::k_s2_points", "mc::k_scan_reduce",
+                        "mc::k_scan_down"], ["mc::k_s2_degree"]),
+    "s3_undo_s5": (["mc::k_s3_undo", "mc::k_s5_nodes"], ["mc::k_s5_nodes"]),
+    "s4_observer_hist": (["mc::k_s4_hist", "mc::k_s4_ranges", "mc::k_s4_thresholds"], ["mc::k_s4_thresholds"]),
+    "s6_columns": (["mc::k6_colcount", "mc::k6_colscatter", "mc::k6_colupdate"], ["mc::k6_colcount"]),
+    "s6_pairs": (["mc::k6_pairs"], ["mc::k6_pairs"]),
+    "s6_components": (["mc::k6_components", "mc::k6_compress", "mc::k6_relabel", "mc::k6_memscatter"],
+                      ["mc::k6_components", "mc::k6_compress"]),
+    "s6_merge": (["mc::k6_merge"], ["mc::k6_merge"]),
+    "s7_points": (["mc::k7"], ["mc::k7_words", "mc::k7_count"]),
+    "bp_voxel": (["mc::k_bp_voxel"], ["mc::k_bp_voxel"]),
+    "bp_denoise": (["mc::k_bp_denoise", "mc::k_bp_classify"], ["mc::k_bp_classify"]),
+    "bp_query": (["mc::k_bp_query", "mc::k_bp_keepflags", "mc::k_bp_emit"], ["mc::k_bp_query", "mc::k_bp_emit"]),
 }
 
 
@@ -45,13 +53,14 @@ def main():
         f, w = fetch.get(k, []), write.get(k, [])
         res["kernels"][k] = {"launches": max(len(f), len(w)),
                              "fetch_kb_avg": sum(f) / max(len(f), 1), "write_kb_avg": sum(w) / max(len(w), 1)}
-    for g, prefixes in GROUPS.items():
+    for g, (prefixes, anchors) in GROUPS.items():
         ks = [k for k in res["kernels"] if any(k.startswith(p) for p in prefixes)]
-        if not ks:
+        n = sum(res["kernels"][k]["launches"] for k in res["kernels"] if any(k.startswith(p) for p in anchors))
+        if not ks or not n:
             continue
-        # one group launch = one launch of each of its kernels (per-kernel averages summed)
-        b = sum(2 * res["kernels"][k]["fetch_kb_avg"] * 1024 + res["kernels"][k]["write_kb_avg"] * 1024 for k in ks)
-        res["groups"][g] = {"bytes_per_launch": b, "kernels": ks}
+        kk = res["kernels"]
+        b = sum((2 * kk[k]["fetch_kb_avg"] + kk[k]["write_kb_avg"]) * 1024 * kk[k]["launches"] for k in ks) / n
+        res["groups"][g] = {"bytes_per_launch": b, "kernels": ks, "group_launches": n}
     json.dump(res, open(out, "w"), indent=1)
     for g, v in res["groups"].items():
         print(f"{g:20s} {v['bytes_per_launch'] / 1e6:10.2f} MB/launch")

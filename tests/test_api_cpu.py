@@ -82,3 +82,16 @@ def test_install_routes_reference_module_names(tmp_path):
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(REPO, "integration"), REPO]))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=str(tmp_path), env=env)
     assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
+
+
+def test_seg_ids_above_255_raise():
+    """Mask images are uint8 (mask_predict.py:102); 16-bit ids above 255 would wrap and merge masks."""
+    import numpy as np
+    import pytest as _pt
+    from maskclustering_amd._device import seg_u8
+    a = np.array([[0, 3], [255, 7]], np.uint16)
+    assert seg_u8(a).dtype == np.uint8 and seg_u8(a).tolist() == [[0, 3], [255, 7]]
+    with _pt.raises(ValueError):
+        seg_u8(np.array([[0, 256]], np.uint16))
+    with _pt.raises(ValueError):
+        seg_u8(np.array([[0, 1.5]]))

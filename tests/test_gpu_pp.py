@@ -216,3 +216,13 @@ def test_pp_split_dbscan_path(seed, monkeypatch):
     assert len(got[0]) == len(oo) - 1
     for k in range(len(oo) - 1):
         np.testing.assert_array_equal(got[0][k], oi[oo[k]:oo[k + 1]].astype(np.int64))
+
+
+@pytest.mark.parametrize("seed", [1, 3])
+def test_pp_device_greedy_merge(seed, monkeypatch):
+    """MC_PP_GREEDY_CAP=0 sends every merge decision to the device greedy pass (k_pp_greedy, the
+    path for more than 65536 non-zero decisions): same objects as the oracle."""
+    monkeypatch.setenv("MC_PP_GREEDY_CAP", "0")
+    scene, pfm, fids, mpc, nodes = synthetic_pp(seed, **(dict(nb=12, n_nodes=50) if seed == 3 else {}))
+    got = _oracle_vs_gpu(scene, pfm, fids, mpc, nodes, 0.5)
+    assert len(got[0]) > 3
