@@ -171,10 +171,12 @@ class GraphStep:
         from oracle import oracle
         s = self.scene
         tm = {}
-        oracle.run(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, timings=tm, **CFG)
+        run = oracle.run if s.num_masks <= 30000 else oracle.run_sparse  # dense matrices beyond C2 do not fit
+        run(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, timings=tm, **CFG)
         cpu_s = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
         return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
-                "sample": f"oracle/mcgraph_oracle.c S2-S6 on the same scene (1 full scene, {cpu_s:.2f} s: "
+                "sample": f"{'oracle/mcgraph_oracle.c' if run is oracle.run else 'oracle/graph_sparse.c'} S2-S6 on "
+                          f"the same scene (1 full scene, {cpu_s:.2f} s: "
                           f"S2 {tm['s2']:.2f} S3 {tm['s3']:.2f} S4 {tm['s4']:.2f} S6 {tm['s6']:.2f})",
                 "scene_ms": round(cpu_s * 1e3, 1)}
 
@@ -188,14 +190,14 @@ class EndToEndStep:
         from maskclustering_amd.pipeline import GraphRun
         from maskclustering_amd.synthetic_frames import make_frames_shape
         t0 = time.perf_counter()
-        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}")
+        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}", out="torch")
         log(f"rendered {fr.num_frames} frames {fr.depth.shape[1]}x{fr.depth.shape[2]} P={fr.num_points} "
             f"in {time.perf_counter() - t0:.1f} s")
         self.fr = fr
         dev = torch.device("cuda", local)
         self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)  # construction.py:37
-        self.t_depth = torch.from_numpy(fr.depth).to(dev)
-        self.t_seg = torch.from_numpy(fr.seg).to(dev)
+        self.t_depth = fr.depth
+        self.t_seg = fr.seg
         self.t_K = torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev)
         self.t_T = torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)
         self.run = GraphRun(local)
@@ -232,12 +234,12 @@ class EndToEndStep:
         t0 = time.perf_counter()
         k = 0
         while k < fr.num_frames and time.perf_counter() - t0 < budget_s:
-            oracle.s1_frame(scene, fr.depth[k], fr.seg[k], fr.intrinsics[k], fr.poses[k])
+            oracle.s1_frame(scene, fr.depth[k].cpu().numpy(), fr.seg[k].cpu().numpy(), fr.intrinsics[k], fr.poses[k])
             k += 1
         s1 = (time.perf_counter() - t0) / k * fr.num_frames
         col, lab, off, pts = self.ctx.bp_masks()
         tm = {}
-        oracle.run(fr.num_points, fr.num_frames, col, lab, off, pts, timings=tm, **CFG)
+        oracle.run_sparse(fr.num_points, fr.num_frames, col, lab, off, pts, timings=tm, **CFG)
         g = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
         cpu_s = s1 + g
         return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
@@ -246,39 +248,81 @@ class EndToEndStep:
                 "scene_ms": round(cpu_s * 1e3, 1)}
 
 
-class ShardedEndToEndStep(EndToEndStep):
-    """--variant e2e --shard frames: ONE scene per step for the whole job.  Rank r holds its
-    frame slice in HBM, back-projects it, the mask lists are all-gathered over RCCL and
-    S2-S6 run replicated (maskclustering_amd/frame_shard.py)."""
+class ShardedGraphStep(GraphStep):
+    """--variant g --shard frames: ONE scene per step for the whole job (strong scaling).  Rank r
+    holds its frame slice's masks (the S1 output of its frames) in HBM; a step all-gathers them
+    and runs the row-block sharded S2-S6 (maskclustering_amd/frame_shard.py, graph_shard.py,
+    SURVEY.md §8(e))."""
 
     def __init__(self, shape, seed, local):
         import torch
-        from maskclustering_amd import _native
         from maskclustering_amd.frame_shard import FrameShardedScene
         from maskclustering_amd.pipeline import GraphRun
-        from maskclustering_amd.synthetic_frames import make_frames_shape
+        from maskclustering_amd.synthetic import SHAPES, make_shape
+        self.scene = s = make_shape(shape, seed=seed)
+        self.run = GraphRun(local)
+        self.run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.sh = FrameShardedScene(self.run, s.num_points, s.num_frames)
+        lo, hi = self.sh.lo, self.sh.hi
+        sel = np.nonzero((s.mask_col >= lo) & (s.mask_col < hi))[0]
+        off = np.zeros(len(sel) + 1, np.int64)
+        np.cumsum(np.diff(s.mask_off)[sel], out=off[1:])
+        pts = np.concatenate([s.mask_points(g) for g in sel]) if len(sel) else np.zeros(0, np.int32)
+        self.local = (s.mask_col[sel] - lo, s.mask_label[sel], off,
+                      torch.from_numpy(pts.astype(np.int32)).to(torch.device("cuda", local)))
+        self.groups = G_GROUPS
+        sh = SHAPES[shape]
+        self.workload = (f"{shape}: synthetic scene (SURVEY App. C), P={sh['num_points']} F={sh['num_frames']}, "
+                         f"S2-S6, frames sharded over {self.sh.world} GPU(s)")
+
+    def step(self):
+        self.sh.set_local_masks(*self.local)
+        self.sh.step(**CFG)
+
+    def work(self):
+        s = self.scene
+        return graph_work(self.run.ctx, self.sh.pts.cpu().numpy(), s.num_points, s.num_frames)
+
+
+class ShardedEndToEndStep(EndToEndStep):
+    """--variant e2e --shard frames: ONE scene per step for the whole job (strong scaling).  Rank
+    r renders and holds only its frame slice in HBM, back-projects it (S1 is independent per
+    frame), the mask lists are all-gathered over RCCL and S2-S6 run row-block sharded
+    (maskclustering_amd/frame_shard.py, graph_shard.py)."""
+
+    def __init__(self, shape, seed, local):
+        import torch
+        import torch.distributed as dist
+        from maskclustering_amd import _native
+        from maskclustering_amd.frame_shard import FrameShardedScene, frame_slice
+        from maskclustering_amd.pipeline import GraphRun
+        from maskclustering_amd.synthetic_frames import FRAME_SHAPES, make_frames_shape
         t0 = time.perf_counter()
-        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}")
-        self.fr = fr
+        F = FRAME_SHAPES[shape]["num_frames"]
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        lo, hi = frame_slice(F, world, rank)
         dev = torch.device("cuda", local)
+        fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}", frames=range(lo, hi), out="torch")
+        self.fr = fr
         self.run = GraphRun(local)
         self.ctx = self.run.ctx
         self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
         self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
-        self.sh = FrameShardedScene(self.run, fr.num_points, fr.num_frames)
-        lo, hi = self.sh.lo, self.sh.hi
+        self.sh = FrameShardedScene(self.run, fr.num_points, F)
+        assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
-        self.t_depth = up(fr.depth[lo:hi], torch.float32)
-        self.t_seg = up(fr.seg[lo:hi], torch.uint8)
-        self.t_K = up(fr.intrinsics[lo:hi], torch.float64)
-        self.t_T = up(fr.poses[lo:hi].reshape(-1, 16), torch.float64)
+        self.t_depth, self.t_seg = fr.depth, fr.seg
+        self.t_K = up(fr.intrinsics, torch.float64)
+        self.t_T = up(fr.poses.reshape(-1, 16), torch.float64)
         self.prm = _native.bp_params()
         self.groups = BP_GROUPS + G_GROUPS
-        F, H, W = fr.depth.shape
+        _, H, W = fr.depth.shape
+        self.F_total = F
         self.shape = (hi - lo, H, W)
-        log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F}, rendered in {time.perf_counter() - t0:.1f} s")
-        self.workload = (f"{shape}: ScanNet-shaped synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
+        log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
+        self.workload = (f"{shape}: synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
                          f"S1-S6, frames sharded over {self.sh.world} GPU(s)")
 
     def step(self):
@@ -287,12 +331,34 @@ class ShardedEndToEndStep(EndToEndStep):
 
     def work(self):
         F, H, W = self.shape
-        n = int(self.ctx.graph_info().num_masks)
         pts = self.sh.pts.cpu().numpy()
-        w = graph_work(self.ctx, pts, self.fr.num_points, self.fr.num_frames)
+        w = graph_work(self.ctx, pts, self.fr.num_points, self.F_total)
         w.update(bp_work(self.ctx, F, H, W))
-        assert n > 0
         return w
+
+    def cpu_baseline(self, budget_s=12.0):
+        """oracle S1 on the first frames (bounded sample, extrapolated per frame) + the sparse
+        oracle's S2-S6 on the full mask set (identical to the device's by the parity tests)."""
+        from oracle import oracle
+        fr = self.fr
+        scene = fr.scene_points.astype(np.float32)
+        t0 = time.perf_counter()
+        k = 0
+        while k < len(fr.depth) and time.perf_counter() - t0 < budget_s:
+            oracle.s1_frame(scene, fr.depth[k].cpu().numpy(), fr.seg[k].cpu().numpy(), fr.intrinsics[k], fr.poses[k])
+            k += 1
+        s1 = (time.perf_counter() - t0) / k * self.F_total
+        col, lab, off = self.sh.mask_index
+        pts = self.sh.pts.cpu().numpy()
+        tm = {}
+        oracle.run_sparse(fr.num_points, self.F_total, col, lab, off, pts, timings=tm, **CFG)
+        g = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
+        cpu_s = s1 + g
+        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
+                "sample": f"oracle S1 (oracle/s1_oracle.c, 1 thread) timed on {k} of {self.F_total} frames and "
+                          f"extrapolated ({s1:.1f} s) + the sparse oracle's S2-S6 (oracle/graph_sparse.c, "
+                          f"{tm['threads']} threads) on the full scene ({g:.2f} s)",
+                "scene_ms": round(cpu_s * 1e3, 1)}
 
 
 class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic the path reads
@@ -419,13 +485,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--variant", choices=["g", "e2e", "pp"], default="g")
-    ap.add_argument("--shape", default="c2")
+    ap.add_argument("--variant", choices=["g", "e2e", "pp"], default="e2e")
+    ap.add_argument("--shape", default="c3")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["scene", "frames"], default="scene",
-                    help="scene: every rank its own scene (weak scaling); frames: one scene, frames split "
-                         "over the ranks (e2e only, strong scaling)")
+    ap.add_argument("--shard", choices=["scene", "frames"], default="frames",
+                    help="frames: one scene, its frames split over the ranks, S2-S6 row-block sharded (strong "
+                         "scaling; the north_star's ScanNet++-sized C3 by default); scene: every rank its own "
+                         "scene (weak scaling, the reference's run.py sweep, BASELINE configs[4])")
     args = ap.parse_args()
     if args.variant == "pp":
         return run_post_process(args)
@@ -441,10 +508,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     frames = args.shard == "frames"
-    if frames and args.variant != "e2e":
-        raise SystemExit("--shard frames needs --variant e2e (S1 is the stage that shards by frame)")
     if frames:  # one scene, frame slices per rank (strong scaling)
-        runner = ShardedEndToEndStep(args.shape, args.seed, local)
+        runner = (ShardedGraphStep if args.variant == "g" else ShardedEndToEndStep)(args.shape, args.seed, local)
     else:  # every rank its own scene (weak scaling)
         runner = (GraphStep if args.variant == "g" else EndToEndStep)(args.shape, args.seed + rank, local)
     ctx = runner.run.ctx
@@ -515,7 +580,7 @@ def main():
                     stages[g][k] = e[k]
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = runner.cpu_baseline()
         ratio_path = os.path.join(REPO, "profiles", f"cpu_ratio_{args.shape}.json")
         if os.path.exists(ratio_path) and args.variant == "g":

@@ -201,6 +201,32 @@ int mc_cluster_get_objects(mc_ctx *ctx, uint64_t *vf_bits /* K*ceil(F/64) */,
                            int64_t *pt_off /* K+1 */, int32_t *pt_idx,
                            int64_t *mask_off /* K+1 */, int32_t *mask_idx /* level-0 node ids */);
 
+/* ---- row-block sharding over processes ------------------------------------
+ * One process per GPU, each with its own context holding the same scene (mc_scene_set_masks).
+ * After mc_shard_set(ctx, rank, world > 1):
+ *   - mc_graph_build runs S2 and S3 (graph/construction.py:98-170) on this rank's block of mask
+ *     rows only and leaves MC_SHARD_S3 pending;
+ *   - mc_shard_import(MC_SHARD_S3) takes every rank's block, runs the under-segmentation undo,
+ *     S5 and this rank's tiles of the S4 observer histogram (:80-96), leaves MC_SHARD_HIST pending;
+ *   - mc_shard_import(MC_SHARD_HIST) takes the histogram SUMMED over the ranks and computes the
+ *     thresholds (the graph is then complete and identical on every rank);
+ *   - mc_cluster_run evaluates the first iteration's N0 x N0 pairs (iterative_clustering.py:20-29)
+ *     on the rows a = rank (mod world) and leaves MC_SHARD_FOREST pending;
+ *   - mc_shard_import(MC_SHARD_FOREST) unites every rank's union-find forest and runs the rest
+ *     of S6 (identical on every rank).
+ * The host moves the blocks with its own collectives between the calls: mc_shard_export gives
+ * this rank's block (size query with dst_dev = NULL; a stream-ordered copy into a device
+ * buffer); all-gather the S3 and FOREST blocks into [world][stride_bytes] in rank order; all-reduce
+ * (sum, 64-bit) the HIST block.  mc_shard_pending reports the phase waiting (0 = none).
+ * world = 1 restores the single-process path. */
+#define MC_SHARD_S3 1
+#define MC_SHARD_HIST 2
+#define MC_SHARD_FOREST 3
+int mc_shard_set(mc_ctx *ctx, int32_t rank, int32_t world);
+int mc_shard_pending(mc_ctx *ctx, int32_t *phase);
+int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes);
+int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes);
+
 /* ---- post-processing of the clustered objects ----------------------
  * Replaces the compute of utils/post_process.py:173-194 (post_process up to export):
  * dbscan_process (:104-123), filter_point (:40-101), merge_overlapping_objects (:7-37).

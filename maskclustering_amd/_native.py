@@ -36,7 +36,12 @@ EXPORTED = [
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
+    "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
 ]
+
+MC_SHARD_S3 = 1
+MC_SHARD_HIST = 2
+MC_SHARD_FOREST = 3
 
 MC_BP_NSTAT = 10
 BP_STATS = ["frame", "id", "npix", "nvox", "ndbscan", "nsor", "ncand", "ncovered", "nneighbors", "kept"]
@@ -160,6 +165,10 @@ def load():
         "mc_pp_get_results": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
         "mc_eval_match_counts": (ctypes.c_int, [vp, i64, i32, vp, vp, i32, vp, vp, vp, vp]),
         "mc_frames_decode": (ctypes.c_int, [vp, i32, i32, i32, vp, dbl, i32, i32, vp, ctypes.c_int, vp, vp]),
+        "mc_shard_set": (ctypes.c_int, [vp, i32, i32]),
+        "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
+        "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
+        "mc_shard_import": (ctypes.c_int, [vp, i32, vp, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -177,6 +186,7 @@ class Context:
     """One libmcgraph context (device memory + stream) — one scene at a time."""
 
     def __init__(self, device: int = 0):
+        self.device_index = int(device)
         self.L = load()
         h = ctypes.c_void_p()
         rc = self.L.mc_ctx_create(int(device), ctypes.byref(h))
@@ -222,6 +232,34 @@ class Context:
 
     def reset_kernel_times(self):
         self._check(self.L.mc_ctx_reset_kernel_times(self.h))
+
+    # ---- row-block sharding over processes (include/mcgraph.h) ----
+    @property
+    def torch_device(self):
+        import torch
+        return torch.device("cuda", self.device_index)
+
+    def shard_set(self, rank, world):
+        self._check(self.L.mc_shard_set(self.h, int(rank), int(world)))
+
+    def shard_pending(self) -> int:
+        ph = ctypes.c_int32()
+        self._check(self.L.mc_shard_pending(self.h, ctypes.byref(ph)))
+        return ph.value
+
+    def shard_export_size(self, phase) -> int:
+        n = ctypes.c_int64()
+        self._check(self.L.mc_shard_export(self.h, int(phase), None, ctypes.byref(n)))
+        return n.value
+
+    def shard_export(self, phase, out):
+        """this rank's block into the device tensor ``out`` (stream-ordered on the context stream)"""
+        n = ctypes.c_int64()
+        self._check(self.L.mc_shard_export(self.h, int(phase), ctypes.c_void_p(out.data_ptr()), ctypes.byref(n)))
+
+    def shard_import(self, phase, blocks, stride_bytes):
+        """every rank's block ([world][stride_bytes] in rank order; HIST: the summed block)"""
+        self._check(self.L.mc_shard_import(self.h, int(phase), ctypes.c_void_p(blocks.data_ptr()), int(stride_bytes)))
 
     # ---- scene ----
     def set_masks(self, num_points, num_frames, mask_col, mask_label, mask_off, mask_pts=None, pts_device_ptr=None):

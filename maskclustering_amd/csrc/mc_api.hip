@@ -13,6 +13,7 @@
 #include "mc_pp_kernels.inl"
 #include "mc_eval_kernels.inl"
 #include "mc_io_kernels.inl"
+#include "mc_shard_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -114,6 +115,18 @@ struct mc_ctx {
     std::vector<int32_t> bp_col, bp_label, bp_stats;
     std::vector<int64_t> bp_off;
 
+    // ---- row-block sharding over processes ----
+    int sh_rank = 0, sh_world = 1;
+    int sh_pending = 0;          // MC_SHARD_* phase waiting for the host's exchange, 0 = none
+    int sh_r0 = 0, sh_r1 = 0;    // this rank's S3 mask rows
+    int64_t sh_s3_words = -1;    // size of this rank's S3 block (valid while sh_pending == MC_SHARD_S3)
+    mc_graph_params sh_params{};
+    DevBuf d_sh_eoff;
+    // S6 state kept across the FOREST exchange
+    int s6_nthr = 0;
+    bool s6_dense_obs = false;
+    float s6_ctf = 0.f;
+
     // ---- post-processing ----
     DevBuf d_pp_posmap;  // one P-entry position map per workgroup, -1 at rest
     int64_t pp_posmap_P = 0;
@@ -166,7 +179,8 @@ void sync_stats(mc_ctx *ctx)
 
 // S4 histogram launch: persistent blocks, R lane-indexed LDS replicas (odd stride)
 // rng: >= ceil(M / 64) int2 of scratch
-void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsigned long long *hist, int2 *rng)
+void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsigned long long *hist, int2 *rng,
+                 int shard_rank = 0, int shard_world = 1)
 {
     if (!M || !F) return;
     const int FW = (F + 63) / 64;
@@ -179,7 +193,61 @@ void launch_hist(hipStream_t s, const unsigned long long *vf, int M, int F, unsi
     const size_t lds = 2 * mc::kHistTile * mc::kHistKW * sizeof(unsigned long long) + static_cast<size_t>(R) * HS * 4;
     const long long grid = std::min<long long>(ntiles, 1024);
     hipLaunchKernelGGL(mc::k_s4_hist, dim3(static_cast<unsigned>(grid)), dim3(256), lds, s, vf, M, FW, F, nblk, ntiles, R,
-                       HS, rng, hist);
+                       HS, rng, hist, shard_rank, shard_world);
+}
+
+// S3 work lists of this rank's mask rows [sh_r0, sh_r1) (all rows when not sharded): a wave per
+// mask for the bulk, a workgroup per mask for large masks, largest first.  Rows are split over
+// the ranks in contiguous blocks of about equal point counts.
+void build_s3_lists(mc_ctx *ctx, const std::vector<int32_t> &frame_start)
+{
+    const int M = ctx->M, F = ctx->F;
+    hipStream_t s = ctx->stream;
+    {
+        const int64_t tot = ctx->h_off[M];
+        const int r = ctx->sh_rank, W = ctx->sh_world;
+        auto cut = [&](int k) {  // first row whose cumulative points reach k/W of the total
+            if (k <= 0) return 0;
+            if (k >= W) return M;
+            const int64_t target = (tot * k + W - 1) / W;
+            return static_cast<int>(std::lower_bound(ctx->h_off.begin(), ctx->h_off.begin() + M + 1,
+                                                     static_cast<int32_t>(target)) - ctx->h_off.begin());
+        };
+        ctx->sh_r0 = std::min(cut(r), M);
+        ctx->sh_r1 = std::max(ctx->sh_r0, std::min(cut(r + 1), M));
+    }
+    int max_per_frame = 0;
+    for (int c = 0; c < F; c++) max_per_frame = std::max(max_per_frame, frame_start[c + 1] - frame_start[c]);
+    const bool wave_ok = F <= 64 * mc::kS3wFrameWords64 && max_per_frame < mc::kS3wCounters;
+    std::vector<int> small, big;
+    for (int g = ctx->sh_r0; g < ctx->sh_r1; g++) {
+        const int sz = ctx->h_off[g + 1] - ctx->h_off[g];
+        (wave_ok && sz <= mc::kS3SmallPts ? small : big).push_back(g);
+    }
+    // largest masks first: the long waves start early instead of forming the tail
+    auto by_size = [&](int x, int y) { return ctx->h_off[x + 1] - ctx->h_off[x] > ctx->h_off[y + 1] - ctx->h_off[y]; };
+    std::stable_sort(small.begin(), small.end(), by_size);
+    std::stable_sort(big.begin(), big.end(), by_size);
+    ctx->n_s3_small = static_cast<int>(small.size());
+    ctx->n_s3_big = static_cast<int>(big.size());
+    ctx->d_s3_small.reserve((small.size() + 1) * sizeof(int));
+    ctx->d_s3_big.reserve((big.size() + 1) * sizeof(int));
+    if (!small.empty())
+        MC_HIP(hipMemcpyAsync(ctx->d_s3_small.ptr, small.data(), small.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!big.empty())
+        MC_HIP(hipMemcpyAsync(ctx->d_s3_big.ptr, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    MC_HIP(hipStreamSynchronize(s));
+}
+
+std::vector<int32_t> frame_starts(const mc_ctx *ctx)
+{
+    std::vector<int32_t> fs(ctx->F + 1, 0);
+    int g = 0;
+    for (int c = 0; c <= ctx->F; c++) {
+        while (g < ctx->M && ctx->h_col[g] < c) g++;
+        fs[c] = g;
+    }
+    return fs;
 }
 
 }  // namespace
@@ -231,7 +299,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
                       &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out, &ctx->d_owner0,
                       &ctx->d_node_of_mask, &ctx->d_ownA, &ctx->d_ownB, &ctx->d_cap, &ctx->d_obj_of_mask,
-                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen};
+                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen, &ctx->d_sh_eoff};
     for (DevBuf *b : bufs) b->release();
     DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
                          &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg,
@@ -448,32 +516,7 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
         ctx->d_owner0.reserve((static_cast<size_t>(M) * F + 1) * sizeof(int));
         ctx->d_node_of_mask.reserve((M + 1) * sizeof(int));
         ctx->d_obj_of_mask.reserve((M + 1) * sizeof(int));
-        // S3 work lists: wave-per-mask for the bulk, workgroup-per-mask for large masks
-        {
-            int max_per_frame = 0;
-            for (int c = 0; c < F; c++) max_per_frame = std::max(max_per_frame, frame_start[c + 1] - frame_start[c]);
-            const bool wave_ok = F <= 64 * mc::kS3wFrameWords64 && max_per_frame < mc::kS3wCounters;
-            std::vector<int> small, big;
-            for (int g = 0; g < M; g++) {
-                const int sz = ctx->h_off[g + 1] - ctx->h_off[g];
-                (wave_ok && sz <= mc::kS3SmallPts ? small : big).push_back(g);
-            }
-            // largest masks first: the long waves start early instead of forming the tail
-            auto by_size = [&](int x, int y) {
-                return ctx->h_off[x + 1] - ctx->h_off[x] > ctx->h_off[y + 1] - ctx->h_off[y];
-            };
-            std::stable_sort(small.begin(), small.end(), by_size);
-            std::stable_sort(big.begin(), big.end(), by_size);
-            ctx->n_s3_small = static_cast<int>(small.size());
-            ctx->n_s3_big = static_cast<int>(big.size());
-            ctx->d_s3_small.reserve((small.size() + 1) * sizeof(int));
-            ctx->d_s3_big.reserve((big.size() + 1) * sizeof(int));
-            if (!small.empty())
-                MC_HIP(hipMemcpyAsync(ctx->d_s3_small.ptr, small.data(), small.size() * sizeof(int), hipMemcpyHostToDevice, s));
-            if (!big.empty())
-                MC_HIP(hipMemcpyAsync(ctx->d_s3_big.ptr, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice, s));
-            MC_HIP(hipStreamSynchronize(s));
-        }
+        build_s3_lists(ctx, frame_start);
         ctx->have_scene = true;
     });
 }
@@ -481,6 +524,63 @@ int mc_scene_set_masks(mc_ctx *ctx, int64_t num_points, int32_t num_frames, int3
 // ---------------------------------------------------------------------------------------------
 // S2–S5
 // ---------------------------------------------------------------------------------------------
+// S3 undo + S5 + S4 (this rank's tiles of the observer histogram when sharded)
+static void graph_build_tail(mc_ctx *ctx)
+{
+    hipStream_t s = ctx->stream;
+    const int F = ctx->F, FW = ctx->FW, M = ctx->M;
+    int *stats = ctx->d_stats.as<int>();
+    if (M) {  // S3 undo + S5
+        TimedScope ts(ctx->timer, s, "s3_undo_s5");
+        hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(std::max(M, F + 1), 256)), dim3(256), 0, s,
+                           ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
+                           ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>(),
+                           ctx->d_hist.as<unsigned long long>(), ctx->d_spread.as<int>(), stats + ST_NBND);
+        mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC,
+                          ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), stats + ST_N0);
+        hipLaunchKernelGGL(mc::k_s3_undo_write, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
+                           ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), ctx->d_mask_col.as<int>(), M,
+                           F, FW, ctx->d_c_off.as<int>(), ctx->d_c_idx.as<int>(),
+                           ctx->d_vf.as<unsigned long long>());
+        hipLaunchKernelGGL(mc::k_s5_nodes, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_node_pos.as<int>(),
+                           ctx->d_useg.as<unsigned char>(), ctx->d_c_off.as<int>(), ctx->d_mask_off.as<int>(),
+                           ctx->d_vf.as<unsigned long long>(), M, FW, ctx->d_node0_g.as<int>(),
+                           ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
+                           ctx->d_n0_ptlen.as<int>(), ctx->d_n0_vf.as<unsigned long long>(),
+                           ctx->d_owner0.as<int>(), ctx->d_node_of_mask.as<int>());
+    } else {
+        MC_HIP(hipMemsetAsync(ctx->d_hist.ptr, 0, (F + 1) * sizeof(unsigned long long), s));
+    }
+    {  // S4: observer histogram (the thresholds follow in graph_build_thresholds)
+        TimedScope ts(ctx->timer, s, "s4_observer_hist");
+        launch_hist(s, ctx->d_vf.as<unsigned long long>(), M, F, ctx->d_hist.as<unsigned long long>(),
+                    ctx->d_s4rng.as<int2>(), ctx->sh_rank, ctx->sh_world);
+    }
+    MC_HIP(hipGetLastError());
+}
+
+static void graph_build_thresholds(mc_ctx *ctx)
+{
+    hipStream_t s = ctx->stream;
+    const int F = ctx->F;
+    int *stats = ctx->d_stats.as<int>();
+    {
+        TimedScope ts(ctx->timer, s, "s4_observer_hist");
+        hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
+                           ctx->d_hist.as<unsigned long long>(), F, ctx->d_thr.as<float>(), ctx->d_isint.as<int>(),
+                           stats + ST_NTHR, stats + ST_THR_STATUS);
+    }
+    MC_HIP(hipGetLastError());
+    // level-0 nodes live in the graph's buffers
+    ctx->n0_pool = ctx->d_c_idx.as<int>();
+    ctx->n0_pts = ctx->d_mask_pts.as<int>();
+    ctx->Mn = ctx->M;
+    ctx->n0_pts_total = ctx->nnz;
+    ctx->nodes_from_graph = true;
+    ctx->have_graph = true;
+    ctx->have_nodes = true;
+}
+
 int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
 {
     return guarded(ctx, [&] {
@@ -491,6 +591,9 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
         const int F = ctx->F, FW = ctx->FW, M = ctx->M, nnz = ctx->nnz;
         int *stats = ctx->d_stats.as<int>();
         ctx->have_cluster = false;
+        ctx->have_graph = ctx->have_nodes = false;
+        ctx->sh_pending = 0;
+        ctx->sh_params = *params;
         {  // S2
             TimedScope ts(ctx->timer, s, "s2_point_lists");
             hipLaunchKernelGGL(mc::k_s2_degree, grid_for(nnz), dim3(256), 0, s, ctx->d_mask_pts.as<int>(), nnz,
@@ -539,44 +642,13 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
             }
         }
-        if (M) {  // S3 undo + S5
-            TimedScope ts(ctx->timer, s, "s3_undo_s5");
-            hipLaunchKernelGGL(mc::k_s3_undo_count, dim3(ceil_div(std::max(M, F + 1), 256)), dim3(256), 0, s,
-                               ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), M, F,
-                               ctx->d_keep_cnt.as<int>(), ctx->d_node_flag.as<int>(),
-                               ctx->d_hist.as<unsigned long long>(), ctx->d_spread.as<int>(), stats + ST_NBND);
-            mc::scan_device_n(s, ctx->d_keep_cnt.as<int>(), ctx->d_c_off.as<int>(), nullptr, M, stats + ST_NNZC,
-                              ctx->d_node_flag.as<int>(), ctx->d_node_pos.as<int>(), stats + ST_N0);
-            hipLaunchKernelGGL(mc::k_s3_undo_write, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_ctmp.as<int>(),
-                               ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>(), ctx->d_mask_col.as<int>(), M,
-                               F, FW, ctx->d_c_off.as<int>(), ctx->d_c_idx.as<int>(),
-                               ctx->d_vf.as<unsigned long long>());
-            hipLaunchKernelGGL(mc::k_s5_nodes, dim3(ceil_div(M, 256)), dim3(256), 0, s, ctx->d_node_pos.as<int>(),
-                               ctx->d_useg.as<unsigned char>(), ctx->d_c_off.as<int>(), ctx->d_mask_off.as<int>(),
-                               ctx->d_vf.as<unsigned long long>(), M, FW, ctx->d_node0_g.as<int>(),
-                               ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->d_n0_ptoff.as<int>(),
-                               ctx->d_n0_ptlen.as<int>(), ctx->d_n0_vf.as<unsigned long long>(),
-                               ctx->d_owner0.as<int>(), ctx->d_node_of_mask.as<int>());
-        } else {
-            MC_HIP(hipMemsetAsync(ctx->d_hist.ptr, 0, (F + 1) * sizeof(unsigned long long), s));
+        if (ctx->sh_world > 1) {  // this rank's S3 rows go to the others first (mc_shard_export/import)
+            ctx->sh_pending = MC_SHARD_S3;
+            ctx->sh_s3_words = -1;
+            return;
         }
-        {  // S4
-            TimedScope ts(ctx->timer, s, "s4_observer_hist");
-            launch_hist(s, ctx->d_vf.as<unsigned long long>(), M, F, ctx->d_hist.as<unsigned long long>(),
-                        ctx->d_s4rng.as<int2>());
-            hipLaunchKernelGGL(mc::k_s4_thresholds, dim3(1), dim3(256), (F + 1) * sizeof(unsigned long long), s,
-                               ctx->d_hist.as<unsigned long long>(), F, ctx->d_thr.as<float>(), ctx->d_isint.as<int>(),
-                               stats + ST_NTHR, stats + ST_THR_STATUS);
-        }
-        MC_HIP(hipGetLastError());
-        // level-0 nodes live in the graph's buffers
-        ctx->n0_pool = ctx->d_c_idx.as<int>();
-        ctx->n0_pts = ctx->d_mask_pts.as<int>();
-        ctx->Mn = M;
-        ctx->n0_pts_total = nnz;
-        ctx->nodes_from_graph = true;
-        ctx->have_graph = true;
-        ctx->have_nodes = true;
+        graph_build_tail(ctx);
+        graph_build_thresholds(ctx);
     });
 }
 
@@ -822,6 +894,155 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
 // ---------------------------------------------------------------------------------------------
 // S6
 // ---------------------------------------------------------------------------------------------
+// S6 iterations t_begin .. nthr-1 (after_pairs: iteration t_begin's pairs are done) and the final
+// object state; the level-t node arrays are re-derived from the ping-pong pools
+static void s6_iterations(mc_ctx *ctx, int t_begin, bool after_pairs)
+{
+    hipStream_t s = ctx->stream;
+    const int nthr = ctx->s6_nthr, N0 = ctx->N0, FW = ctx->FW, Mn = ctx->Mn;
+    const bool dense_obs = ctx->s6_dense_obs;
+    const float ctf = ctx->s6_ctf;
+    const size_t n0 = static_cast<size_t>(std::max(N0, 1));
+    int *Nlev = ctx->d_Nlev.as<int>();
+    int *dcap = ctx->d_cap.as<int>();
+    MC_REQUIRE(t_begin == 0, MC_ERR_STATE, "S6 resumes only at iteration 0");
+    const int *cur_off = ctx->d_n0_off.as<int>(), *cur_len = ctx->d_n0_len.as<int>(), *cur_pool = ctx->n0_pool;
+    const unsigned long long *cur_vf = ctx->d_n0_vf.as<unsigned long long>();
+    const dim3 gN = grid_for(N0), gW = grid_for(N0, mc::kPairWaves, 2048), gK = grid_for(N0, 1, 2048);
+    for (int t = t_begin; t < nthr; t++) {
+        const int *dN = Nlev + t;
+        int *dNn = Nlev + t + 1;
+        const bool toA = (t % 2) == 0;
+        int *nx_off = toA ? ctx->d_offA.as<int>() : ctx->d_offB.as<int>();
+        int *nx_len = toA ? ctx->d_lenA.as<int>() : ctx->d_lenB.as<int>();
+        int *nx_pool = toA ? ctx->d_poolA.as<int>() : ctx->d_poolB.as<int>();
+        int *nx_own = toA ? ctx->d_ownA.as<int>() : ctx->d_ownB.as<int>();
+        unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
+        if (t == t_begin && after_pairs) {
+            // level 0's pairs ran on every rank's share and their forests were united
+        } else if (!dense_obs) {
+            TimedScope ts(ctx->timer, s, "s6_pairs");
+            const mc::OvfWork ow{ctx->d_scratch.as<int>(), ctx->d_touched.as<int>(), N0, ctx->d_ovf_n.as<int>() + 1};
+            hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
+                               ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
+                               ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
+                               ctx->d_edges.as<unsigned long long>(), ow, 0, 1);
+        } else {
+            TimedScope ts(ctx->timer, s, "s6_pairs");
+            hipLaunchKernelGGL(mc::k6_parent_init, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>());
+            hipLaunchKernelGGL(mc::k6_pairs_dense, dim3(4096), dim3(256), 0, s, dN, cur_vf, FW,
+                               ctx->d_thr.as<float>(), t, ctx->d_parent.as<int>(),
+                               ctx->d_edges.as<unsigned long long>());
+        }
+        {
+            TimedScope ts(ctx->timer, s, "s6_components");
+            if (t > 0 && N0 <= kFusedComponentsMaxN0) {  // N_t <= N_1, typically N0 / 8: one workgroup
+                hipLaunchKernelGGL(mc::k6_components, dim3(1), dim3(1024), 0, s, dN, dNn, ctx->d_parent.as<int>(),
+                                   ctx->d_root.as<int>(), ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
+                                   ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
+                                   ctx->d_memoff.as<int>(), ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(),
+                                   dcap + t + 1, ctx->d_members.as<int>(), ctx->d_ovf_n.as<int>());
+            } else {
+                hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
+                                   ctx->d_root.as<int>(), ctx->d_isroot.as<int>(), ctx->d_ublen.as<int>(),
+                                   ctx->d_ovf_n.as<int>());
+                mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
+                hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(),
+                                   ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
+                                   ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
+                                   ctx->d_ublen.as<int>());
+                mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr,
+                                  ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dcap + t + 1);
+                hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, 0, ctx->d_label.as<int>(),
+                                   ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>(),
+                                   nullptr);
+            }
+        }
+        {
+            TimedScope ts(ctx->timer, s, "s6_merge");
+            // + the next iteration's column lists (nodes containing each mask, relabelled)
+            const bool cols = !dense_obs && t + 1 < nthr;
+            const mc::ColUpdate cu{Mn, dNn, ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(),
+                                   ctx->d_colnodes.as<int>(), cols ? ctx->d_label.as<int>() : nullptr,
+                                   ctx->d_parent.as<int>(), N0, ctx->d_label.as<int>(),
+                                   ctx->d_final_label.as<int>()};
+            hipLaunchKernelGGL(mc::k6_merge, gK, dim3(256), 0, s, dNn, ctx->d_memoff.as<int>(),
+                               ctx->d_members.as<int>(), cur_off, cur_len, cur_pool, cur_vf, FW,
+                               ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_own, nx_vf, cu);
+        }
+        cur_off = nx_off;
+        cur_len = nx_len;
+        cur_pool = nx_pool;
+        cur_vf = nx_vf;
+    }
+    ctx->fin_off = cur_off;
+    ctx->fin_len = cur_len;
+    ctx->fin_pool = cur_pool;
+    ctx->fin_vf = cur_vf;
+    ctx->n_iter = nthr;
+    // ---- final point sets (node.py:35), per-object range bitmaps ----
+    const int *dK = Nlev + nthr;
+    int *stats = ctx->d_stats.as<int>();
+    const bool point_path = ctx->nodes_from_graph;
+    {
+        TimedScope ts(ctx->timer, s, "s7_points");
+        hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+        if (point_path) {
+            hipLaunchKernelGGL(mc::k7_obj_of_mask, grid_for(ctx->M), dim3(256), 0, s, ctx->M,
+                               ctx->d_node_of_mask.as<int>(), ctx->d_final_label.as<int>(),
+                               ctx->d_obj_of_mask.as<int>());
+            hipLaunchKernelGGL(mc::k7p_points<0>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
+                               ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
+                               ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(), nullptr,
+                               nullptr, stats + ST_OBJOVF);
+        }
+        else
+            hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                               ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+        hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                           ctx->d_nwords.as<int>(), stats + ST_K);
+        mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
+    }
+    sync_stats(ctx);  // bitmap capacity
+    ctx->K = ctx->h_stats[ST_K];
+    const bool use_points = point_path && ctx->h_stats[ST_OBJOVF] == 0;
+    if (point_path && !use_points) {  // a point in > 8 objects: redo the ranges per node
+        hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+        hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                           ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                           ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
+        hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                           ctx->d_nwords.as<int>(), stats + ST_K);
+        mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
+        sync_stats(ctx);
+    }
+    const size_t words = static_cast<size_t>(std::max(ctx->h_stats[ST_WORDS], 1));
+    ctx->d_bm.reserve(words * 8);
+    {
+        TimedScope ts(ctx->timer, s, "s7_points");
+        MC_HIP(hipMemsetAsync(ctx->d_bm.ptr, 0, words * 8, s));
+        if (use_points)
+            hipLaunchKernelGGL(mc::k7p_points<1>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
+                               ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
+                               ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
+                               ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>(), stats + ST_OBJOVF);
+        else
+            hipLaunchKernelGGL(mc::k7_setbits, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
+                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
+                               ctx->d_pmin.as<int>(), ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>());
+        hipLaunchKernelGGL(mc::k7_count, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
+                           ctx->d_bm.as<unsigned long long>(), ctx->d_ptcnt.as<int>());
+        mc::scan_device_n(s, ctx->d_ptcnt.as<int>(), ctx->d_ptoff_out.as<int>(), dK, 0, stats + ST_NPTS);
+        hipLaunchKernelGGL(mc::k7_extract, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
+                           ctx->d_bm.as<unsigned long long>(), ctx->d_pmin.as<int>(), ctx->d_ptoff_out.as<int>(),
+                           ctx->d_pts_out.as<int>());
+    }
+    MC_HIP(hipGetLastError());
+    MC_HIP(hipMemcpyAsync(ctx->h_stats, ctx->d_stats.ptr, ST_COUNT * sizeof(int), hipMemcpyDeviceToHost, s));
+    ctx->have_cluster = true;
+}
+
 int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double connect_threshold)
 {
     return guarded(ctx, [&] {
@@ -912,12 +1133,8 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
                            dcap, ctx->nodes_from_graph ? stats + ST_NNZC : nullptr, static_cast<int>(ctx->nnzC0),
                            ctx->d_edges.as<unsigned long long>(), nthr);
 
-        const int *cur_off = ctx->d_n0_off.as<int>(), *cur_len = ctx->d_n0_len.as<int>(), *cur_pool = ctx->n0_pool;
-        const int *cur_own = ctx->d_owner0.as<int>();
-        const unsigned long long *cur_vf = ctx->d_n0_vf.as<unsigned long long>();
-        const dim3 gN = grid_for(N0), gE = grid_for(std::max<int64_t>(N0, ctx->nnzC0)),
-                   gW = grid_for(N0, mc::kPairWaves, 2048), gK = grid_for(N0, 1, 2048),
-                   gC = grid_for(std::max(N0, Mn), 64, 8192);
+        const dim3 gE = grid_for(std::max<int64_t>(N0, ctx->nnzC0)), gC = grid_for(std::max(N0, Mn), 64, 8192);
+        const int *cur_pool = ctx->n0_pool, *cur_own = ctx->d_owner0.as<int>();
         if (!dense_obs && nthr > 0) {  // level-0 column lists (nodes contained by each mask)
             TimedScope ts(ctx->timer, s, "s6_columns");
             hipLaunchKernelGGL(mc::k6_colcount, gE, dim3(256), 0, s, Nlev, dcap, cur_pool, cur_own,
@@ -928,136 +1145,128 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
             hipLaunchKernelGGL(mc::k6_colupdate, gC, dim3(64), 0, s, Mn, Nlev, ctx->d_coloff.as<int>(),
                                ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), nullptr, ctx->d_parent.as<int>());
         }
-        for (int t = 0; t < nthr; t++) {
-            const int *dN = Nlev + t;
-            int *dNn = Nlev + t + 1;
-            const bool toA = (t % 2) == 0;
-            int *nx_off = toA ? ctx->d_offA.as<int>() : ctx->d_offB.as<int>();
-            int *nx_len = toA ? ctx->d_lenA.as<int>() : ctx->d_lenB.as<int>();
-            int *nx_pool = toA ? ctx->d_poolA.as<int>() : ctx->d_poolB.as<int>();
-            int *nx_own = toA ? ctx->d_ownA.as<int>() : ctx->d_ownB.as<int>();
-            unsigned long long *nx_vf = toA ? ctx->d_vfA.as<unsigned long long>() : ctx->d_vfB.as<unsigned long long>();
-            if (!dense_obs) {
-                TimedScope ts(ctx->timer, s, "s6_pairs");
-                const mc::OvfWork ow{ctx->d_scratch.as<int>(), ctx->d_touched.as<int>(), N0, ctx->d_ovf_n.as<int>() + 1};
-                hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
-                                   ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
-                                   ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
-                                   ctx->d_edges.as<unsigned long long>(), ow);
-            } else {
-                TimedScope ts(ctx->timer, s, "s6_pairs");
-                hipLaunchKernelGGL(mc::k6_parent_init, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>());
-                hipLaunchKernelGGL(mc::k6_pairs_dense, dim3(4096), dim3(256), 0, s, dN, cur_vf, FW,
-                                   ctx->d_thr.as<float>(), t, ctx->d_parent.as<int>(),
-                                   ctx->d_edges.as<unsigned long long>());
-            }
-            {
-                TimedScope ts(ctx->timer, s, "s6_components");
-                if (t > 0 && N0 <= kFusedComponentsMaxN0) {  // N_t <= N_1, typically N0 / 8: one workgroup
-                    hipLaunchKernelGGL(mc::k6_components, dim3(1), dim3(1024), 0, s, dN, dNn, ctx->d_parent.as<int>(),
-                                       ctx->d_root.as<int>(), ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
-                                       ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
-                                       ctx->d_memoff.as<int>(), ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(),
-                                       dcap + t + 1, ctx->d_members.as<int>(), ctx->d_ovf_n.as<int>());
-                } else {
-                    hipLaunchKernelGGL(mc::k6_compress, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>(),
-                                       ctx->d_root.as<int>(), ctx->d_isroot.as<int>(), ctx->d_ublen.as<int>(),
-                                       ctx->d_ovf_n.as<int>());
-                    mc::scan_device_n(s, ctx->d_isroot.as<int>(), ctx->d_rank.as<int>(), dN, 0, dNn);
-                    hipLaunchKernelGGL(mc::k6_relabel, gN, dim3(256), 0, s, dN, ctx->d_root.as<int>(),
-                                       ctx->d_rank.as<int>(), cur_len, ctx->d_label.as<int>(),
-                                       ctx->d_levels.as<int>() + static_cast<size_t>(t) * n0, ctx->d_memcnt.as<int>(),
-                                       ctx->d_ublen.as<int>());
-                    mc::scan_device_n(s, ctx->d_memcnt.as<int>(), ctx->d_memoff.as<int>(), dNn, 0, nullptr,
-                                      ctx->d_ublen.as<int>(), ctx->d_newoff.as<int>(), dcap + t + 1);
-                    hipLaunchKernelGGL(mc::k6_memscatter, gN, dim3(256), 0, s, dN, 0, ctx->d_label.as<int>(),
-                                       ctx->d_memoff.as<int>(), ctx->d_memcnt.as<int>(), ctx->d_members.as<int>(),
-                                       nullptr);
-                }
-            }
-            {
-                TimedScope ts(ctx->timer, s, "s6_merge");
-                // + the next iteration's column lists (nodes containing each mask, relabelled)
-                const bool cols = !dense_obs && t + 1 < nthr;
-                const mc::ColUpdate cu{Mn, dNn, ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(),
-                                       ctx->d_colnodes.as<int>(), cols ? ctx->d_label.as<int>() : nullptr,
-                                       ctx->d_parent.as<int>(), N0, ctx->d_label.as<int>(),
-                                       ctx->d_final_label.as<int>()};
-                hipLaunchKernelGGL(mc::k6_merge, gK, dim3(256), 0, s, dNn, ctx->d_memoff.as<int>(),
-                                   ctx->d_members.as<int>(), cur_off, cur_len, cur_pool, cur_vf, FW,
-                                   ctx->d_newoff.as<int>(), nx_off, nx_len, nx_pool, nx_own, nx_vf, cu);
-            }
-            cur_off = nx_off;
-            cur_len = nx_len;
-            cur_pool = nx_pool;
-            cur_own = nx_own;
-            cur_vf = nx_vf;
+        ctx->s6_nthr = nthr;
+        ctx->s6_dense_obs = dense_obs;
+        ctx->s6_ctf = ctf;
+        ctx->have_cluster = false;
+        ctx->sh_pending = 0;
+        if (nthr > 0 && N0 > 0 && ctx->sh_world > 1 && !dense_obs) {
+            // iteration 0 (the N0 x N0 pairs) on this rank's rows; the union-find forests of all
+            // ranks are united by mc_shard_import(MC_SHARD_FOREST), which runs the rest
+            TimedScope ts(ctx->timer, s, "s6_pairs");
+            const mc::OvfWork ow{ctx->d_scratch.as<int>(), ctx->d_touched.as<int>(), N0, ctx->d_ovf_n.as<int>() + 1};
+            hipLaunchKernelGGL(mc::k6_pairs, grid_for(N0, mc::kPairWaves, 2048), dim3(256), 0, s, Nlev,
+                               ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->n0_pool, ctx->d_coloff.as<int>(),
+                               ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), ctx->d_n0_vf.as<unsigned long long>(),
+                               FW, ctx->d_thr.as<float>(), 0, ctf, ctx->d_parent.as<int>(),
+                               ctx->d_edges.as<unsigned long long>(), ow, ctx->sh_rank, ctx->sh_world);
+            MC_HIP(hipGetLastError());
+            ctx->sh_pending = MC_SHARD_FOREST;
+            return;
         }
-        ctx->fin_off = cur_off;
-        ctx->fin_len = cur_len;
-        ctx->fin_pool = cur_pool;
-        ctx->fin_vf = cur_vf;
-        ctx->n_iter = nthr;
-        // ---- final point sets (node.py:35), per-object range bitmaps ----
-        const int *dK = Nlev + nthr;
-        const bool point_path = ctx->nodes_from_graph;
-        {
-            TimedScope ts(ctx->timer, s, "s7_points");
-            hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
-            if (point_path) {
-                hipLaunchKernelGGL(mc::k7_obj_of_mask, grid_for(ctx->M), dim3(256), 0, s, ctx->M,
-                                   ctx->d_node_of_mask.as<int>(), ctx->d_final_label.as<int>(),
-                                   ctx->d_obj_of_mask.as<int>());
-                hipLaunchKernelGGL(mc::k7p_points<0>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
-                                   ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
-                                   ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(), nullptr,
-                                   nullptr, stats + ST_OBJOVF);
+        s6_iterations(ctx, 0, false);
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// row-block sharding over processes; kernels in mc_shard_kernels.inl
+// ---------------------------------------------------------------------------------------------
+int mc_shard_set(mc_ctx *ctx, int32_t rank, int32_t world)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(world >= 1 && world <= 1024 && rank >= 0 && rank < world, MC_ERR_INVALID, "bad rank / world");
+        ctx->sh_rank = rank;
+        ctx->sh_world = world;
+        ctx->sh_pending = 0;
+        if (ctx->have_scene) build_s3_lists(ctx, frame_starts(ctx));
+    });
+}
+
+int mc_shard_pending(mc_ctx *ctx, int32_t *phase)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(phase, MC_ERR_INVALID, "null phase");
+        *phase = ctx->sh_pending;
+    });
+}
+
+int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(bytes, MC_ERR_INVALID, "null bytes");
+        MC_REQUIRE(phase == ctx->sh_pending && phase != 0, MC_ERR_STATE, "no such exchange pending");
+        hipStream_t s = ctx->stream;
+        if (phase == MC_SHARD_S3) {
+            const int nr = ctx->sh_r1 - ctx->sh_r0;
+            if (ctx->sh_s3_words < 0) {  // entry offsets of this rank's rows + their total (one host sync)
+                ctx->d_sh_eoff.reserve((nr + 2) * 4);
+                DevBuf dt;
+                dt.reserve(8);
+                mc::scan_device_n(s, ctx->d_crow_len.as<int>() + ctx->sh_r0, ctx->d_sh_eoff.as<int>(), nullptr, nr,
+                                  dt.as<int>());
+                int h = 0;
+                MC_HIP(hipMemcpyAsync(&h, dt.ptr, 4, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipStreamSynchronize(s));
+                ctx->sh_s3_words = 2 + 2 * static_cast<int64_t>(nr) + h;
             }
-            else
-                hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
-                                   ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
-                                   ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
-            hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
-                               ctx->d_nwords.as<int>(), stats + ST_K);
-            mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
-        }
-        sync_stats(ctx);  // bitmap capacity
-        ctx->K = ctx->h_stats[ST_K];
-        const bool use_points = point_path && ctx->h_stats[ST_OBJOVF] == 0;
-        if (point_path && !use_points) {  // a point in > 8 objects: redo the ranges per node
-            hipLaunchKernelGGL(mc::k7_reset, gN, dim3(256), 0, s, N0, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
-            hipLaunchKernelGGL(mc::k7_minmax, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
-                               ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
-                               ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>());
-            hipLaunchKernelGGL(mc::k7_words, gN, dim3(256), 0, s, dK, ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
-                               ctx->d_nwords.as<int>(), stats + ST_K);
-            mc::scan_device_n(s, ctx->d_nwords.as<int>(), ctx->d_woff.as<int>(), dK, 0, stats + ST_WORDS);
-            sync_stats(ctx);
-        }
-        const size_t words = static_cast<size_t>(std::max(ctx->h_stats[ST_WORDS], 1));
-        ctx->d_bm.reserve(words * 8);
-        {
-            TimedScope ts(ctx->timer, s, "s7_points");
-            MC_HIP(hipMemsetAsync(ctx->d_bm.ptr, 0, words * 8, s));
-            if (use_points)
-                hipLaunchKernelGGL(mc::k7p_points<1>, dim3(ceil_div(ctx->P, 256)), dim3(256), 0, s, static_cast<int>(ctx->P),
-                                   ctx->d_pt_off.as<int>(), ctx->d_pt_list.as<unsigned>(), ctx->d_frame_start.as<int>(),
-                                   ctx->d_obj_of_mask.as<int>(), ctx->d_pmin.as<int>(), ctx->d_pmax.as<int>(),
-                                   ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>(), stats + ST_OBJOVF);
-            else
-                hipLaunchKernelGGL(mc::k7_setbits, gW, dim3(256), 0, s, N0, ctx->d_final_label.as<int>(),
-                                   ctx->d_n0_ptoff.as<int>(), ctx->d_n0_ptlen.as<int>(), ctx->n0_pts,
-                                   ctx->d_pmin.as<int>(), ctx->d_woff.as<int>(), ctx->d_bm.as<unsigned long long>());
-            hipLaunchKernelGGL(mc::k7_count, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
-                               ctx->d_bm.as<unsigned long long>(), ctx->d_ptcnt.as<int>());
-            mc::scan_device_n(s, ctx->d_ptcnt.as<int>(), ctx->d_ptoff_out.as<int>(), dK, 0, stats + ST_NPTS);
-            hipLaunchKernelGGL(mc::k7_extract, gK, dim3(256), 0, s, dK, ctx->d_woff.as<int>(),
-                               ctx->d_bm.as<unsigned long long>(), ctx->d_pmin.as<int>(), ctx->d_ptoff_out.as<int>(),
-                               ctx->d_pts_out.as<int>());
+            *bytes = 4 * ctx->sh_s3_words;
+            if (dst_dev)
+                hipLaunchKernelGGL(mc::k_sh_s3_pack, grid_for(std::max(nr, 1) * 64, 256, 2048), dim3(256), 0, s,
+                                   ctx->sh_r0, ctx->sh_r1, ctx->F, ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(),
+                                   ctx->d_useg.as<unsigned char>(), ctx->d_sh_eoff.as<int>(), static_cast<int *>(dst_dev));
+        } else if (phase == MC_SHARD_HIST) {
+            *bytes = 8 * static_cast<int64_t>(ctx->F + 1);
+            if (dst_dev)
+                MC_HIP(hipMemcpyAsync(dst_dev, ctx->d_hist.ptr, *bytes, hipMemcpyDeviceToDevice, s));
+        } else if (phase == MC_SHARD_FOREST) {
+            *bytes = 4 * (static_cast<int64_t>(ctx->N0) + 2);
+            if (dst_dev)
+                hipLaunchKernelGGL(mc::k_sh_forest_export, grid_for(ctx->N0), dim3(256), 0, s, ctx->d_Nlev.as<int>(),
+                                   ctx->d_parent.as<int>(), ctx->d_edges.as<unsigned long long>(),
+                                   static_cast<int *>(dst_dev), ctx->N0);
+        } else {
+            throw McError{MC_ERR_INVALID, "unknown exchange phase"};
         }
         MC_HIP(hipGetLastError());
-        MC_HIP(hipMemcpyAsync(ctx->h_stats, ctx->d_stats.ptr, ST_COUNT * sizeof(int), hipMemcpyDeviceToHost, s));
-        ctx->have_cluster = true;
+    });
+}
+
+int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(phase == ctx->sh_pending && phase != 0, MC_ERR_STATE, "no such exchange pending");
+        MC_REQUIRE(src_dev, MC_ERR_INVALID, "null source");
+        hipStream_t s = ctx->stream;
+        const int W = ctx->sh_world;
+        if (phase == MC_SHARD_S3) {
+            MC_REQUIRE(stride_bytes % 4 == 0 && stride_bytes >= 8, MC_ERR_INVALID, "bad S3 block stride");
+            hipLaunchKernelGGL(mc::k_sh_s3_unpack, dim3(mc::kUnpackWg, W), dim3(256), 0, s,
+                               static_cast<const int *>(src_dev), static_cast<long long>(stride_bytes / 4), ctx->sh_rank,
+                               ctx->F, ctx->d_ctmp.as<int>(), ctx->d_crow_len.as<int>(), ctx->d_useg.as<unsigned char>());
+            MC_HIP(hipGetLastError());
+            ctx->sh_pending = MC_SHARD_HIST;
+            graph_build_tail(ctx);  // undo + S5 replicated, this rank's S4 tiles
+        } else if (phase == MC_SHARD_HIST) {
+            // src: the histogram summed over the ranks
+            MC_HIP(hipMemcpyAsync(ctx->d_hist.ptr, src_dev, 8 * static_cast<size_t>(ctx->F + 1), hipMemcpyDeviceToDevice, s));
+            ctx->sh_pending = 0;
+            graph_build_thresholds(ctx);
+        } else if (phase == MC_SHARD_FOREST) {
+            MC_REQUIRE(stride_bytes % 4 == 0 && stride_bytes >= 4 * (static_cast<int64_t>(ctx->N0) + 2), MC_ERR_INVALID,
+                       "bad FOREST block stride");
+            {
+                TimedScope ts(ctx->timer, s, "s6_pairs");
+                hipLaunchKernelGGL(mc::k_sh_forest_import, dim3(grid_for(ctx->N0, 256, 1024).x, W), dim3(256), 0, s,
+                                   ctx->d_Nlev.as<int>(), static_cast<const int *>(src_dev),
+                                   static_cast<long long>(stride_bytes / 4), ctx->sh_rank, ctx->N0,
+                                   ctx->d_parent.as<int>(), ctx->d_edges.as<unsigned long long>());
+            }
+            MC_HIP(hipGetLastError());
+            ctx->sh_pending = 0;
+            s6_iterations(ctx, 0, true);
+        } else {
+            throw McError{MC_ERR_INVALID, "unknown exchange phase"};
+        }
     });
 }
 

@@ -881,9 +881,12 @@ __global__ __launch_bounds__(256) void k_s4_ranges(const unsigned long long *__r
     }
 }
 
+// shard_rank / shard_world: row-block sharding over processes — this rank takes
+// every shard_world-th tile; the partial histograms are summed by the host's all-reduce.
 __global__ __launch_bounds__(256) void k_s4_hist(const unsigned long long *__restrict__ vf, int M, int FW, int F,
                                                  int nblk, long long ntiles, int R, int HS,
-                                                 const int2 *__restrict__ rng, unsigned long long *__restrict__ hist_g)
+                                                 const int2 *__restrict__ rng, unsigned long long *__restrict__ hist_g,
+                                                 int shard_rank, int shard_world)
 {
     extern __shared__ unsigned char smem_raw[];
     unsigned long long *A = reinterpret_cast<unsigned long long *>(smem_raw);
@@ -896,7 +899,8 @@ __global__ __launch_bounds__(256) void k_s4_hist(const unsigned long long *__res
     const int tj0 = (threadIdx.x & 3) * 16;   // 16 columns
 
     auto row_start = [&](long long r) { return r * nblk - (r * (r - 1)) / 2; };
-    for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (long long tile = static_cast<long long>(blockIdx.x) * shard_world + shard_rank; tile < ntiles;
+         tile += static_cast<long long>(gridDim.x) * shard_world) {
         // triangular decode: tile -> (bi, bj), bi <= bj
         const double nn = nblk;
         long long bi = static_cast<long long>(floor((2.0 * nn + 1.0 - sqrt((2.0 * nn + 1.0) * (2.0 * nn + 1.0) - 8.0 * static_cast<double>(tile))) / 2.0));
@@ -1307,7 +1311,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                                                 const unsigned long long *__restrict__ nvf, int FW,
                                                 const float *__restrict__ thr, int t, float ctf,
                                                 int *__restrict__ parent, unsigned long long *__restrict__ edges,
-                                                OvfWork ow)
+                                                OvfWork ow, int shard_rank, int shard_world)
 {
     __shared__ int s_ovf[kOvfLocal];
     __shared__ int s_novf;
@@ -1327,14 +1331,16 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     short *used = hused[wv];
     unsigned long long nedges = 0;
 
-    if (blockIdx.x * kPairWaves >= N) return;  // uniform: nothing for this block
+    // rows a = shard_rank (mod shard_world): the row-block share of this process
+    if ((blockIdx.x * kPairWaves) * shard_world + shard_rank >= N) return;  // uniform: nothing for this block
     if (threadIdx.x == 0) s_novf = 0;
     for (int s = lane; s < kHashSize; s += 64) {
         keys[s] = -1;
         cnts[s] = 0;
     }
     __syncthreads();
-    for (int a = blockIdx.x * kPairWaves + wv; a < N; a += gridDim.x * kPairWaves) {
+    for (int a = (blockIdx.x * kPairWaves + wv) * shard_world + shard_rank; a < N;
+         a += gridDim.x * kPairWaves * shard_world) {
         if (lane == 0) {
             hfill[wv] = 0;
             hovf[wv] = 0;

@@ -1,17 +1,18 @@
-"""Frame-sharded back-projection over ranks (north_star steps 1-2).
+"""Frame-sharded scenes over ranks (BASELINE north_star).
 
 One process per GPU.  Rank r owns the contiguous frame slice ``frame_slice(F, world, r)``
 and runs S1 (``utils/mask_backprojection.py:70-151``, per frame and independent across
 frames) on its own GPU, so every frame's masks are exactly the single-GPU ones.  The
 per-rank mask CSRs are then all-gathered in rank order.  Slices are contiguous and
 ascending, so the concatenation is the reference's global mask order (frames ascending,
-ids ascending: ``graph/construction.py:46-60``).  S2-S6 then run replicated on every rank:
-each process ends with the full result, as the reference's per-process callers expect
-(``main.py:17-19``).
+ids ascending: ``graph/construction.py:46-60``).  The graph stages then run row-block
+sharded (``graph_shard.ShardedGraph``: S3 rows, S4 histogram tiles and S6's first N0 x N0
+pair evaluation split over the ranks, exchanged as row blocks, one summed histogram and
+union-find forests); every process ends with the full result, as the reference's
+per-process callers expect (``main.py:17-19``).
 
-The only exchange is the all-gather of the mask lists (C2 ≈ 15 MB of point ids, C3 ≈
-190 MB; one collective per array over RCCL/xGMI).  S2-S6 are not sharded: at C2 they
-take ≈1.7 ms on one GPU, less than the collectives the §8(e) count exchange would add.
+Exchanges per scene: the mask lists (C2 ≈ 15 MB of point ids, C3 ≈ 105 MB), the S3 rows
+(C3 ≈ 13 MB), the histogram (8·(F+1) B) and the forests (4·N0 B per rank).
 """
 from __future__ import annotations
 
@@ -87,7 +88,8 @@ class FrameShardedScene:
     frame slice, resident on its GPU.
     """
 
-    def __init__(self, run, num_points: int, num_frames: int, group=None):
+    def __init__(self, run, num_points: int, num_frames: int, group=None, shard_graph: bool = True):
+        from .graph_shard import ShardedGraph
         self.run = run
         self.ctx = run.ctx
         self.P, self.F = int(num_points), int(num_frames)
@@ -97,6 +99,20 @@ class FrameShardedScene:
         self.world = dist.get_world_size(group) if on else 1
         self.lo, self.hi = frame_slice(self.F, self.world, self.rank)
         self.pts = None  # global point ids (kept alive until the graph input copy is done)
+        # the graph stages row-block sharded over the same ranks (shard_graph=False: replicated)
+        self.graph = ShardedGraph(run, group) if shard_graph else None
+
+    def set_local_masks(self, mask_col, mask_label, mask_off, mask_pts: torch.Tensor):
+        """This rank's frames' masks (mask_col relative to the slice) as the S1 output would
+        leave them (the G variant's input): all-gathered into the graph input."""
+        g_col, g_lab, g_off, self.pts = gather_masks(mask_col, mask_label, mask_off, mask_pts, self.lo, self.group)
+        self.mask_index = (g_col, g_lab, g_off)
+        if self.pts.device.type == "cuda":
+            torch.cuda.current_stream(self.pts.device).synchronize()
+            self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, pts_device_ptr=self.pts.data_ptr())
+        else:
+            self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, self.pts.numpy())
+        return g_col, g_lab, g_off
 
     def backproject(self, depth: torch.Tensor, seg: torch.Tensor, intrinsics: torch.Tensor,
                     poses: torch.Tensor, params=None):
@@ -122,11 +138,13 @@ class FrameShardedScene:
             col, lab, off = np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64)
             local = torch.zeros(1, dtype=torch.int32, device=depth.device)
         g_col, g_lab, g_off, self.pts = gather_masks(col, lab, off, local, self.lo, self.group)
+        self.mask_index = (g_col, g_lab, g_off)
         torch.cuda.current_stream(self.pts.device).synchronize()  # the context stream reads them next
         self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, pts_device_ptr=self.pts.data_ptr())
         return g_col, g_lab, g_off
 
     def step(self, mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
              contained_threshold):
-        self.run.step(mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
-                      contained_threshold)
+        runner = self.graph if self.graph is not None else self.run
+        runner.step(mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
+                    contained_threshold)

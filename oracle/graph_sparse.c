@@ -85,8 +85,10 @@ int orcs_s3(int M_in, const int32_t *col, const int32_t *label, const int64_t *o
             const uint8_t *kept, const int32_t *gidx, const uint8_t *boundary, const int64_t *pt_off,
             const int32_t *pt_ent, double mask_visible_threshold, double contained_threshold,
             double undersegment_filter_threshold, int F_cap, int32_t *ct_frame, int32_t *ct_tgt, int32_t *ct_len,
-            uint8_t *useg)
+            uint8_t *useg, const uint8_t *own)
 {
+    /* own (NULL = every mask): evaluate only the input masks g with own[g] != 0 (a rank's row
+     * block in the sharded restatement, tests/oracle_shard_ctx.py) */
     int nU = 0;
 #pragma omp parallel reduction(+ : nU)
     {
@@ -94,7 +96,7 @@ int orcs_s3(int M_in, const int32_t *col, const int32_t *label, const int64_t *o
         int64_t *keys = (int64_t *)malloc((size_t)cap * sizeof(int64_t));
 #pragma omp for schedule(dynamic, 16)
         for (int g = 0; g < M_in; g++) {
-            if (!kept[g]) continue;
+            if (!kept[g] || (own && !own[g])) continue;
             const int r = gidx[g];
             /* valid points (mask minus boundary, :105) and their (frame, mask) entries;
              * key = frame << 32 | label (the column value of pim, :108) */
@@ -181,7 +183,9 @@ void orcs_undo(int M, int F_cap, int32_t *ct_frame, int32_t *ct_tgt, int32_t *ct
 /* ------------------------------------------------------------------------ */
 /* S4 (construction.py:84-86): histogram over all ordered pairs (i, j), i == j
  * included, of O = popcount(VF_i & VF_j), from VF bit rows. */
-void orcs_observer_hist(int M, int FW, const uint64_t *vf, uint64_t *hist, int F)
+/* rank / world: only the pairs (i, j >= i) with i = rank (mod world) — one rank's share in the
+ * sharded restatement; the shares' histograms sum to the whole one */
+void orcs_observer_hist(int M, int FW, const uint64_t *vf, uint64_t *hist, int F, int rank, int world)
 {
     /* per row: first and last non-zero word; a pair whose word ranges do not overlap has O = 0 */
     int32_t *wlo = (int32_t *)malloc((size_t)(M > 0 ? M : 1) * sizeof(int32_t));
@@ -201,6 +205,7 @@ void orcs_observer_hist(int M, int FW, const uint64_t *vf, uint64_t *hist, int F
         uint64_t *h = (uint64_t *)calloc((size_t)F + 1, sizeof(uint64_t));
 #pragma omp for schedule(dynamic, 32)
         for (int i = 0; i < M; i++) {
+            if (i % world != rank) continue;
             const uint64_t *a = vf + (size_t)i * FW;
             int o = 0;
             for (int w = 0; w < FW; w++) o += __builtin_popcountll(a[w]);
@@ -428,4 +433,55 @@ int orcs_cluster(int N0, int FW, int Mn, const uint64_t *vf0, const int64_t *c_o
     free(tedges); free(tedge_n); free(tcap);
     free(vf); free(coff); free(cidx);
     return N;
+}
+
+/* ------------------------------------------------------------------------ */
+/* The edges of one S6 iteration (graph/iterative_clustering.py:20-29) for the rows a with
+ * a = rank (mod world), b > a: the same rule as orcs_cluster.  Writes up to cap (a, b) pairs
+ * into edges (a << 32 | b); returns the number of edges (callers retry with a larger cap). */
+int64_t orcs_level_edges(int N, int FW, int Mn, const uint64_t *vf, const int64_t *coff, const int32_t *cidx,
+                         float th, double ct, int rank, int world, int64_t *edges, int64_t cap)
+{
+    const float ctf = (float)ct;
+    const int dense = !(ct > 0.0);
+    int64_t *moff = (int64_t *)calloc((size_t)Mn + 1, sizeof(int64_t));
+    for (int64_t e = 0; e < coff[N]; e++) moff[cidx[e] + 1]++;
+    for (int m = 0; m < Mn; m++) moff[m + 1] += moff[m];
+    int32_t *mnodes = (int32_t *)malloc((size_t)(moff[Mn] + 1) * sizeof(int32_t));
+    int64_t *mfill = (int64_t *)malloc((size_t)(Mn + 1) * sizeof(int64_t));
+    memcpy(mfill, moff, (size_t)(Mn + 1) * sizeof(int64_t));
+    for (int a = 0; a < N; a++)
+        for (int64_t e = coff[a]; e < coff[a + 1]; e++) mnodes[mfill[cidx[e]]++] = a;
+    free(mfill);
+    int32_t *cnt = (int32_t *)calloc((size_t)N + 1, sizeof(int32_t));
+    int32_t *touched = (int32_t *)malloc((size_t)(N + 1) * sizeof(int32_t));
+    int64_t ne = 0;
+    for (int a = rank; a < N; a += world) {
+        int nt = 0;
+        if (dense) {
+            for (int b = a + 1; b < N; b++) touched[nt++] = b;
+        } else {
+            for (int64_t e = coff[a]; e < coff[a + 1]; e++)
+                for (int64_t q = moff[cidx[e]]; q < moff[cidx[e] + 1]; q++) {
+                    const int b = mnodes[q];
+                    if (b > a && cnt[b]++ == 0) touched[nt++] = b;
+                }
+        }
+        for (int x = 0; x < nt; x++) {
+            const int b = touched[x];
+            const int sv = cnt[b];
+            cnt[b] = 0;
+            int o = 0;
+            for (int w = 0; w < FW; w++) o += __builtin_popcountll(vf[(size_t)a * FW + w] & vf[(size_t)b * FW + w]);
+            volatile float of = (float)o;
+            if (of < th) continue;
+            volatile float den = of + 1e-7f;
+            volatile float rate = (float)sv / den;
+            if (!(rate >= ctf)) continue;
+            if (ne < cap) edges[ne] = ((int64_t)a << 32) | (int64_t)b;
+            ne++;
+        }
+    }
+    free(cnt); free(touched); free(moff); free(mnodes);
+    return ne;
 }

@@ -140,11 +140,15 @@ def lib():
         L.orcs_s3.restype = ctypes.c_int
         L.orcs_s3.argtypes = [ctypes.c_int, _i32p, _i32p, _i64p, _i32p, _u8p, _i32p, _u8p, _i64p, _i32p,
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, _i32p, _i32p, _i32p,
-                              _u8p]
+                              _u8p, ctypes.c_void_p]
         L.orcs_undo.restype = None
         L.orcs_undo.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i32p, _u8p]
         L.orcs_observer_hist.restype = None
-        L.orcs_observer_hist.argtypes = [ctypes.c_int, ctypes.c_int, _u64p, _u64p, ctypes.c_int]
+        L.orcs_observer_hist.argtypes = [ctypes.c_int, ctypes.c_int, _u64p, _u64p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int]
+        L.orcs_level_edges.restype = ctypes.c_int64
+        L.orcs_level_edges.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _i64p, _i32p, ctypes.c_float,
+                                       ctypes.c_double, ctypes.c_int, ctypes.c_int, _i64p, ctypes.c_int64]
         L.orcs_cluster.restype = ctypes.c_int
         L.orcs_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _i64p, _i32p, ctypes.c_int, _f32p,
                                    ctypes.c_double, _i32p, _i32p, _i32p, _i64p, _u64p, _i64p, _i32p]
@@ -329,7 +333,7 @@ def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     useg = np.zeros(max(M, 1), np.uint8)
     L.orcs_s3(M_in, col, label, off, pts, np.ascontiguousarray(kept), gidx, bnd, pt_off, pt_ent,
               float(mask_visible_threshold), float(contained_threshold), float(undersegment_filter_threshold), Fc,
-              ct_frame, ct_tgt, ct_len, useg)
+              ct_frame, ct_tgt, ct_len, useg, None)
     L.orcs_undo(M, Fc, ct_frame, ct_tgt, ct_len, useg)
     ct_frame, ct_tgt = ct_frame.reshape(-1, Fc), ct_tgt.reshape(-1, Fc)
     ct_len, useg = ct_len[:M], useg[:M]
@@ -343,7 +347,7 @@ def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     vfw = np.ascontiguousarray(vfw[:M] if M else vfw)
     t2 = time.perf_counter()
     hist = np.zeros(F + 1, np.uint64)
-    L.orcs_observer_hist(M, FW, vfw, hist, F)
+    L.orcs_observer_hist(M, FW, vfw, hist, F, 0, 1)
     thr, thr_isint = thresholds_from_hist(hist)
     t3 = time.perf_counter()
     if thr is None:
@@ -375,6 +379,21 @@ def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     if timings is not None:
         timings.update(s2=t1 - t0, s3=t2 - t1, s4=t3 - t2, s6=t5 - t4,
                        pairs=int(sum(int(s) ** 2 for s in sizes[:-1])) if T else 0, threads=L.orc_num_threads())
+    return assemble_sparse(P, F, col, label, off, pts, kept, bnd, rr, tt, useg, vfw, hist, thr, thr_isint, node0,
+                           [labels[t, :sizes[t]].copy() for t in range(T)], sizes, final[:N0], edges[:T],
+                           vf_out[:K], co_out[:K + 1], ci_out[:co_out[K]])
+
+
+def assemble_sparse(P, F, col, label, off, pts, kept, bnd, c_rows, c_tgts, useg, vfw, hist, thr, thr_isint, node0,
+                    parts, sizes, final, edges, vf_fin, c_off_fin, c_idx_fin):
+    """The golden-fixture dictionary (without pim_*) from the sparse stages' pieces: c_rows / c_tgts
+    = the contained entries (row, target global mask) after the undo, any order."""
+    M = int(np.count_nonzero(kept))
+    T = len(parts)
+    K = len(c_off_fin) - 1
+    order = np.lexsort((c_tgts, c_rows))
+    rr_s, tt_s = np.asarray(c_rows)[order], np.asarray(c_tgts)[order]
+    N0 = len(node0)
     out = {}
     keep_idx = np.nonzero(kept)[0]
     out["gl_col"], out["gl_label"] = col[keep_idx].copy(), label[keep_idx].copy()
@@ -387,10 +406,10 @@ def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     out["observer_hist"] = hist
     out["num_iters"] = np.array(T, np.int32)
     out["level_sizes"] = sizes
-    out["edge_counts"] = edges[:T].copy()
+    out["edge_counts"] = np.asarray(edges, np.int64)[:T].copy()
     for t in range(T):
-        out[f"part_{t}"] = labels[t, :sizes[t]].copy()
-    fin = final[:N0]
+        out[f"part_{t}"] = np.asarray(parts[t], np.int32)
+    fin = np.asarray(final)[:N0]
     order = np.argsort(fin, kind="stable")
     mo = np.zeros(K + 1, np.int64)
     np.cumsum(np.bincount(fin, minlength=K), out=mo[1:])
@@ -408,11 +427,11 @@ def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
     po = np.zeros(K + 1, np.int64)
     np.cumsum(np.bincount(ko, minlength=K), out=po[1:])
     out["obj_pt_off"], out["obj_pt_idx"] = po, (key % max(P, 1)).astype(np.int32)
-    out["obj_vf_bits"] = np.packbits(_bits_to_bool(vf_out[:K], F), axis=1) if K else np.zeros((0, (F + 7) // 8), np.uint8)
-    out["obj_c_off"], out["obj_c_idx"] = co_out[:K + 1].copy(), ci_out[:co_out[K]].copy()
+    out["obj_vf_bits"] = np.packbits(_bits_to_bool(vf_fin, F), axis=1) if K else np.zeros((0, (F + 7) // 8), np.uint8)
+    out["obj_c_off"], out["obj_c_idx"] = np.asarray(c_off_fin, np.int64).copy(), np.asarray(c_idx_fin, np.int32).copy()
     out["obj_node_info"] = np.array([(T, k) if T else (0, k) for k in range(K)], np.int32).reshape(-1, 2)
     if T:
-        last = labels[T - 1, :sizes[T - 1]]
+        last = np.asarray(parts[T - 1])
         so = np.zeros(K + 1, np.int64)
         np.cumsum(np.bincount(last, minlength=K), out=so[1:])
         out["obj_son_off"], out["obj_son_idx"] = so, np.argsort(last, kind="stable").astype(np.int32)

@@ -5,13 +5,19 @@
 mode "gather" (CPU, gloo): every rank cuts the synthetic scene's masks to its frame slice,
 all-gathers them with maskclustering_amd.frame_shard.gather_masks and saves the result.
 mode "e2e" (GPU, gloo over host tensors: all ranks share cuda:0): every rank back-projects
-its frame slice on the device, all-gathers, runs S2-S6 and saves the canonical outputs.
+its frame slice on the device, all-gathers, runs the row-block sharded S2-S6
+(graph_shard.ShardedGraph) and saves the canonical outputs.
+mode "graph:<shape>:<seed>:<cfg>" (CPU, gloo): every rank holds its frame slice's masks, all-gathers
+them and runs the sharded S2-S6 through ShardedGraph on the oracle-backed stand-in context
+(tests/oracle_shard_ctx.py); saves the canonical outputs.
+mode "gpugraph:<shape>:<seed>" (GPU, gloo, ranks share cuda:0): the same with the HIP context.
 """
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -29,11 +35,48 @@ def local_masks(scene, lo, hi):
     return scene.mask_col[sel] - lo, scene.mask_label[sel], off, pts.astype(np.int32)
 
 
+CFGS = {"scannet": dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
+                       contained_threshold=0.8),
+        "scannetpp": dict(mask_visible_threshold=0.4, undersegment_filter_threshold=0.2, view_consensus_threshold=1,
+                          contained_threshold=0.9)}
+
+
 def main():
     mode, rank, world, port, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        if mode == "gather":
+        if mode.startswith("graph:"):
+            from maskclustering_amd.synthetic import make_shape
+            from oracle_shard_ctx import OracleShardCtx
+            _, shape, seed, cfg = mode.split(":")
+            s = make_shape(shape, seed=int(seed))
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+
+            class Run:  # the GraphRun surface FrameShardedScene / ShardedGraph use
+                ctx = OracleShardCtx()
+
+                def set_masks(self, *a, **kw):
+                    self.ctx.set_masks(*a, **kw)
+
+            run = Run()
+            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
+            sh.step(**CFGS[cfg])
+            np.savez(out, **{k: np.asarray(v) for k, v in run.ctx.canonical().items()})
+        elif mode.startswith("gpugraph:"):
+            from maskclustering_amd.pipeline import GraphRun
+            from maskclustering_amd.synthetic import make_shape
+            _, shape, seed = mode.split(":")
+            s = make_shape(shape, seed=int(seed))
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+            run = GraphRun(0)
+            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            sh.set_local_masks(col, lab, off, torch.from_numpy(pts).cuda())
+            sh.step(**CFGS["scannet"])
+            np.savez(out, **{k: np.asarray(v) for k, v in run.canonical(dense=False).items()})
+        elif mode == "gather":
             from maskclustering_amd.synthetic import make_shape
             s = make_shape("tiny", seed=4)
             lo, hi = frame_slice(s.num_frames, world, rank)

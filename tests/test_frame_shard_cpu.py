@@ -1,5 +1,9 @@
-"""Frame sharding on the CPU: slice arithmetic and the all-gather of
-per-rank mask CSRs over gloo, world_size 2 and 3, against the single-process mask list."""
+"""Frame sharding on the CPU: slice arithmetic, the all-gather of per-rank mask
+CSRs, and the row-block sharded S2-S6 (maskclustering_amd.graph_shard.ShardedGraph: S3 row blocks,
+S4 histogram shares summed, S6 level-0 union-find forests united) over gloo at world sizes 1-3,
+against the single-process result.  The per-rank compute is the sparse oracle behind the same
+exchange API as the HIP library (tests/oracle_shard_ctx.py); the GPU twin is
+tests/test_gpu_frame_shard.py."""
 import numpy as np
 import pytest
 
@@ -29,3 +33,26 @@ def test_gather_equals_global_mask_list(tmp_path, world):
         np.testing.assert_array_equal(z["label"], s.mask_label)
         np.testing.assert_array_equal(z["off"], s.mask_off)
         np.testing.assert_array_equal(z["pts"], s.mask_pts)
+
+
+KW = {"scannet": dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
+                      contained_threshold=0.8),
+      "scannetpp": dict(mask_visible_threshold=0.4, undersegment_filter_threshold=0.2, view_consensus_threshold=1,
+                        contained_threshold=0.9)}
+
+
+@pytest.mark.parametrize("world,shape,seed,cfg", [(1, "tiny", 4, "scannet"), (2, "tiny", 4, "scannet"),
+                                                  (3, "tiny", 5, "scannetpp"), (2, "c1", 1, "scannet"),
+                                                  (3, "c1", 2, "scannet")])
+def test_sharded_graph_equals_single_process(tmp_path, world, shape, seed, cfg):
+    """Every rank ends with exactly the single-process S2-S6 outputs (every stage, canonical form)."""
+    from maskclustering_amd.synthetic import make_shape
+    from oracle import oracle
+    s = make_shape(shape, seed=seed)
+    want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, **KW[cfg])
+    assert int(want["num_iters"]) > 1
+    for out in run_ranks(f"graph:{shape}:{seed}:{cfg}", world, tmp_path):
+        got = np.load(out)
+        assert sorted(got.files) == sorted(want)
+        for k in want:
+            np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)

@@ -1,6 +1,7 @@
-"""Frame-sharded S1 + all-gather + replicated S2-S6 against the
-single-process run on the same frames: two ranks sharing cuda:0 (gloo carries the
-gather; RCCL needs one GPU per rank, the bench's multi-GPU runs use it)."""
+"""Frame-sharded S1 + all-gather + row-block sharded S2-S6 (SURVEY.md §8(e),
+maskclustering_amd/graph_shard.py) through the HIP library against the single-process run on
+the same input: two and three ranks sharing cuda:0 (gloo carries the exchanges; RCCL needs one
+GPU per rank, the bench's multi-GPU runs use it)."""
 import numpy as np
 import pytest
 
@@ -21,6 +22,25 @@ def test_two_rank_frame_sharding_equals_single(tmp_path):
     run.step(0.3, 0.3, 0.9, 0.8)
     want = run.canonical()
     for out in run_ranks("e2e", 2, tmp_path):
+        got = np.load(out)
+        assert sorted(got.files) == sorted(want)
+        for k in want:
+            np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("world,shape,seed", [(2, "c1", 1), (3, "c1", 2)])
+def test_sharded_graph_stages_equal_single(tmp_path, world, shape, seed):
+    """S3 row blocks, S4 histogram shares and S6 level-0 forests over the ranks give every rank the
+    single-GPU result, every stage compared."""
+    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.synthetic import make_shape
+    s = make_shape(shape, seed=seed)
+    run = GraphRun(0)
+    run.set_scene(s)
+    run.step(0.3, 0.3, 0.9, 0.8)
+    want = run.canonical(dense=False)
+    assert int(want["num_iters"]) > 1
+    for out in run_ranks(f"gpugraph:{shape}:{seed}", world, tmp_path):
         got = np.load(out)
         assert sorted(got.files) == sorted(want)
         for k in want:
