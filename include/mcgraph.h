@@ -189,6 +189,12 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
  * connect_threshold: args.view_consensus_threshold (compared in float32).   */
 int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double connect_threshold);
 int mc_cluster_get_info(mc_ctx *ctx, mc_cluster_info *info);
+/* Edge capture for the set-order replay: with capacity > 0 the next
+ * mc_cluster_run records every edge of every iteration as key = t << 48 | a << 24 | b (a < b,
+ * any order); mc_cluster_get_edges gives their count (keys NULL) and the keys
+ * (MC_ERR_UNSUPPORTED when more than capacity were found).  Single-process runs only. */
+int mc_cluster_set_edge_capture(mc_ctx *ctx, int64_t capacity);
+int mc_cluster_get_edges(mc_ctx *ctx, uint64_t *keys, int64_t *n);
 int mc_cluster_get_level_sizes(mc_ctx *ctx, int32_t *sizes /* num_iterations+1 */);
 /* contained-pool slots of every level (sum of the members' row lengths: the merge's row
  * upper bounds), level 0 = nnz of the initial rows; used for the S6 byte models of bench.py */

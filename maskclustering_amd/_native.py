@@ -37,6 +37,7 @@ EXPORTED = [
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
+    "mc_cluster_set_edge_capture", "mc_cluster_get_edges",
 ]
 
 MC_SHARD_S3 = 1
@@ -166,6 +167,8 @@ def load():
         "mc_eval_match_counts": (ctypes.c_int, [vp, i64, i32, vp, vp, i32, vp, vp, vp, vp]),
         "mc_frames_decode": (ctypes.c_int, [vp, i32, i32, i32, vp, dbl, i32, i32, vp, ctypes.c_int, vp, vp]),
         "mc_shard_set": (ctypes.c_int, [vp, i32, i32]),
+        "mc_cluster_set_edge_capture": (ctypes.c_int, [vp, i64]),
+        "mc_cluster_get_edges": (ctypes.c_int, [vp, vp, P(i64)]),
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
         "mc_shard_import": (ctypes.c_int, [vp, i32, vp, i64]),
@@ -377,6 +380,19 @@ class Context:
         out = np.zeros(n_iter + 1, np.int32)
         self._check(self.L.mc_cluster_get_level_sizes(self.h, _ptr(out)))
         return out
+
+    def set_edge_capture(self, capacity):
+        self._check(self.L.mc_cluster_set_edge_capture(self.h, int(capacity)))
+
+    def edges(self):
+        """captured edges as (t, a, b) int64 arrays, sorted by (t, a, b)"""
+        n = ctypes.c_int64()
+        self._check(self.L.mc_cluster_get_edges(self.h, None, ctypes.byref(n)))
+        keys = np.zeros(max(n.value, 1), np.uint64)
+        self._check(self.L.mc_cluster_get_edges(self.h, _ptr(keys), ctypes.byref(n)))
+        keys = np.sort(keys[:n.value])
+        return ((keys >> np.uint64(48)).astype(np.int64), ((keys >> np.uint64(24)) & np.uint64(0xffffff)).astype(np.int64),
+                (keys & np.uint64(0xffffff)).astype(np.int64))
 
     def level_caps(self, n_iter):
         out = np.zeros(n_iter + 1, np.int32)

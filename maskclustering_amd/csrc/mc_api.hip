@@ -126,6 +126,9 @@ struct mc_ctx {
     int s6_nthr = 0;
     bool s6_dense_obs = false;
     float s6_ctf = 0.f;
+    // edge capture for the set-order replay (mc_cluster_set_edge_capture)
+    int64_t cap_edges = 0;
+    DevBuf d_cap_buf, d_cap_cnt;
 
     // ---- post-processing ----
     DevBuf d_pp_posmap;  // one P-entry position map per workgroup, -1 at rest
@@ -299,7 +302,8 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
                       &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out, &ctx->d_owner0,
                       &ctx->d_node_of_mask, &ctx->d_ownA, &ctx->d_ownB, &ctx->d_cap, &ctx->d_obj_of_mask,
-                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen, &ctx->d_sh_eoff};
+                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen, &ctx->d_sh_eoff,
+                      &ctx->d_cap_buf, &ctx->d_cap_cnt};
     for (DevBuf *b : bufs) b->release();
     DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
                          &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg,
@@ -894,6 +898,13 @@ int mc_nodes_set(mc_ctx *ctx, int32_t num_nodes, int32_t num_frames, int32_t num
 // ---------------------------------------------------------------------------------------------
 // S6
 // ---------------------------------------------------------------------------------------------
+static mc::EdgeCap edge_cap(mc_ctx *ctx)
+{
+    if (ctx->cap_edges <= 0) return mc::EdgeCap{nullptr, nullptr, 0};
+    return mc::EdgeCap{ctx->d_cap_buf.as<unsigned long long>(), ctx->d_cap_cnt.as<unsigned long long>(),
+                       static_cast<long long>(ctx->cap_edges)};
+}
+
 // S6 iterations t_begin .. nthr-1 (after_pairs: iteration t_begin's pairs are done) and the final
 // object state; the level-t node arrays are re-derived from the ping-pong pools
 static void s6_iterations(mc_ctx *ctx, int t_begin, bool after_pairs)
@@ -926,13 +937,13 @@ static void s6_iterations(mc_ctx *ctx, int t_begin, bool after_pairs)
             hipLaunchKernelGGL(mc::k6_pairs, gW, dim3(256), 0, s, dN, cur_off, cur_len, cur_pool,
                                ctx->d_coloff.as<int>(), ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), cur_vf, FW,
                                ctx->d_thr.as<float>(), t, ctf, ctx->d_parent.as<int>(),
-                               ctx->d_edges.as<unsigned long long>(), ow, 0, 1);
+                               ctx->d_edges.as<unsigned long long>(), ow, 0, 1, edge_cap(ctx));
         } else {
             TimedScope ts(ctx->timer, s, "s6_pairs");
             hipLaunchKernelGGL(mc::k6_parent_init, gN, dim3(256), 0, s, dN, ctx->d_parent.as<int>());
             hipLaunchKernelGGL(mc::k6_pairs_dense, dim3(4096), dim3(256), 0, s, dN, cur_vf, FW,
                                ctx->d_thr.as<float>(), t, ctx->d_parent.as<int>(),
-                               ctx->d_edges.as<unsigned long long>());
+                               ctx->d_edges.as<unsigned long long>(), edge_cap(ctx));
         }
         {
             TimedScope ts(ctx->timer, s, "s6_components");
@@ -1133,6 +1144,11 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
                            dcap, ctx->nodes_from_graph ? stats + ST_NNZC : nullptr, static_cast<int>(ctx->nnzC0),
                            ctx->d_edges.as<unsigned long long>(), nthr);
 
+        if (ctx->cap_edges > 0) {
+            ctx->d_cap_buf.reserve(static_cast<size_t>(ctx->cap_edges) * 8);
+            ctx->d_cap_cnt.reserve(8);
+            MC_HIP(hipMemsetAsync(ctx->d_cap_cnt.ptr, 0, 8, s));
+        }
         const dim3 gE = grid_for(std::max<int64_t>(N0, ctx->nnzC0)), gC = grid_for(std::max(N0, Mn), 64, 8192);
         const int *cur_pool = ctx->n0_pool, *cur_own = ctx->d_owner0.as<int>();
         if (!dense_obs && nthr > 0) {  // level-0 column lists (nodes contained by each mask)
@@ -1159,7 +1175,8 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
                                ctx->d_n0_off.as<int>(), ctx->d_n0_len.as<int>(), ctx->n0_pool, ctx->d_coloff.as<int>(),
                                ctx->d_collen.as<int>(), ctx->d_colnodes.as<int>(), ctx->d_n0_vf.as<unsigned long long>(),
                                FW, ctx->d_thr.as<float>(), 0, ctf, ctx->d_parent.as<int>(),
-                               ctx->d_edges.as<unsigned long long>(), ow, ctx->sh_rank, ctx->sh_world);
+                               ctx->d_edges.as<unsigned long long>(), ow, ctx->sh_rank, ctx->sh_world,
+                               mc::EdgeCap{nullptr, nullptr, 0});
             MC_HIP(hipGetLastError());
             ctx->sh_pending = MC_SHARD_FOREST;
             return;
@@ -1266,6 +1283,32 @@ int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t str
             s6_iterations(ctx, 0, true);
         } else {
             throw McError{MC_ERR_INVALID, "unknown exchange phase"};
+        }
+    });
+}
+
+int mc_cluster_set_edge_capture(mc_ctx *ctx, int64_t capacity)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(capacity >= 0, MC_ERR_INVALID, "negative capacity");
+        ctx->cap_edges = capacity;
+    });
+}
+
+int mc_cluster_get_edges(mc_ctx *ctx, uint64_t *keys, int64_t *n)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(ctx->have_cluster && n, MC_ERR_STATE, "no clustering result");
+        MC_REQUIRE(ctx->cap_edges > 0, MC_ERR_STATE, "edge capture is off");
+        unsigned long long cnt = 0;
+        MC_HIP(hipMemcpyAsync(&cnt, ctx->d_cap_cnt.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+        MC_HIP(hipStreamSynchronize(ctx->stream));
+        *n = static_cast<int64_t>(cnt);
+        if (keys && cnt) {
+            MC_REQUIRE(static_cast<int64_t>(cnt) <= ctx->cap_edges, MC_ERR_UNSUPPORTED,
+                       "more edges than the capture capacity (raise it and run again)");
+            MC_HIP(hipMemcpyAsync(keys, ctx->d_cap_buf.ptr, cnt * 8, hipMemcpyDeviceToHost, ctx->stream));
+            MC_HIP(hipStreamSynchronize(ctx->stream));
         }
     });
 }

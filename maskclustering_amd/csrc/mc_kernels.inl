@@ -1291,6 +1291,22 @@ constexpr int kPairWaves = 4, kPairBatch = 8, kTestBatch = 4, kTestWords = 4;
 #define MC_ABLATE_PAIRS 0
 #endif
 
+// Optional capture of every edge (replay of the reference's set orders):
+// key = t << 48 | a << 24 | b with a < b; buf == nullptr: off.
+struct EdgeCap {
+    unsigned long long *buf;
+    unsigned long long *cnt;
+    long long cap;
+};
+__device__ __forceinline__ void edge_capture(EdgeCap ec, int t, int a, int b)
+{
+    if (!ec.buf) return;
+    const unsigned long long pos = atomicAdd(ec.cnt, 1ull);
+    if (pos < static_cast<unsigned long long>(ec.cap))
+        ec.buf[pos] = (static_cast<unsigned long long>(t) << 48) | (static_cast<unsigned long long>(a) << 24) |
+                      static_cast<unsigned long long>(b);
+}
+
 struct OvfWork {
     int *scratch, *touched;  // kOvfSlots dense counters / touched lists of N0 ints (zero at rest)
     int N0;
@@ -1302,7 +1318,7 @@ __device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf,
                                      const int *__restrict__ coloff, const int *__restrict__ collen,
                                      const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
                                      int FW, EdgeRule er, int *__restrict__ parent,
-                                     unsigned long long *__restrict__ edges_t);
+                                     unsigned long long *__restrict__ edges_t, EdgeCap ec, int t);
 
 __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, const int *__restrict__ n_off,
                                                 const int *__restrict__ n_len, const int *__restrict__ pool,
@@ -1311,7 +1327,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                                                 const unsigned long long *__restrict__ nvf, int FW,
                                                 const float *__restrict__ thr, int t, float ctf,
                                                 int *__restrict__ parent, unsigned long long *__restrict__ edges,
-                                                OvfWork ow, int shard_rank, int shard_world)
+                                                OvfWork ow, int shard_rank, int shard_world, EdgeCap ec)
 {
     __shared__ int s_ovf[kOvfLocal];
     __shared__ int s_novf;
@@ -1452,6 +1468,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                 for (int r = 0; r < kTestBatch; r++) {
                     if (bn[r] >= 0 && edge_ok(ob[r], sc[r], er)) {
                         nedges++;
+                        edge_capture(ec, t, a, bn[r]);
                         if (MC_ABLATE_PAIRS != 1 && MC_ABLATE_PAIRS != 5) uf_unite(parent, a, bn[r]);
                     }
                 }
@@ -1473,7 +1490,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     __syncthreads();
     if (s_novf > 0)  // uniform
         pairs_overflow_local(ow, s_ovf, s_novf, n_off, n_len, pool, coloff, collen, colnodes, nvf, FW, er, parent,
-                             edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL);
+                             edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, ec, t);
 }
 
 // K4b: nodes whose partner set overflowed the LDS hash, by a whole workgroup with dense global
@@ -1483,7 +1500,7 @@ __device__ void pairs_overflow_node(int a, const int *__restrict__ n_off, const 
                                     const int *__restrict__ collen, const int *__restrict__ colnodes,
                                     const unsigned long long *__restrict__ nvf, int FW, EdgeRule er,
                                     int *__restrict__ parent, int *__restrict__ scr, int *__restrict__ tl,
-                                    int *ntouch, unsigned long long &nedges)
+                                    int *ntouch, unsigned long long &nedges, EdgeCap ec, int t)
 {
     if (threadIdx.x == 0) *ntouch = 0;
     __syncthreads();
@@ -1510,6 +1527,7 @@ __device__ void pairs_overflow_node(int a, const int *__restrict__ n_off, const 
         for (int w = 0; w < FW; w++) ob += __popcll(va[w] & vb[w]);
         if (edge_ok(ob, sv, er)) {
             nedges++;
+            edge_capture(ec, t, a, bnode);
             uf_unite(parent, a, bnode);
         }
     }
@@ -1527,7 +1545,7 @@ __device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf,
                                      const int *__restrict__ coloff, const int *__restrict__ collen,
                                      const int *__restrict__ colnodes, const unsigned long long *__restrict__ nvf,
                                      int FW, EdgeRule er, int *__restrict__ parent,
-                                     unsigned long long *__restrict__ edges_t)
+                                     unsigned long long *__restrict__ edges_t, EdgeCap ec, int t)
 {
     __shared__ int s_slot, ntouch;
     __shared__ int ws[4];
@@ -1545,7 +1563,7 @@ __device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf,
     unsigned long long nedges = 0;
     for (int q = 0; q < novf; q++)
         pairs_overflow_node(ovf_nodes[q], n_off, n_len, pool, coloff, collen, colnodes, nvf, FW, er, parent, scr, tl,
-                            &ntouch, nedges);
+                            &ntouch, nedges, ec, t);
     const int ne = block_sum<256>(static_cast<int>(nedges), ws);  // (its barriers order the clears before the release)
     if (threadIdx.x == 0) {
         if (ne) spread_add(edges_t, static_cast<unsigned long long>(ne));
@@ -1557,7 +1575,7 @@ __device__ void pairs_overflow_local(OvfWork ow, const int *ovf_nodes, int novf,
 __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN,
                                                       const unsigned long long *__restrict__ nvf, int FW,
                                                       const float *__restrict__ thr, int t, int *__restrict__ parent,
-                                                      unsigned long long *__restrict__ edges)
+                                                      unsigned long long *__restrict__ edges, EdgeCap ec)
 {
     __shared__ int ws[4];
     const int N = *dN;
@@ -1571,6 +1589,7 @@ __global__ __launch_bounds__(256) void k6_pairs_dense(const int *__restrict__ dN
         for (int w = 0; w < FW; w++) ob += __popcll(nvf[static_cast<size_t>(a) * FW + w] & nvf[static_cast<size_t>(b) * FW + w]);
         if (!(static_cast<float>(ob) < thr_f)) {  // ct <= 0: every rate >= ct
             nedges++;
+            edge_capture(ec, t, a, b);
             uf_unite(parent, a, b);
         }
     }

@@ -11,11 +11,28 @@ on-device merge).  Nodes that come straight from this package's
 ``mask_graph_construction`` are clustered from the device graph without a
 host round trip; any other node list is packed into CSR rows first.
 
-``mask_list`` of a merged node lists its members' masks in ascending member
-order and ``point_ids`` is the union set; the reference's order inside these
-containers follows CPython set iteration and is not reproduced.
+Two contracts for the containers whose order follows CPython set iteration in the
+reference:
+
+* default (canonical): ``mask_list`` of a merged node lists its members' masks in
+  ascending member order and ``point_ids`` is the union set, built once from the
+  device's sorted ids.  Contents are the reference's; their iteration order is not
+  (post_process numbers its DBSCAN objects by ``list(point_ids)``, graph/node.py:45,
+  so its exports can differ at DBSCAN border ties and in object order).
+* replay (``replay=True``, or MASKCLUSTERING_REPLAY_SET_ORDER=1): the device also
+  records every edge of every iteration; the host then replays exactly what the
+  reference's Python does with them: ``nx.connected_components``' BFS from the smallest
+  unseen node over ascending neighbours (``from_numpy_array``'s row-major insertion,
+  iterative_clustering.py:7,32) into a set, and ``Node.create_node_from_list``'s
+  ``mask_list +=`` / chained ``set.union`` / ``son_node_info.add`` in that set's
+  iteration order (graph/node.py:31-36).  The containers are then the reference's
+  objects in CPython's own iteration order, so post_process exports what the reference
+  exports (tests/test_gpu_api.py, golden from the reference's own S1->S6->post_process).
+  It costs what the reference's set unions cost (a fraction of a second at C2).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
@@ -54,7 +71,67 @@ def _pack(ctx, nodes):
     return F, M
 
 
-def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug):
+REPLAY_SET_ORDER = os.environ.get("MASKCLUSTERING_REPLAY_SET_ORDER", "0") == "1"
+_EDGE_CAP0 = 1 << 22
+
+
+def _replay(nodes, T, sizes, edges, parts):
+    """The reference's container building, level by level (see the module docstring).  Returns
+    [(mask_list, point_ids, son_node_info)] of the final nodes, in component order."""
+    level = [(n.mask_list, n.point_ids, n.node_info) for n in nodes]
+    tt, aa, bb = edges
+    bounds = np.searchsorted(tt, np.arange(T + 1))
+    out = None
+    for t in range(T):
+        N = int(sizes[t])
+        a, b = aa[bounds[t]:bounds[t + 1]], bb[bounds[t]:bounds[t + 1]]
+        src, dst = np.concatenate([a, b]), np.concatenate([b, a])
+        order = np.lexsort((dst, src))
+        off = np.zeros(N + 1, np.int64)
+        np.cumsum(np.bincount(src, minlength=N), out=off[1:])
+        nbr = dst[order].tolist()
+        adj = [nbr[off[v]:off[v + 1]] for v in range(N)]
+        seen = bytearray(N)
+        comps = []
+        for v in range(N):                       # nx.connected_components: `for v in G`
+            if seen[v]:
+                continue
+            c = {v}                              # _plain_bfs
+            nextlevel = [v]
+            while nextlevel:
+                thislevel = nextlevel
+                nextlevel = []
+                for u in thislevel:
+                    for w in adj[u]:
+                        if w not in c:
+                            c.add(w)
+                            nextlevel.append(w)
+            for u in c:
+                seen[u] = 1
+            comps.append(c)
+        lab = np.empty(N, np.int64)
+        for k, c in enumerate(comps):
+            lab[list(c)] = k
+        if not np.array_equal(lab, parts[t]):
+            raise RuntimeError(f"replay: components of iteration {t} differ from the device's")
+        new = []
+        for k, c in enumerate(comps):            # Node.create_node_from_list (graph/node.py:24-37)
+            mask_list = []
+            point_ids = set()
+            son_node_info = set()
+            for i in c:
+                ml, pts, info = level[i]
+                mask_list += ml
+                point_ids = point_ids.union(pts)
+                son_node_info.add(info)
+            new.append((mask_list, point_ids, (t + 1, k), son_node_info))
+        level = [(m, p, i) for m, p, i, _ in new]
+        out = [(m, p, s) for m, p, _, s in new]
+    return out
+
+
+def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay=None):
+    replay = REPLAY_SET_ORDER if replay is None else bool(replay)
     if debug:
         print('====> Start iterative clustering')
     if len(observer_num_thresholds) == 0:
@@ -70,7 +147,19 @@ def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debu
         construction._current["token"] = None  # set_nodes replaces the device graph's nodes
         F, M = _pack(ctx, nodes)
     thr = np.array([float(t) for t in observer_num_thresholds], np.float32)
-    ctx.cluster(thr, connect_threshold)
+    if replay:
+        cap = _EDGE_CAP0
+        while True:
+            ctx.set_edge_capture(cap)
+            ctx.cluster(thr, connect_threshold)
+            n = int(sum(ctx.edge_counts(ctx.cluster_info().num_iterations)))
+            if n <= cap:
+                break
+            cap = n  # S6 re-runs on the same level-0 nodes with room for every edge
+        edges = ctx.edges()
+        ctx.set_edge_capture(0)
+    else:
+        ctx.cluster(thr, connect_threshold)
     ci = ctx.cluster_info()
     T = ci.num_iterations
     sizes = ctx.level_sizes(T)
@@ -80,6 +169,11 @@ def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debu
     obj = ctx.objects(ci, F)
     last = ctx.partition(T - 1, int(sizes[T - 1]))
     vf = bits_to_bool(obj["vf_bits"], F)
+    if replay:
+        parts = [ctx.partition(t, int(sizes[t])) for t in range(T)]
+        rep = _replay(nodes, T, sizes, edges, parts)
+        return [Node.compact(ml, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M, pts, (T, k), sons)
+                for k, (ml, pts, sons) in enumerate(rep)]
     out = []
     for k in range(ci.num_objects):
         members = obj["mask_idx"][obj["mask_off"][k]:obj["mask_off"][k + 1]]

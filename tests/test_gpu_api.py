@@ -103,3 +103,69 @@ def test_dropin_frame_backprojection_matches_reference():
             seen += 1
         assert set(fpts) == set().union(*info.values()) if info else fpts == []
     assert seen == len(z["mpc_col"])
+
+
+def _pp_golden(cfg):
+    return np.load(os.path.join(GOLDEN, f"e2e_pp_small_{cfg}.npz"))
+
+
+def _exports(objects, mpc, frames, pfm, fids, thr):
+    from maskclustering_amd.utils import post_process as pp
+    pts, masks = pp.post_process_objects(objects, mpc, frames.scene_points, np.asarray(pfm), fids, thr)
+    return [np.asarray(p, np.int64) for p in pts], [[(str(f), int(m), float(c)) for f, m, c in ml] for ml in masks]
+
+
+def _golden_exports(g):
+    oo, oi = g["obj_pt_off"], g["obj_pt_idx"]
+    qo = g["obj_mask_off"]
+    pts = [oi[oo[k]:oo[k + 1]].astype(np.int64) for k in range(len(oo) - 1)]
+    masks = [[(str(f), int(m), float(c)) for f, m, c in zip(g["obj_mask_frame"][qo[k]:qo[k + 1]],
+                                                          g["obj_mask_id"][qo[k]:qo[k + 1]],
+                                                          g["obj_mask_cov"][qo[k]:qo[k + 1]])]
+             for k in range(len(qo) - 1)]
+    return pts, masks
+
+
+@pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
+def test_dropin_main_path_exports_match_reference(cfg):
+    """main.py:17-21 through the drop-ins with the set-order replay (S1 -> S6 -> post_process) exports
+    exactly what the reference's own run exports (tests/golden/make_e2e_pp_golden.py): the same
+    objects in the same order, their point ids in the same order, the same mask lists and
+    coverages; every final node's list(point_ids) is the reference's iteration order."""
+    import make_api_golden as ag
+    from maskclustering_amd.graph import construction, iterative_clustering
+    z, frames, fids, args = _load(f"api_small_{cfg}")
+    g = _pp_golden(cfg)
+    nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
+                                                                ag.FrameDataset(frames, fids, PinholeIntrinsic))
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False, replay=True)
+    no, ni = g["node_order_off"], g["node_order_idx"]
+    assert len(objects) == len(no) - 1
+    for k, o in enumerate(objects):
+        assert [int(x) for x in o.point_ids] == ni[no[k]:no[k + 1]].tolist(), f"node {k} point order"
+        assert ";".join(f"{f}_{m}" for f, m in o.mask_list) == str(g["node_mask_lists"][k]), f"node {k} mask_list"
+    gp, gm = _exports(objects, mpc, frames, pfm, fids, float(g["pp_thr"]))
+    wp, wm = _golden_exports(g)
+    assert len(gp) == len(wp) > 5
+    for k in range(len(wp)):
+        np.testing.assert_array_equal(gp[k], wp[k], err_msg=f"object {k}")
+        assert gm[k] == wm[k], f"object {k} masks"
+
+
+@pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
+def test_dropin_default_exports_canonical(cfg):
+    """Without the replay the drop-in's containers hold the reference's contents in another order;
+    on these scenes the exported objects still equal the reference's as sets of point sets with
+    the same mask lists (order-free comparison: the canonical contract)."""
+    import make_api_golden as ag
+    from maskclustering_amd.graph import construction, iterative_clustering
+    z, frames, fids, args = _load(f"api_small_{cfg}")
+    g = _pp_golden(cfg)
+    nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
+                                                                ag.FrameDataset(frames, fids, PinholeIntrinsic))
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+    gp, gm = _exports(objects, mpc, frames, pfm, fids, float(g["pp_thr"]))
+    wp, wm = _golden_exports(g)
+    got = sorted((tuple(sorted(p.tolist())), tuple(sorted(m))) for p, m in zip(gp, gm))
+    want = sorted((tuple(sorted(p.tolist())), tuple(sorted(m))) for p, m in zip(wp, wm))
+    assert got == want
