@@ -49,6 +49,8 @@ struct mc_ctx {
     bool own_stream = false;
     hipStream_t side = nullptr;                 // S3: workgroup-per-mask kernel beside the wave kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t cls_stream[4] = {};             // S1 denoise: the LDS size classes run side by side
+    hipEvent_t ev_cls[4] = {};
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
@@ -271,6 +273,10 @@ int mc_ctx_create(int device, mc_ctx **out)
         MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+        for (int c = 0; c < 4; c++) {
+            MC_HIP(hipStreamCreateWithFlags(&ctx->cls_stream[c], hipStreamNonBlocking));
+            MC_HIP(hipEventCreateWithFlags(&ctx->ev_cls[c], hipEventDisableTiming));
+        }
         MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stats), ST_COUNT * sizeof(int), hipHostMallocDefault));
         ctx->d_stats.reserve(ST_COUNT * sizeof(int));
         MC_HIP(hipMemset(ctx->d_stats.ptr, 0, ST_COUNT * sizeof(int)));
@@ -324,6 +330,10 @@ void mc_ctx_destroy(mc_ctx *ctx)
     if (ctx->side) (void)hipStreamSynchronize(ctx->side), (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    for (int c = 0; c < 4; c++) {
+        if (ctx->cls_stream[c]) (void)hipStreamSynchronize(ctx->cls_stream[c]), (void)hipStreamDestroy(ctx->cls_stream[c]);
+        if (ctx->ev_cls[c]) (void)hipEventDestroy(ctx->ev_cls[c]);
+    }
     delete ctx;
 }
 
@@ -1475,6 +1485,18 @@ enum BpStat : int {
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
+// u16 entries of per-workgroup eps-neighbour lists before class cls's region
+inline size_t nbl_offset(const mc_ctx *ctx, int cls)
+{
+    const size_t per_cls[4] = {static_cast<size_t>(mc::BpLdsClass<512>::kWgPerCu) * 512,
+                               static_cast<size_t>(mc::BpLdsClass<1024>::kWgPerCu) * 1024,
+                               static_cast<size_t>(mc::BpLdsClass<2048>::kWgPerCu) * 2048,
+                               static_cast<size_t>(mc::BpLdsClass<3072>::kWgPerCu) * 3072};
+    size_t o = 0;
+    for (int c = 0; c < cls; c++) o += per_cls[c];
+    return o * static_cast<size_t>(ctx->num_cu) * mc::kBpNbCap;
+}
+
 void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
 {
     const size_t px = static_cast<size_t>(fb) * H * W + 1;
@@ -1496,8 +1518,8 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_moff.reserve((slots + 1) * 4);
     ctx->d_slot_box.reserve(slots * 6 * 4);
     ctx->d_cls_list.reserve(5 * slots * 4);
-    // per-workgroup eps-neighbour lists: N x WGs per CU is 2048 for the 512/1024/2048 classes, 3072 for the lean one
-    ctx->d_nbl.reserve(static_cast<size_t>(ctx->num_cu) * 3072 * mc::kBpNbCap * 2);
+    // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
+    ctx->d_nbl.reserve(nbl_offset(ctx, 4) * 2);
     ctx->d_lean.reserve(static_cast<size_t>(ctx->num_cu) * mc::kBpLeanInts<3072> * 4);
     if (ctx->bp_px_cap < px) {
         ctx->d_pix_list.reserve(px * 4);
@@ -1567,11 +1589,13 @@ template <int N>
 void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, const mc::BpDev &dv)
 {
     using C = mc::BpLdsClass<N>;
+    // the classes run concurrently: each has its own region of per-workgroup neighbour lists
     hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
-                       ctx->d_nbl.as<unsigned short>(), ctx->d_lean.as<int>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
-                       ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
+                       ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>(),
+                       ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
+                       ctx->d_slot_box.as<float>());
 }
 const int kBpStatInit[BS_COUNT] = {INT_MAX};  // the rest zero
 
@@ -1666,7 +1690,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         int min_cls = 0;
         if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(4, std::max(0, atoi(e)));
         // frames per batch: bounded pixel capacity of the per-slot arrays
-        size_t budget = static_cast<size_t>(48) << 20;
+        // (≈ 180 B of per-batch arrays per pixel: 192 M pixels ≈ 35 GB of HBM; a C3 frame is 2.76 M
+        // pixels, so a batch holds ~70 frames and the per-batch sync and slot tails amortise)
+        size_t budget = static_cast<size_t>(192) << 20;
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         const int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
         bp_reserve(ctx, FB, H, W, nbands, s);
@@ -1751,10 +1777,17 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_avg.as<double>(), ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(),
                                    ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
                 MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
-                bp_denoise_class<3072>(ctx, s, 3, ncap, st, dv);
-                bp_denoise_class<2048>(ctx, s, 2, ncap, st, dv);
-                bp_denoise_class<1024>(ctx, s, 1, ncap, st, dv);
-                bp_denoise_class<512>(ctx, s, 0, ncap, st, dv);
+                // the LDS classes side by side, each on its own stream: a class with few slots
+                // (the large ones) leaves most CUs to the others instead of serialising the batch
+                for (int c = 0; c < 4; c++) MC_HIP(hipStreamWaitEvent(ctx->cls_stream[c], ctx->ev_fork, 0));
+                bp_denoise_class<3072>(ctx, ctx->cls_stream[3], 3, ncap, st, dv);
+                bp_denoise_class<2048>(ctx, ctx->cls_stream[2], 2, ncap, st, dv);
+                bp_denoise_class<1024>(ctx, ctx->cls_stream[1], 1, ncap, st, dv);
+                bp_denoise_class<512>(ctx, ctx->cls_stream[0], 0, ncap, st, dv);
+                for (int c = 0; c < 4; c++) {
+                    MC_HIP(hipEventRecord(ctx->ev_cls[c], ctx->cls_stream[c]));
+                    MC_HIP(hipStreamWaitEvent(s, ctx->ev_cls[c], 0));
+                }
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
 
             }
