@@ -375,18 +375,89 @@ class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic
 class FrameDataset:  # dataset/scannet.py:34-73 over arrays
     def __init__(self, fr, frame_ids):
         self.fr, self.col = fr, {f: c for c, f in enumerate(frame_ids)}
+        for x in (fr.depth, fr.seg, fr.poses):
+            x.flags.writeable = False
 
     def get_intrinsics(self, f):
         return PinholeIntrinsic(*self.fr.intrinsics[self.col[f]])
 
+    # decoded frames served from memory as read-only views (a dataset with its frames cached; the
+    # reference's ScanNetDataset decodes files here, dataset/scannet.py:48-64)
     def get_extrinsic(self, f):
-        return self.fr.poses[self.col[f]].copy()
+        return self.fr.poses[self.col[f]]
 
     def get_depth(self, f):
-        return self.fr.depth[self.col[f]].copy()
+        return self.fr.depth[self.col[f]]
 
     def get_segmentation(self, f, align_with_depth=False):
-        return self.fr.seg[self.col[f]].copy()
+        return self.fr.seg[self.col[f]]
+
+
+def run_api(a):
+    """--variant api: the reference-API boundary exactly as main.py:17-21 calls it, on the synthetic
+    RGB-D scene whose dataset object serves decoded frames from host memory (dataset/scannet.py:
+    get_depth / get_segmentation / get_intrinsics / get_extrinsic): one step =
+    mask_graph_construction + iterative_clustering (+ post_process's compute, without the file
+    export).  ms_per_step is the wall time of that Python call sequence, host packing and PCIe
+    included; the device part is the S1-S6 of the e2e variant."""
+    import cProfile
+    import pstats
+
+    import torch
+    from maskclustering_amd.graph import construction, iterative_clustering
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    from maskclustering_amd.utils import post_process as pp
+
+    t0 = time.perf_counter()
+    fr = make_frames_shape(a.shape, seed=a.seed, device="cuda:0")
+    fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
+    log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
+    args = SimpleNamespace(debug=False, point_filter_threshold=0.5, **CFG)
+    ds = FrameDataset(fr, fids)
+    parts = {"graph": [], "cluster": [], "post_process": []}
+
+    def step():
+        t = time.perf_counter()
+        nodes, thr, mpc, pfm = construction.mask_graph_construction(args, fr.scene_points, fids, ds)
+        t1 = time.perf_counter()
+        objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+        t2 = time.perf_counter()
+        out = pp.post_process_objects(objects, mpc, fr.scene_points, pfm, fids, args.point_filter_threshold) \
+            if a.with_pp else None
+        t3 = time.perf_counter()
+        parts["graph"].append(t1 - t)
+        parts["cluster"].append(t2 - t1)
+        parts["post_process"].append(t3 - t2)
+        return nodes, objects, out
+
+    for _ in range(max(a.warmup, 1)):
+        nodes, objects, _ = step()
+    for v in parts.values():
+        v.clear()
+    torch.cuda.synchronize()
+    walls = []
+    for _ in range(a.steps):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t)
+    if a.profile:
+        pr = cProfile.Profile()
+        pr.enable()
+        step()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
+    ms = 1e3 * float(np.mean(walls))
+    res = {"metric": "reference-API graph path ms per scene (main.py:17-21 through the drop-in modules)",
+           "value": round(ms, 3), "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(ms, 3), "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
+           "dtype": "int32", "data": "synthetic",
+           "config": {"workload": f"{a.shape}: synthetic RGB-D scene, {fr.num_frames} frames "
+                                  f"{fr.depth.shape[2]}x{fr.depth.shape[1]}, P={fr.num_points}, "
+                                  f"{len(nodes)} nodes -> {len(objects)} objects", "variant": "api",
+                      "with_post_process": bool(a.with_pp),
+                      "part_ms": {k: round(1e3 * float(np.mean(v)), 3) for k, v in parts.items() if v}}}
+    print(json.dumps(res), flush=True)
 
 
 def run_post_process(a):
@@ -485,7 +556,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--variant", choices=["g", "e2e", "pp"], default="e2e")
+    ap.add_argument("--variant", choices=["g", "e2e", "pp", "api"], default="e2e")
+    ap.add_argument("--with-pp", action="store_true", help="api: include post_process's compute")
+    ap.add_argument("--profile", action="store_true", help="api: cProfile one extra step to stderr")
     ap.add_argument("--shape", default="c3")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -496,6 +569,8 @@ def main():
     args = ap.parse_args()
     if args.variant == "pp":
         return run_post_process(args)
+    if args.variant == "api":
+        return run_api(args)
 
     import torch
     import torch.distributed as dist

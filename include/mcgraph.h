@@ -143,6 +143,13 @@ int mc_scene_set_points(mc_ctx *ctx, int64_t num_points, const float *xyz, int o
 int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
                    const uint8_t *seg, const double *intrinsics, const double *poses, int on_device,
                    const mc_bp_params *params);
+/* the same, with one host pointer per frame (depth_frames[f]: float32 [H,W], seg_frames[f]: uint8
+ * [H,W]) as a dataset hands them out (dataset/scannet.py:48-64, construction.py:47-48): the frames
+ * are staged through pinned memory by host threads while the previous chunk's DMA runs, with no
+ * [F,H,W] host copy.  intrinsics / poses as above (host).                                        */
+int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                          const float *const *depth_frames, const uint8_t *const *seg_frames,
+                          const double *intrinsics, const double *poses, const mc_bp_params *params);
 int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info);
 /* kept masks in frame order then id order: mask_col (frame index), mask_label
  * (id), mask_off [M+1], mask_pts = sorted unique scene ids (mask_info[id], :148) */
@@ -293,6 +300,18 @@ int mc_frames_decode(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t wi
                      const uint16_t *depth /* F*H*W */, double depth_scale, int32_t seg_height, int32_t seg_width,
                      const uint8_t *seg /* F*seg_height*seg_width */, int inputs_on_device,
                      float *depth_out /* device, F*H*W */, uint8_t *seg_out /* device, F*H*W */);
+
+/* ---- open-vocabulary label query ---------------------------------------
+ * Replaces the per-object compute of semantics/open-voc_query.py:32-53: for object k, the mean of
+ * its representative masks' features (rows obj_rows[obj_off[k] .. obj_off[k+1]) of the
+ * num_rows x dim float32 table, summed in that order), its similarity with every label text
+ * feature (num_labels x dim), exp(temperature * sim), the softmax and its first argmax (NaN
+ * first, like np.argmax; -1 for an object without representative masks).  Float32 like the
+ * reference except the dot products, which are summed in float64 and rounded once (the
+ * reference's BLAS order is its own). */
+int mc_openvoc_query(mc_ctx *ctx, int32_t num_objects, const int64_t *obj_off, const int32_t *obj_rows,
+                     int32_t num_rows, int32_t dim, const float *features, int32_t num_labels,
+                     const float *label_features, float temperature, int32_t *out_label);
 
 #ifdef __cplusplus
 }

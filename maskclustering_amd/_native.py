@@ -32,12 +32,12 @@ EXPORTED = [
     "mc_nodes_set",
     "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_level_caps", "mc_cluster_get_partition",
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
-    "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_get_info",
+    "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_frames", "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
-    "mc_cluster_set_edge_capture", "mc_cluster_get_edges",
+    "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query",
 ]
 
 MC_SHARD_S3 = 1
@@ -156,6 +156,7 @@ def load():
         "mc_bp_params_default": (None, [P(BpParams)]),
         "mc_scene_set_points": (ctypes.c_int, [vp, i64, vp, ctypes.c_int]),
         "mc_backproject": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, ctypes.c_int, P(BpParams)]),
+        "mc_backproject_frames": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, P(BpParams)]),
         "mc_backproject_get_info": (ctypes.c_int, [vp, P(BpInfo)]),
         "mc_backproject_get_masks": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "mc_backproject_copy_points_device": (ctypes.c_int, [vp, vp]),
@@ -168,6 +169,7 @@ def load():
         "mc_frames_decode": (ctypes.c_int, [vp, i32, i32, i32, vp, dbl, i32, i32, vp, ctypes.c_int, vp, vp]),
         "mc_shard_set": (ctypes.c_int, [vp, i32, i32]),
         "mc_cluster_set_edge_capture": (ctypes.c_int, [vp, i64]),
+        "mc_openvoc_query": (ctypes.c_int, [vp, i32, vp, vp, i32, i32, vp, i32, vp, ctypes.c_float, vp]),
         "mc_cluster_get_edges": (ctypes.c_int, [vp, vp, P(i64)]),
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
@@ -467,6 +469,23 @@ def _bp_methods():
         self._check(self.L.mc_backproject(self.h, F, H, W, _ptr(depth), _ptr(seg), _ptr(K), _ptr(T), 0,
                                           ctypes.byref(prm)))
 
+    def backproject_frames(self, depth_frames, seg_frames, intrinsics, poses, params: BpParams | None = None):
+        """S1 from per-frame host arrays (depth float32 [H,W], seg uint8 [H,W] each, C-contiguous),
+        staged to the device without an [F,H,W] host copy (mc_backproject_frames)."""
+        prm = params or bp_params()
+        F = len(depth_frames)
+        assert len(seg_frames) == F and F > 0
+        H, W = depth_frames[0].shape
+        for d, sg in zip(depth_frames, seg_frames):
+            if d.shape != (H, W) or sg.shape != (H, W) or d.dtype != np.float32 or sg.dtype != np.uint8 \
+                    or not d.flags.c_contiguous or not sg.flags.c_contiguous:
+                raise ValueError("frames must be C-contiguous float32 depth / uint8 seg arrays of one shape")
+        dp = (ctypes.c_void_p * F)(*[d.ctypes.data for d in depth_frames])
+        sp = (ctypes.c_void_p * F)(*[sg.ctypes.data for sg in seg_frames])
+        K = np.ascontiguousarray(intrinsics, np.float64).reshape(F, 4)
+        T = np.ascontiguousarray(poses, np.float64).reshape(F, 16)
+        self._check(self.L.mc_backproject_frames(self.h, F, H, W, dp, sp, _ptr(K), _ptr(T), ctypes.byref(prm)))
+
     def bp_info(self) -> BpInfo:
         info = BpInfo()
         self._check(self.L.mc_backproject_get_info(self.h, ctypes.byref(info)))
@@ -504,7 +523,7 @@ def _bp_methods():
     def use_backprojection(self):
         self._check(self.L.mc_scene_use_backprojection(self.h))
 
-    for f in (set_points, backproject, bp_info, bp_masks, bp_mask_index, bp_points_to_device, bp_candidates,
+    for f in (set_points, backproject, backproject_frames, bp_info, bp_masks, bp_mask_index, bp_points_to_device, bp_candidates,
               use_backprojection):
         setattr(Context, f.__name__, f)
 
@@ -567,6 +586,25 @@ def _eval_methods():
 
 
 _eval_methods()
+
+
+def _ov_methods():
+    def openvoc_query(self, obj_off, obj_rows, features, label_features, temperature=100.0):
+        """semantics/open-voc_query.py:32-50 on the device: label index of every object (-1: none)."""
+        off = np.ascontiguousarray(obj_off, np.int64)
+        rows = np.ascontiguousarray(obj_rows, np.int32)
+        feats = np.ascontiguousarray(features, np.float32)
+        labs = np.ascontiguousarray(label_features, np.float32)
+        K = len(off) - 1
+        out = np.zeros(max(K, 1), np.int32)
+        self._check(self.L.mc_openvoc_query(self.h, K, _ptr(off), _ptr(rows), feats.shape[0], labs.shape[1],
+                                            _ptr(feats), labs.shape[0], _ptr(labs), float(temperature), _ptr(out)))
+        return out[:K]
+
+    Context.openvoc_query = openvoc_query
+
+
+_ov_methods()
 
 
 def _io_methods():

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mc_internal.hpp"
@@ -14,6 +15,7 @@
 #include "mc_eval_kernels.inl"
 #include "mc_io_kernels.inl"
 #include "mc_shard_kernels.inl"
+#include "mc_ov_kernels.inl"
 
 using mc::DevBuf;
 using mc::McError;
@@ -54,6 +56,11 @@ struct mc_ctx {
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
+    // pinned staging ring of mc_backproject_frames (two chunks, ping-pong)
+    char *h_stage[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
+    hipEvent_t ev_stage[2] = {};
+    bool stage_used[2] = {false, false};
 
     // ---- scene ----
     bool have_scene = false, have_graph = false, have_nodes = false, have_cluster = false;
@@ -326,6 +333,10 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    for (int b = 0; b < 2; b++) {
+        if (ctx->h_stage[b]) (void)hipHostFree(ctx->h_stage[b]);
+        if (ctx->ev_stage[b]) (void)hipEventDestroy(ctx->ev_stage[b]);
+    }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side), (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
@@ -1637,6 +1648,97 @@ int mc_scene_set_points(mc_ctx *ctx, int64_t num_points, const float *xyz, int o
     });
 }
 
+// Per-frame host arrays -> one device array [F, frame_bytes]: the frames are copied by host
+// threads into a pinned chunk while the previous chunk's DMA runs (pageable hipMemcpy would stage
+// through the runtime's own buffers on one thread, and np.stack would add a full host copy).
+static void stage_frames(mc_ctx *ctx, const void *const *frames, size_t frame_bytes, int F, char *dst)
+{
+    if (!F || !frame_bytes) return;
+    hipStream_t s = ctx->stream;
+    const size_t want = std::max<size_t>(frame_bytes, static_cast<size_t>(32) << 20);
+    if (ctx->stage_bytes < want) {
+        for (int b = 0; b < 2; b++) {
+            if (ctx->stage_used[b]) MC_HIP(hipEventSynchronize(ctx->ev_stage[b]));
+            if (ctx->h_stage[b]) MC_HIP(hipHostFree(ctx->h_stage[b]));
+            ctx->h_stage[b] = nullptr;
+            ctx->stage_used[b] = false;
+        }
+        ctx->stage_bytes = 0;
+        for (int b = 0; b < 2; b++) {
+            MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stage[b]), want, hipHostMallocDefault));
+            if (!ctx->ev_stage[b]) MC_HIP(hipEventCreateWithFlags(&ctx->ev_stage[b], hipEventDisableTiming));
+        }
+        ctx->stage_bytes = want;
+    }
+    int nthreads = static_cast<int>(std::min(8u, std::max(1u, std::thread::hardware_concurrency())));
+    if (const char *e = getenv("MC_STAGE_THREADS")) nthreads = std::max(1, std::min(64, atoi(e)));
+    const int per = static_cast<int>(std::max<size_t>(1, ctx->stage_bytes / frame_bytes));
+    int b = 0;
+    for (int f0 = 0; f0 < F; f0 += per, b ^= 1) {
+        const int n = std::min(per, F - f0);
+        if (ctx->stage_used[b]) MC_HIP(hipEventSynchronize(ctx->ev_stage[b]));  // its last DMA is done
+        char *buf = ctx->h_stage[b];
+        const size_t total = static_cast<size_t>(n) * frame_bytes;
+        auto copy_range = [&](size_t lo, size_t hi) {
+            while (lo < hi) {
+                const size_t f = lo / frame_bytes, o = lo % frame_bytes;
+                const size_t len = std::min(hi - lo, frame_bytes - o);
+                memcpy(buf + lo, static_cast<const char *>(frames[f0 + f]) + o, len);
+                lo += len;
+            }
+        };
+        const int nt = static_cast<int>(std::min<size_t>(nthreads, std::max<size_t>(1, total >> 22)));  // >= 4 MB each
+        if (nt <= 1) {
+            copy_range(0, total);
+        } else {
+            std::vector<std::thread> th;
+            const size_t step = (total + nt - 1) / nt;
+            for (int t = 1; t < nt; t++) th.emplace_back(copy_range, std::min(total, t * step), std::min(total, (t + 1) * step));
+            copy_range(0, std::min(total, step));
+            for (auto &x : th) x.join();
+        }
+        MC_HIP(hipMemcpyAsync(dst + static_cast<size_t>(f0) * frame_bytes, buf, total, hipMemcpyHostToDevice, s));
+        MC_HIP(hipEventRecord(ctx->ev_stage[b], s));
+        ctx->stage_used[b] = true;
+    }
+}
+
+int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                          const float *const *depth_frames, const uint8_t *const *seg_frames,
+                          const double *intrinsics, const double *poses, const mc_bp_params *params)
+{
+    const int rc = guarded(ctx, [&] {
+        MC_REQUIRE(num_frames >= 0 && height > 0 && width > 0, MC_ERR_INVALID, "bad frame sizes");
+        MC_REQUIRE(num_frames == 0 || (depth_frames && seg_frames && intrinsics && poses), MC_ERR_INVALID,
+                   "null frame arrays");
+        for (int f = 0; f < num_frames; f++)
+            MC_REQUIRE(depth_frames[f] && seg_frames[f], MC_ERR_INVALID, "null frame array");
+        const int F = num_frames;
+        const size_t HW = static_cast<size_t>(height) * width;
+        if (!F) return;
+        hipStream_t s = ctx->stream;
+        ctx->d_in_depth.reserve(F * HW * 4);
+        ctx->d_in_seg.reserve(F * HW);
+        ctx->d_in_intr.reserve(F * 4 * 8ull);
+        ctx->d_in_pose.reserve(F * 16 * 8ull);
+        MC_HIP(hipMemcpyAsync(ctx->d_in_intr.ptr, intrinsics, F * 4 * 8ull, hipMemcpyHostToDevice, s));
+        MC_HIP(hipMemcpyAsync(ctx->d_in_pose.ptr, poses, F * 16 * 8ull, hipMemcpyHostToDevice, s));
+        stage_frames(ctx, reinterpret_cast<const void *const *>(depth_frames), HW * 4, F,
+                     static_cast<char *>(ctx->d_in_depth.ptr));
+        stage_frames(ctx, reinterpret_cast<const void *const *>(seg_frames), HW, F,
+                     static_cast<char *>(ctx->d_in_seg.ptr));
+    });
+    if (rc != MC_OK) return rc;
+    if (!num_frames) {
+        static const float zf = 0.f;
+        static const uint8_t zs = 0;
+        static const double zd[16] = {};
+        return mc_backproject(ctx, 0, height, width, &zf, &zs, zd, zd, 0, params);
+    }
+    return mc_backproject(ctx, num_frames, height, width, ctx->d_in_depth.as<float>(), ctx->d_in_seg.as<uint8_t>(),
+                          ctx->d_in_intr.as<double>(), ctx->d_in_pose.as<double>(), 1, params);
+}
+
 int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
                    const uint8_t *seg, const double *intrinsics, const double *poses, int on_device,
                    const mc_bp_params *params)
@@ -1922,9 +2024,9 @@ int mc_debug_bp_slot_times(unsigned *out, int n)
 }
 int mc_debug_bp_stamps(unsigned long long *out32)
 {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 32 * 8) != hipSuccess) return MC_ERR_HIP;
-    static const unsigned long long zero[32] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_stamps), zero, 32 * 8) == hipSuccess ? MC_OK : MC_ERR_HIP;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 40 * 8) != hipSuccess) return MC_ERR_HIP;
+    static const unsigned long long zero[40] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_stamps), zero, 40 * 8) == hipSuccess ? MC_OK : MC_ERR_HIP;
 }
 #endif
 
@@ -2384,6 +2486,47 @@ int mc_frames_decode(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t wi
         }
         MC_HIP(hipStreamSynchronize(s));
         ctx->timer.collect();
+    });
+}
+
+// ---------------------------------------------------------------------------------------------
+// open-vocabulary label query
+// ---------------------------------------------------------------------------------------------
+int mc_openvoc_query(mc_ctx *ctx, int32_t num_objects, const int64_t *obj_off, const int32_t *obj_rows,
+                     int32_t num_rows, int32_t dim, const float *features, int32_t num_labels,
+                     const float *label_features, float temperature, int32_t *out_label)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(num_objects >= 0 && num_rows >= 0 && dim > 0 && dim <= 12288 && num_labels > 0, MC_ERR_INVALID,
+                   "bad sizes");
+        MC_REQUIRE(obj_off && out_label && label_features && (num_rows == 0 || features), MC_ERR_INVALID, "null array");
+        MC_REQUIRE(obj_off[0] == 0, MC_ERR_INVALID, "obj_off[0] != 0");
+        const int64_t nr = obj_off[num_objects];
+        for (int k = 0; k < num_objects; k++) MC_REQUIRE(obj_off[k + 1] >= obj_off[k], MC_ERR_INVALID, "obj_off not ascending");
+        for (int64_t i = 0; i < nr; i++)
+            MC_REQUIRE(obj_rows[i] >= 0 && obj_rows[i] < num_rows, MC_ERR_INVALID, "feature row out of range");
+        if (!num_objects) return;
+        hipStream_t s = ctx->stream;
+        DevBuf doff, drows, dfeat, dlab, dsim, dout;
+        doff.reserve((num_objects + 1) * 8);
+        drows.reserve((nr + 1) * 4);
+        dfeat.reserve(static_cast<size_t>(num_rows) * dim * 4 + 4);
+        dlab.reserve(static_cast<size_t>(num_labels) * dim * 4);
+        dsim.reserve(static_cast<size_t>(num_objects) * num_labels * 4);
+        dout.reserve(static_cast<size_t>(num_objects) * 4);
+        MC_HIP(hipMemcpyAsync(doff.ptr, obj_off, (num_objects + 1) * 8, hipMemcpyHostToDevice, s));
+        if (nr) MC_HIP(hipMemcpyAsync(drows.ptr, obj_rows, nr * 4, hipMemcpyHostToDevice, s));
+        if (num_rows) MC_HIP(hipMemcpyAsync(dfeat.ptr, features, static_cast<size_t>(num_rows) * dim * 4, hipMemcpyHostToDevice, s));
+        MC_HIP(hipMemcpyAsync(dlab.ptr, label_features, static_cast<size_t>(num_labels) * dim * 4, hipMemcpyHostToDevice, s));
+        {
+            TimedScope ts(ctx->timer, s, "ov_query");
+            hipLaunchKernelGGL(mc::k_ov_query, dim3(num_objects), dim3(256), dim * sizeof(float), s, num_objects,
+                               doff.as<long long>(), drows.as<int>(), dim, dfeat.as<float>(), num_labels,
+                               dlab.as<float>(), temperature, dsim.as<float>(), dout.as<int>());
+        }
+        MC_HIP(hipGetLastError());
+        MC_HIP(hipMemcpyAsync(out_label, dout.ptr, static_cast<size_t>(num_objects) * 4, hipMemcpyDeviceToHost, s));
+        MC_HIP(hipStreamSynchronize(s));
     });
 }
 

@@ -652,7 +652,7 @@ __device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restric
 // Diagnostic build only (-DMC_BP_STAMPS): per-step real-time-clock (100 MHz) totals of k_bp_denoise, summed
 // over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
 #ifdef MC_BP_STAMPS
-__device__ unsigned long long g_bp_stamps[32];
+__device__ unsigned long long g_bp_stamps[40];
 __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks), last batch
 #define BP_STAMP(k)                                                                      \
     do {                                                                                 \
@@ -689,13 +689,19 @@ constexpr int kBpLdsN = 3072;  // largest LDS class
 constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
 template <int N>
 struct BpLdsClass;
+#ifndef MC_BP_WG512
+#define MC_BP_WG512 4  // workgroups per CU the 512 class is compiled for (register budget)
+#endif
+#ifndef MC_BP_WG1024
+#define MC_BP_WG1024 2
+#endif
 template <>
 struct BpLdsClass<512> {
-    static constexpr int T = 256, kWgPerCu = 4;
+    static constexpr int T = 256, kWgPerCu = MC_BP_WG512;
 };
 template <>
 struct BpLdsClass<1024> {
-    static constexpr int T = 512, kWgPerCu = 2;
+    static constexpr int T = 512, kWgPerCu = MC_BP_WG1024;
 };
 template <>
 struct BpLdsClass<2048> {
@@ -866,6 +872,9 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 // kept points of a point with >= 20 kept eps-neighbours are among them (every other point is at
 // distance >= eps).  Workgroups take slots of their size class from a ticket counter.
 // ---------------------------------------------------------------------------------------------
+#ifndef MC_KNN_RING
+#define MC_KNN_RING 1  // 0: points whose eps list holds < k kept points skip the grid rings (whole-cloud scan)
+#endif
 #ifndef MC_ABLATE_BP
 #define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union,
                         // 3 = k-NN list pass without the sorted inserts, 4 = k-NN list pass on self only
@@ -1198,6 +1207,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         __syncthreads();
 #ifdef MC_BP_STAMPS
         if (t == 0) atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(s_ndef));
+#endif
+#if MC_KNN_RING == 0
+        for (int f = t; f < s_ndef; f += T) sfb[atomicAdd(&sfb[kFbCount], 1)] = spar[sring[f]];
+        if (false)
 #endif
         for (int f = t; f < s_ndef; f += T) {
             const int q = sring[f];

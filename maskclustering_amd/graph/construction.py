@@ -30,9 +30,25 @@ from .. import _device
 from .._native import MC_ERR_EMPTY_OBSERVERS, MC_ERR_INVALID, McError
 from ..pipeline import bits_to_bool, bool_to_bits
 from ..utils import mask_backprojection as _mb
-from .node import Node
+from .node import Level0Source, Node
 
 _tokens = itertools.count(1)
+
+
+class PointFrameMatrix(np.ndarray):
+    """point_frame_matrix (construction.py:40,52): the reference's bool [P, F] array, read-only (the
+    reference's callers only read it), carrying the packed bits it was unpacked from so that
+    utils.post_process hands them to the device without re-packing 60 MB at C2."""
+
+    @classmethod
+    def from_bits(cls, words, F):
+        a = bits_to_bool(words, F).view(cls)
+        a._mc_bits = np.ascontiguousarray(words)
+        a.flags.writeable = False
+        return a
+
+    def __array_finalize__(self, obj):
+        self._mc_bits = None  # views / copies / results of operations carry no bits
 
 
 class GraphHandle:
@@ -49,14 +65,18 @@ class GraphHandle:
 _current = {"token": None}
 
 
-def _stack_frames(frame_list, dataset):
+def _read_frames(frame_list, dataset):
+    """the dataset calls of construction.py:47-48 / mask_backprojection.py:71-80, per frame (the
+    arrays are handed to the device as they are, no [F,H,W] host stack)"""
     depth, seg, K, T = [], [], [], []
     for frame_id in frame_list:
-        depth.append(np.asarray(dataset.get_depth(frame_id), np.float32))
-        seg.append(_device.seg_u8(dataset.get_segmentation(frame_id, align_with_depth=True)))
+        depth.append(np.ascontiguousarray(dataset.get_depth(frame_id), np.float32))
+        seg.append(np.ascontiguousarray(_device.seg_u8(dataset.get_segmentation(frame_id, align_with_depth=True))))
         K.append(_device.intrinsics_tuple(dataset.get_intrinsics(frame_id)))
         T.append(np.asarray(dataset.get_extrinsic(frame_id), np.float64).reshape(4, 4))
-    return np.stack(depth), np.stack(seg), np.stack(K), np.stack(T)
+    if any(d.shape != depth[0].shape or s.shape != depth[0].shape for d, s in zip(depth, seg)):
+        raise ValueError("all frames must share one depth / segmentation shape")
+    return depth, seg, np.stack(K), np.stack(T)
 
 
 def _backproject_all(scene_points, frame_list, dataset):
@@ -66,9 +86,9 @@ def _backproject_all(scene_points, frame_list, dataset):
         ctx.backproject(np.zeros((0, 1, 1), np.float32), np.zeros((0, 1, 1), np.uint8), np.zeros((0, 4)),
                         np.zeros((0, 4, 4)), _mb.params())
         return ctx
-    depth, seg, K, T = _stack_frames(frame_list, dataset)
+    depth, seg, K, T = _read_frames(frame_list, dataset)
     try:
-        ctx.backproject(depth, seg, K, T, _mb.params())
+        ctx.backproject_frames(depth, seg, K, T, _mb.params())
     except McError as e:
         if e.code == MC_ERR_INVALID and "depth_trunc" in str(e):
             raise IndexError(str(e)) from e
@@ -77,16 +97,81 @@ def _backproject_all(scene_points, frame_list, dataset):
 
 
 class MaskPointClouds(dict):
-    """``{f"{frame_id}_{mask_id}": set}`` exactly as the reference builds it (:57), which also
-    keeps the CSR it was made from (``csr``: key -> row, offsets, point ids) so that
-    utils.post_process can hand the device the rows instead of re-reading every set.  Any
-    assignment or deletion drops the CSR; post_process also checks the set sizes."""
+    """``{f"{frame_id}_{mask_id}": set}`` exactly as the reference builds it (:57), built lazily: the
+    sets are made from the device's CSR rows on first access (one set per mask: 3.7 M Python ints
+    at C2 that the graph path itself never reads).  Iteration, ``len``, ``in``, ``keys`` / ``values``
+    / ``items`` and every mutator see the full mapping in the reference's insertion order (the
+    global mask order).  ``csr`` (key -> row, offsets, point ids) lets utils.post_process hand the
+    device the rows instead of re-reading the sets; any mutation of the mapping drops it, and
+    post_process checks the sizes of the sets that were materialised."""
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         self.csr = None
+        self._lazy = {}
+        self._made = {}
+        self._order = None
+
+    @classmethod
+    def from_csr(cls, keys, off, pts):
+        m = cls()
+        m._lazy = {k: g for g, k in enumerate(keys)}
+        m._order = list(keys)
+        m._off, m._pts = off, pts
+        m.csr = (dict(m._lazy), off, pts)
+        return m
+
+    def _make(self, k):
+        g = self._lazy.pop(k)
+        v = self._made[k] = set(self._pts[self._off[g]:self._off[g + 1]].tolist())
+        dict.__setitem__(self, k, v)
+        return v
+
+    def original(self, k):
+        """the set first stored under ``k`` (a level-0 node's point_ids aliases it even after the
+        mapping is changed, as in the reference)"""
+        v = self._made.get(k)
+        if v is None:
+            v = self._make(k) if k in self._lazy else self[k]
+        return v
+
+    def __missing__(self, k):
+        if k in self._lazy:
+            return self._make(k)
+        raise KeyError(k)
+
+    def is_materialized(self, k):
+        return dict.__contains__(self, k)
+
+    def _materialize(self):
+        """every set made, dict order = the reference's insertion order"""
+        if self._order is None:
+            return
+        if self._lazy:
+            items = [(k, dict.get(self, k) if dict.__contains__(self, k) else None) for k in self._order]
+            dict.clear(self)
+            for k, v in items:
+                if v is None:
+                    g = self._lazy.pop(k)
+                    v = self._made[k] = set(self._pts[self._off[g]:self._off[g + 1]].tolist())
+                dict.__setitem__(self, k, v)
+        self._order = None
+
+    def __contains__(self, k):
+        return dict.__contains__(self, k) or k in self._lazy
+
+    def __len__(self):
+        return dict.__len__(self) + len(self._lazy)
+
+    def __iter__(self):
+        self._materialize()
+        return dict.__iter__(self)
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
 
     def _drop(self):
+        self._materialize()
         self.csr = None
 
     def __setitem__(self, k, v):
@@ -97,6 +182,30 @@ class MaskPointClouds(dict):
         self._drop()
         super().__delitem__(k)
 
+    def __eq__(self, other):
+        self._materialize()
+        return dict.__eq__(self, other)
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    __hash__ = None
+
+    def __repr__(self):
+        self._materialize()
+        return dict.__repr__(self)
+
+    def __reduce__(self):
+        self._materialize()
+        return (dict, (dict(self),))
+
+
+def _reading(name):
+    def f(self, *a, **kw):
+        self._materialize()
+        return getattr(dict, name)(self, *a, **kw)
+    f.__name__ = name
+    return f
 
 
 def _dropping(name):
@@ -107,6 +216,8 @@ def _dropping(name):
     return f
 
 
+for _n in ("keys", "values", "items", "copy", "__reversed__"):
+    setattr(MaskPointClouds, _n, _reading(_n))
 for _n in ("update", "pop", "popitem", "clear", "setdefault"):
     setattr(MaskPointClouds, _n, _dropping(_n))
 
@@ -114,14 +225,8 @@ for _n in ("update", "pop", "popitem", "clear", "setdefault"):
 def _mask_sets(ctx, frame_list):
     col, lab, off, pts = ctx.bp_masks()
     gl = [(frame_list[c], np.uint8(m)) for c, m in zip(col.tolist(), lab.tolist())]
-    mpc = MaskPointClouds()
-    row = {}
-    for g, (fid, mid) in enumerate(gl):
-        key = f"{fid}_{mid}"
-        dict.__setitem__(mpc, key, set(pts[off[g]:off[g + 1]].tolist()))
-        row[key] = g
-    mpc.csr = (row, np.asarray(off, np.int64), np.asarray(pts))
-    return gl, mpc
+    keys = [f"{fid}_{mid}" for fid, mid in gl]
+    return gl, keys, MaskPointClouds.from_csr(keys, np.asarray(off, np.int64), np.asarray(pts))
 
 
 def _thresholds(thr, isint):
@@ -131,22 +236,24 @@ def _thresholds(thr, isint):
 def _build(args, scene_points, frame_list, dataset):
     _current["token"] = None  # the device graph is about to be replaced
     ctx = _backproject_all(scene_points, frame_list, dataset)
-    gl_in, mpc = _mask_sets(ctx, frame_list)
+    gl_in, keys_in, mpc = _mask_sets(ctx, frame_list)
     ctx.use_backprojection()
     ctx.build(args.mask_visible_threshold, args.contained_threshold, args.undersegment_filter_threshold)
     gi = ctx.graph_info()
     # frames whose union is empty are skipped (construction.py:50-51): global list = kept input masks
     gidx = ctx.global_masks(gi.num_masks)
     gl = [gl_in[i] for i in gidx.tolist()]
-    return ctx, gi, gl, mpc
+    keys = [keys_in[i] for i in gidx.tolist()]
+    return ctx, gi, gl, keys, mpc
 
 
 def mask_graph_construction(args, scene_points, frame_list, dataset):
     if args.debug:
         print('start building point in mask matrix')
-    ctx, gi, gl, mpc = _build(args, scene_points, frame_list, dataset)
+    ctx, gi, gl, keys, mpc = _build(args, scene_points, frame_list, dataset)
     P, F, M = gi.num_points, gi.num_frames, gi.num_masks
-    pfm = bits_to_bool(ctx.point_frame_bits(P, F), F)
+    pfm_bits = ctx.point_frame_bits(P, F)
+    pfm = PointFrameMatrix.from_bits(pfm_bits, F)
     if gi.threshold_status == MC_ERR_EMPTY_OBSERVERS:
         raise IndexError("index -1 is out of bounds for axis 0 with size 0")  # np.percentile([]) (:89)
     thr, isint = ctx.thresholds()
@@ -156,20 +263,16 @@ def mask_graph_construction(args, scene_points, frame_list, dataset):
     token = next(_tokens)
     _current["token"] = token
     handle = GraphHandle(token, len(node0), F, M, P)
-    nodes = []
-    for i, g in enumerate(node0.tolist()):
-        fid, mid = gl[g]
-        n = Node.compact([(fid, mid)], vf[g], c_idx[c_off[g]:c_off[g + 1]], M, mpc[f"{fid}_{mid}"], (0, i), None)
-        n._graph = handle
-        n._level0 = i
-        nodes.append(n)
+    src = Level0Source(gl, keys, vf, c_off, c_idx, M, mpc)
+    level0 = Node.level0
+    nodes = [level0(src, i, g, handle) for i, g in enumerate(node0.tolist())]
     return nodes, _thresholds(thr, isint), mpc, pfm
 
 
 def build_point_in_mask_matrix(args, scene_points, frame_list, dataset):
     """construction.py:22-64 -> (boundary_points, point_in_mask_matrix, mask_point_clouds,
     point_frame_matrix, global_frame_mask_list)."""
-    ctx, gi, gl, mpc = _build(args, scene_points, frame_list, dataset)
+    ctx, gi, gl, keys, mpc = _build(args, scene_points, frame_list, dataset)
     P, F = gi.num_points, gi.num_frames
     boundary = set(np.nonzero(ctx.boundary(P))[0].tolist())
     pim = ctx.point_in_mask(P, F).copy()

@@ -15,8 +15,8 @@ Two contracts for the containers whose order follows CPython set iteration in th
 reference:
 
 * default (canonical): ``mask_list`` of a merged node lists its members' masks in
-  ascending member order and ``point_ids`` is the union set, built once from the
-  device's sorted ids.  Contents are the reference's; their iteration order is not
+  ascending member order and ``point_ids`` is the union set, built from the device's
+  sorted ids on its first read.  Contents are the reference's; their iteration order is not
   (post_process numbers its DBSCAN objects by ``list(point_ids)``, graph/node.py:45,
   so its exports can differ at DBSCAN border ties and in object order).
 * replay (``replay=True``, or MASKCLUSTERING_REPLAY_SET_ORDER=1): the device also
@@ -38,7 +38,7 @@ import numpy as np
 
 from .. import _device
 from ..pipeline import bits_to_bool, bool_to_bits
-from .node import Node
+from .node import Node, level0_masks
 
 
 def _fast_path(nodes):
@@ -49,8 +49,9 @@ def _fast_path(nodes):
     if h is None or h.token != construction._current["token"] or len(nodes) != h.num_nodes:
         return None
     for i, n in enumerate(nodes):
-        if getattr(n, "_graph", None) is not h or n._level0 != i or getattr(n, "_vf", None) is None \
-                or getattr(n, "_cids", None) is None:
+        d = getattr(n, "__dict__", None)   # (an untouched level-0 node has only its graph identity)
+        if d is None or d.get("_graph") is not h or d.get("_level0") != i or d.get("_vf", 0) is None \
+                or d.get("_cids", 0) is None:
             return None
     return h
 
@@ -179,8 +180,8 @@ def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debu
         members = obj["mask_idx"][obj["mask_off"][k]:obj["mask_off"][k + 1]]
         mask_list = []
         for i in members.tolist():
-            mask_list += nodes[i].mask_list
+            mask_list += level0_masks(nodes[i])
         sons = {(T - 1, int(j)) for j in np.nonzero(last == k)[0].tolist()}
-        out.append(Node.compact(mask_list, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M,
-                                set(obj["pt_idx"][obj["pt_off"][k]:obj["pt_off"][k + 1]].tolist()), (T, k), sons))
+        out.append(Node.compact_lazy_points(mask_list, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M,
+                                            obj["pt_idx"][obj["pt_off"][k]:obj["pt_off"][k + 1]], (T, k), sons))
     return out

@@ -45,6 +45,48 @@ class Node:
         n.son_node_info = son_node_info
         return n
 
+    @classmethod
+    def level0(cls, src, i, g, graph):
+        """init_nodes (construction.py:66-78) node ``i`` (global mask ``g``) of a device graph.  Only
+        the graph identity is stored; ``mask_list``, the rows, ``node_info`` and ``point_ids`` (the
+        mask's set in ``mask_point_clouds``: the same object, as in the reference) are made from
+        ``src`` (a Level0Source) on first read."""
+        n = cls.__new__(cls)
+        n.__dict__.update(_graph=graph, _level0=i, _src0=(src, g))
+        return n
+
+    def __getattr__(self, name):
+        d = self.__dict__
+        if name not in _LAZY0 or "_src0" not in d:
+            raise AttributeError(f"'Node' object has no attribute '{name}'")
+        src, g = d["_src0"]
+        v = d[name] = _lazy0(src, g, d["_level0"], name)
+        return v
+
+    @classmethod
+    def compact_lazy_points(cls, mask_list, vf_bool, contained_ids, num_masks, point_array, node_info, son_node_info):
+        """compact() whose ``point_ids`` set is made from ``point_array`` (the device's sorted ids)
+        on first read"""
+        n = cls.compact(mask_list, vf_bool, contained_ids, num_masks, None, node_info, son_node_info)
+        del n.__dict__["_point_ids"]
+        n.__dict__["_pts_arr"] = point_array
+        return n
+
+    @property
+    def point_ids(self):
+        d = self.__dict__
+        if "_point_ids" not in d:
+            if "_src0" in d:
+                src, g = d["_src0"]
+                d["_point_ids"] = src.mpc.original(src.keys[g])
+            elif "_pts_arr" in d:
+                d["_point_ids"] = set(d.pop("_pts_arr").tolist())
+        return d.get("_point_ids")
+
+    @point_ids.setter
+    def point_ids(self, v):
+        self.__dict__["_point_ids"] = v
+
     @property
     def visible_frame(self):
         if self._visible_frame is None:
@@ -117,6 +159,42 @@ class Node:
             pcld = _PointCloud()
             pcld.points = points
         return pcld, point_ids
+
+
+class Level0Source:
+    """The arrays level-0 nodes of one device graph are made from: per global mask its
+    (frame_id, mask_id), mask_point_clouds key, visible-frame row and contained ids."""
+
+    def __init__(self, gl, keys, vf, c_off, c_idx, num_masks, mpc):
+        self.gl, self.keys, self.vf, self.c_off, self.c_idx = gl, keys, vf, c_off, c_idx
+        self.M, self.mpc = num_masks, mpc
+
+
+_LAZY0 = ("mask_list", "_vf", "_cids", "_M", "_visible_frame", "_contained_mask", "node_info", "son_node_info")
+
+
+def _lazy0(src, g, i, k):
+    if k == "mask_list":
+        return [src.gl[g]]
+    if k == "_vf":
+        return src.vf[g]
+    if k == "_cids":
+        return src.c_idx[src.c_off[g]:src.c_off[g + 1]]
+    if k == "_M":
+        return src.M
+    if k == "node_info":
+        return (0, i)
+    return None  # _visible_frame, _contained_mask, son_node_info
+
+
+def level0_masks(node):
+    """node.mask_list, without making the attribute of an untouched level-0 node"""
+    d = node.__dict__
+    ml = d.get("mask_list")
+    if ml is None and "_src0" in d:
+        src, g = d["_src0"]
+        return (src.gl[g],)
+    return node.mask_list
 
 
 def _np(t):

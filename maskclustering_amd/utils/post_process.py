@@ -66,8 +66,15 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
         fcol.setdefault(fid, c)
     unique_frames = len(fcol) == F
 
+    lazy = csr is not None and hasattr(mask_point_clouds, "is_materialized")
+
     def add(key):
-        pts = mask_point_clouds[key]                              # KeyError as at :70
+        if lazy and not mask_point_clouds.is_materialized(key):  # the CSR row serves it: no set made
+            if key not in mask_point_clouds:
+                raise KeyError(key)
+            pts = None
+        else:
+            pts = mask_point_clouds[key]                          # KeyError as at :70
         table[key] = len(mask_arrays)
         mask_arrays.append(pts)
 
@@ -103,12 +110,17 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     if not nodes:
         return [], []
     scene = np.ascontiguousarray(_host(scene_points), np.float64).reshape(-1, 3)
-    pfm = _bits(_host(point_frame_matrix), F)
+    pfm = getattr(point_frame_matrix, "_mc_bits", None)           # construction's packed words
+    if pfm is None or point_frame_matrix.flags.writeable or point_frame_matrix.shape[1] != F:
+        pfm = _bits(_host(point_frame_matrix), F)
     if csr is not None:      # the construction's rows: table entry -> CSR row, no set is re-read
         rows = np.fromiter((csr[0][k] for k in table), np.int64, count=len(table))
-        lens = np.fromiter((len(p) for p in mask_arrays), np.int64, count=len(mask_arrays))
-        if not np.array_equal(np.diff(csr[1])[rows], lens):       # a set changed in place
+        clen = np.diff(csr[1])[rows]
+        lens = np.fromiter((len(p) if p is not None else -1 for p in mask_arrays), np.int64, count=len(mask_arrays))
+        lens = np.where(lens < 0, clen, lens)
+        if not np.array_equal(clen, lens):                        # a set changed in place
             csr = None
+            mask_arrays = [p if p is not None else mask_point_clouds[k] for k, p in zip(table, mask_arrays)]
     if csr is not None:
         q_dev = rows[np.asarray(q_mask, np.int64)]
         mask_off, mask_pts = csr[1], csr[2]

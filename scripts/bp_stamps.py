@@ -16,14 +16,15 @@ from maskclustering_amd import _native  # noqa: E402
 from maskclustering_amd.synthetic_frames import make_frames_shape  # noqa: E402
 
 shape = sys.argv[1] if len(sys.argv) > 1 else "c2"
-nf = int(sys.argv[2]) if len(sys.argv) > 2 else 250
-fr = make_frames_shape(shape, seed=0, device="cuda", num_frames=nf)
+f0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+nf = int(sys.argv[3]) if len(sys.argv) > 3 else 250
+fr = make_frames_shape(shape, seed=0, device="cuda", frames=range(f0, f0 + nf))
 ctx = _native.Context(0)
 L = _native.load()
 L.mc_debug_bp_stamps.restype = ctypes.c_int
 L.mc_debug_bp_stamps.argtypes = [ctypes.c_void_p]
 ctx.set_points(fr.scene_points.astype(np.float32))
-buf = np.zeros(32, np.uint64)
+buf = np.zeros(40, np.uint64)
 for rep in range(3):
     L.mc_debug_bp_stamps(buf.ctypes.data)
     ctx.set_timing(True)
@@ -45,7 +46,10 @@ for off, kern in ((16, "k_bp_denoise_lds"), (0, "k_bp_denoise (large slots)")):
     for k, n in enumerate(names):
         per = f"{float(buf[off + k]) / 100.0 / nslots:8.2f} us/slot" if off == 16 else ""
         print(f"  {n:12s} {100.0 * float(buf[off + k]) / max(tot, 1):6.2f} % {per}")
-print("k-NN points deferred to the ring search", int(buf[30]))
+print("k-NN sub-phases us/slot: main list pass", round(float(buf[34]) / 100.0 / nslots, 2), "ring search",
+      round(float(buf[35]) / 100.0 / nslots, 2), "whole-cloud fallback", round(float(buf[26]) / 100.0 / nslots, 2))
+print("k-NN points deferred to the ring search", int(buf[30]), "(list overflow", int(buf[32]), "/ < k kept in the list",
+      int(buf[33]), ")", "near-tied keys redone exactly", int(buf[31]))
 print("knn points", int(buf[13]), "candidates/point", round(float(buf[29]) / max(int(buf[13]), 1), 1),
       "fallbacks", int(buf[31]))
 st = ctx.bp_candidates()

@@ -1,0 +1,101 @@
+"""Open-vocabulary query on the device (mc_openvoc_query through the drop-in
+maskclustering_amd.semantics.open_voc_query) against the reference's own main() output
+(tests/golden/openvoc_small.npz) and the CPU restatement (oracle/openvoc_oracle.py).
+
+Tolerance: labels must be equal, except where the oracle's two best probabilities of the object
+are within 1e-5 relative (the device sums the float32 dot products in float64 and rounds once;
+numpy's BLAS order is its own, so exp(100 sim) can differ by a few ULP there).  The fixture's
+exact tie (two equal label features) and overflow (NaN) cases must match exactly."""
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from oracle import openvoc_oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "openvoc_small.npz")
+
+
+def _inputs(z):
+    keys = [str(k) for k in z["keys"]]
+    feats = z["feats"].astype(np.float32)
+    clip = {k: feats[i] for i, k in enumerate(keys)}
+    desc = [str(d) for d in z["descriptions"]]
+    lab = {d: z["labels"][i].astype(np.float32) for i, d in enumerate(desc)}
+    label2id = {d: int(i) for d, i in zip(desc, z["label_ids"])}
+    od = {}
+    for k in range(len(z["obj_off"]) - 1):
+        rows = z["obj_rows"][z["obj_off"][k]:z["obj_off"][k + 1]]
+        ml = [(int(keys[r].split("_")[0]), int(keys[r].split("_")[1]), 0.5) for r in rows]
+        od[k] = {"point_ids": z["pt_idx"][z["pt_off"][k]:z["pt_off"][k + 1]].tolist(), "mask_list": ml,
+                 "repre_mask_list": ml}
+    return od, clip, lab, label2id
+
+
+def _near_tie(prob):
+    if prob is None or not np.all(np.isfinite(prob)):
+        return False
+    top = np.sort(prob)[-2:]
+    return top[1] - top[0] <= 1e-5 * top[1]
+
+
+def test_query_matches_reference_main():
+    from maskclustering_amd.semantics import open_voc_query as ov
+    z = dict(np.load(GOLD))
+    od, clip, lab, label2id = _inputs(z)
+    pred = ov.query(od, clip, lab, label2id, int(z["num_points"]))
+    np.testing.assert_array_equal(pred["pred_classes"], z["pred_classes"])
+    want_masks = np.unpackbits(z["pred_masks_packed"], axis=0, count=int(z["num_points"])).astype(bool)
+    np.testing.assert_array_equal(pred["pred_masks"], want_masks)
+    np.testing.assert_array_equal(pred["pred_score"], z["pred_score"])
+
+
+def test_main_writes_the_reference_file(tmp_path, monkeypatch):
+    from maskclustering_amd.semantics import open_voc_query as ov
+    z = dict(np.load(GOLD))
+    od, clip, lab, label2id = _inputs(z)
+    obj_dir = tmp_path / "objects"
+    (obj_dir / "cfg").mkdir(parents=True)
+    np.save(obj_dir / "cfg" / "object_dict.npy", od, allow_pickle=True)
+    np.save(obj_dir / "cfg" / "open-vocabulary_features.npy", clip, allow_pickle=True)
+    ds = SimpleNamespace(get_scene_points=lambda: np.zeros((int(z["num_points"]), 3)),
+                         get_label_features=lambda: lab, get_label_id=lambda: (label2id, None),
+                         object_dict_dir=str(obj_dir))
+    monkeypatch.chdir(tmp_path)
+    ov.main(SimpleNamespace(config="cfg", seq_name="scene"), dataset=ds)
+    got = np.load(tmp_path / "data" / "prediction" / "cfg" / "scene.npz")
+    np.testing.assert_array_equal(got["pred_classes"], z["pred_classes"])
+
+
+def test_missing_feature_raises_keyerror():
+    from maskclustering_amd.semantics import open_voc_query as ov
+    z = dict(np.load(GOLD))
+    od, clip, lab, label2id = _inputs(z)
+    key = next(f"{m[0]}_{m[1]}" for v in od.values() for m in v["repre_mask_list"])
+    del clip[key]
+    with pytest.raises(KeyError):
+        ov.query(od, clip, lab, label2id, int(z["num_points"]))
+
+
+@pytest.mark.parametrize("num_objects,dim,num_labels", [(700, 1024, 198), (300, 768, 84), (50, 1024, 3000)])
+def test_random_against_oracle(num_objects, dim, num_labels):
+    from maskclustering_amd import _device
+    rng = np.random.default_rng(num_objects + dim)
+    feats = rng.standard_normal((num_objects * 3, dim)).astype(np.float32)
+    feats /= np.linalg.norm(feats, axis=1, keepdims=True)
+    labs = rng.standard_normal((num_labels, dim)).astype(np.float32)
+    labs /= np.linalg.norm(labs, axis=1, keepdims=True)
+    feats[:num_objects] += 2.0 * labs[rng.integers(num_labels, size=num_objects)]
+    feats /= np.linalg.norm(feats, axis=1, keepdims=True)
+    counts = rng.integers(0, 6, num_objects)
+    off = np.zeros(num_objects + 1, np.int64)
+    np.cumsum(counts, out=off[1:])
+    rows = rng.integers(0, len(feats), int(off[-1])).astype(np.int32)
+    got = _device.context().openvoc_query(off, rows, feats, labs, 100.0)
+    want, probs = openvoc_oracle.query(off, rows, feats, labs)
+    bad = [k for k in np.nonzero(got != want)[0] if not _near_tie(probs[k])]
+    assert not bad, f"{len(bad)} labels differ beyond a near-tie, e.g. object {bad[0]}"
+    assert (got == want).mean() > 0.99
