@@ -313,6 +313,11 @@ int mc_openvoc_query(mc_ctx *ctx, int32_t num_objects, const int64_t *obj_off, c
                      int32_t num_rows, int32_t dim, const float *features, int32_t num_labels,
                      const float *label_features, float temperature, int32_t *out_label);
 
+/* host utility: packed little-endian bit rows (bit c of word c/64 = column c) -> one byte per
+ * column, rows * ncols bytes (the dense bool point_frame_matrix the reference's callers read,
+ * graph/construction.py:40,52), split over host threads.                                      */
+int mc_bits_unpack(const uint64_t *words, int64_t rows, int32_t words_per_row, int32_t ncols, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

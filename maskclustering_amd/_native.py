@@ -37,7 +37,7 @@ EXPORTED = [
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
-    "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query",
+    "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query", "mc_bits_unpack",
 ]
 
 MC_SHARD_S3 = 1
@@ -170,6 +170,7 @@ def load():
         "mc_shard_set": (ctypes.c_int, [vp, i32, i32]),
         "mc_cluster_set_edge_capture": (ctypes.c_int, [vp, i64]),
         "mc_openvoc_query": (ctypes.c_int, [vp, i32, vp, vp, i32, i32, vp, i32, vp, ctypes.c_float, vp]),
+        "mc_bits_unpack": (ctypes.c_int, [vp, ctypes.c_int64, i32, i32, vp]),
         "mc_cluster_get_edges": (ctypes.c_int, [vp, vp, P(i64)]),
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
@@ -621,3 +622,16 @@ def _io_methods():
 
 
 _io_methods()
+
+
+def bits_unpack(words, ncols):
+    """(R, W) little-endian uint64 bit rows -> (R, ncols) bool, unpacked by mc_bits_unpack's host
+    threads (no GPU needed)."""
+    words = np.ascontiguousarray(words, dtype="<u8")
+    R = words.shape[0]
+    out = np.empty((R, ncols), np.bool_)
+    if R and ncols:
+        rc = load().mc_bits_unpack(_ptr(words), R, words.shape[1], ncols, _ptr(out))
+        if rc != 0:
+            raise McError(rc, "mc_bits_unpack: bad sizes")
+    return out

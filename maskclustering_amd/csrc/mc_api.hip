@@ -114,7 +114,7 @@ struct mc_ctx {
     DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
         d_blist, d_ncnt, d_par, d_droot, d_rnk, d_lab, d_ccnt, d_ssidx, d_avg, d_qpts;
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
-    DevBuf d_cls_list, d_nbl, d_lean;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
+    DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
@@ -330,7 +330,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_lab, &ctx->d_ccnt, &ctx->d_ssidx, &ctx->d_avg, &ctx->d_qpts, &ctx->d_bpbm, &ctx->d_tmp,
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
-                         &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean};
+                         &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (int b = 0; b < 2; b++) {
@@ -1432,10 +1432,17 @@ int mc_cluster_get_objects(mc_ctx *ctx, uint64_t *vf_bits, int64_t *c_off, int32
         MC_HIP(hipStreamSynchronize(s));
         if (c_off) {
             c_off[0] = 0;
+            int64_t end = 0;
             for (int k = 0; k < K; k++) {
                 c_off[k + 1] = c_off[k] + len[k];
-                if (c_idx && len[k])
-                    MC_HIP(hipMemcpyAsync(c_idx + c_off[k], ctx->fin_pool + off[k], len[k] * 4, hipMemcpyDeviceToHost, s));
+                if (len[k]) end = std::max<int64_t>(end, static_cast<int64_t>(off[k]) + len[k]);
+            }
+            if (c_idx && end) {  // one copy of the pool span, rows gathered on the host
+                std::vector<int> pool(end);
+                MC_HIP(hipMemcpyAsync(pool.data(), ctx->fin_pool, end * 4, hipMemcpyDeviceToHost, s));
+                MC_HIP(hipStreamSynchronize(s));
+                for (int k = 0; k < K; k++)
+                    if (len[k]) memcpy(c_idx + c_off[k], pool.data() + off[k], static_cast<size_t>(len[k]) * 4);
             }
         }
         if (pt_off) {
@@ -1490,7 +1497,9 @@ enum BpStat : int {
     BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
     BS_CLS,             // 5 denoise size-class counts (4 LDS classes + the global-memory kernel)
     BS_TK = BS_CLS + 5,  // ticket counters of the LDS classes
-    BS_COUNT = BS_TK + 4
+    BS_VTK = BS_TK + 4,  // ticket counters of k_bp_voxel, k_bp_query
+    BS_QTK,
+    BS_COUNT
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
@@ -1529,6 +1538,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_moff.reserve((slots + 1) * 4);
     ctx->d_slot_box.reserve(slots * 6 * 4);
     ctx->d_cls_list.reserve(5 * slots * 4);
+    ctx->d_vox_order.reserve(slots * 4);
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
     ctx->d_nbl.reserve(nbl_offset(ctx, 4) * 2);
     ctx->d_lean.reserve(static_cast<size_t>(ctx->num_cu) * mc::kBpLeanInts<3072> * 4);
@@ -1855,8 +1865,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_voxel");
+                hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
+                                   ctx->d_vox_order.as<int>());
                 hipLaunchKernelGGL(mc::k_bp_voxel, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
-                                   ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(),
+                                   ctx->d_vox_order.as<int>(), st + BS_VTK, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(),
                                    ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
                                    ctx->d_hkey.as<unsigned long long>(), ctx->d_hvid.as<int>(), ctx->d_hfirst.as<int>(),
                                    ctx->d_vox_entry.as<int>(), ctx->d_acc.as<double>(), ctx->d_vpts.as<double>(),
@@ -1902,7 +1914,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_bpbm.as<unsigned long long>(), PW, ctx->d_tmp.as<int>(),
                                    static_cast<int>(std::min<size_t>(tmp_cap, INT_MAX)), st + BS_TOP,
                                    ctx->d_slot_nn.as<int>(), ctx->d_slot_toff.as<int>(), ctx->d_slot_cov.as<int>(),
-                                   st + BS_OVF);
+                                   st + BS_OVF, ctx->d_vox_order.as<int>(), st + BS_QTK);
                 hipLaunchKernelGGL(mc::k_bp_keepflags, grid_for(nslot), dim3(256), 0, s, st + BS_NS,
                                    ctx->d_slot_nn.as<int>(), ctx->d_kflag.as<int>(), ctx->d_ksize.as<int>());
                 mc::scan_device_n(s, ctx->d_kflag.as<int>(), ctx->d_midx.as<int>(), st + BS_NS, 0, st + BS_M,
@@ -2487,6 +2499,52 @@ int mc_frames_decode(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t wi
         MC_HIP(hipStreamSynchronize(s));
         ctx->timer.collect();
     });
+}
+
+// ---------------------------------------------------------------------------------------------
+// host: packed bit rows -> bool bytes (the reference's dense point_frame_matrix, construction.py:40)
+// ---------------------------------------------------------------------------------------------
+int mc_bits_unpack(const uint64_t *words, int64_t rows, int32_t words_per_row, int32_t ncols, uint8_t *out)
+{
+    if (rows < 0 || words_per_row < 0 || ncols < 0 || static_cast<int64_t>(ncols) > 64ll * words_per_row)
+        return MC_ERR_INVALID;
+    if (!rows || !ncols) return MC_OK;
+    if (!words || !out) return MC_ERR_INVALID;
+    static const auto lut = [] {  // byte value -> its 8 bits as 8 bytes (little-endian)
+        std::vector<uint64_t> t(256);
+        for (int v = 0; v < 256; v++) {
+            uint64_t x = 0;
+            for (int b = 0; b < 8; b++) x |= static_cast<uint64_t>((v >> b) & 1) << (8 * b);
+            t[v] = x;
+        }
+        return t;
+    }();
+    auto work = [&](int64_t r0, int64_t r1) {
+        const int full = ncols / 8;  // whole output bytes groups of 8 columns
+        for (int64_t r = r0; r < r1; r++) {
+            const uint8_t *wb = reinterpret_cast<const uint8_t *>(words + r * words_per_row);
+            uint8_t *o = out + r * ncols;
+            for (int j = 0; j < full; j++) {
+                const uint64_t x = lut[wb[j]];
+                memcpy(o + 8 * j, &x, 8);
+            }
+            for (int c = 8 * full; c < ncols; c++) o[c] = static_cast<uint8_t>((wb[c >> 3] >> (c & 7)) & 1u);
+        }
+    };
+    const int64_t bytes = rows * ncols;
+    int nt = static_cast<int>(std::min<int64_t>(std::min(8u, std::max(1u, std::thread::hardware_concurrency())),
+                                                std::max<int64_t>(1, bytes >> 22)));
+    if (const char *e = getenv("MC_STAGE_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
+    if (nt <= 1) {
+        work(0, rows);
+        return MC_OK;
+    }
+    std::vector<std::thread> th;
+    const int64_t step = (rows + nt - 1) / nt;
+    for (int t = 1; t < nt; t++) th.emplace_back(work, std::min(rows, t * step), std::min(rows, (t + 1) * step));
+    work(0, std::min(rows, step));
+    for (auto &x : th) x.join();
+    return MC_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

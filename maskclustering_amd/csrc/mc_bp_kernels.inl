@@ -319,7 +319,32 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
 // in list order: voxel keys go into the slot's hash (2 entries per pixel, empty at rest); new
 // voxels get ids in order of their first pixel (atomicMin of the pixel rank, then an ordered
 // scan); the sums are added wave by wave, lane by lane, i.e. in pixel order.
-__global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, const int *__restrict__ slot_frame,
+// Largest slots first for k_bp_voxel (its per-slot time grows with the pixel count; a static
+// round-robin left a few workgroups with several large slots): slots binned by floor(log2(pixels)),
+// bins in descending order.  One workgroup.
+__global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ dNS, const int *__restrict__ slot_np,
+                                                       int *__restrict__ order)
+{
+    __shared__ int cnt[32];
+    const int NS = *dNS, t = threadIdx.x;
+    if (t < 32) cnt[t] = 0;
+    __syncthreads();
+    for (int s = t; s < NS; s += 1024) atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1);
+    __syncthreads();
+    if (t == 0) {
+        int o = 0;
+        for (int b = 31; b >= 0; b--) {
+            const int c = cnt[b];
+            cnt[b] = o;
+            o += c;
+        }
+    }
+    __syncthreads();
+    for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1)] = s;
+}
+
+__global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, const int *__restrict__ order,
+                                                  int *__restrict__ ticket, const int *__restrict__ slot_frame,
                                                   const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
                                                   const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
                                                   const double *__restrict__ intr, const double *__restrict__ pose, BpDev pr,
@@ -331,10 +356,16 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
     __shared__ double sp[256 * 3];
     __shared__ double red[24];
     __shared__ int ws[4];
+    __shared__ int s_next;
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
-    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+    while (true) {  // slots from a ticket, largest first (k_bp_vox_order)
+        if (t == 0) s_next = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int idx = s_next;  // (rewritten only after the barrier that ends this iteration)
+        if (idx >= NS) break;
+        const int s = order[idx];
         const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
         const double *K = intr + 4 * static_cast<size_t>(f);
         const double *T = pose + 16 * static_cast<size_t>(f);
@@ -1628,14 +1659,20 @@ __global__ __launch_bounds__(256) void k_bp_query(
     const int *__restrict__ gidx, const unsigned long long *__restrict__ gcell, const int *__restrict__ gstart,
     unsigned gnb, unsigned long long *__restrict__ bm, int PW, int *__restrict__ tmp, int tmp_cap,
     int *__restrict__ tmp_top, int *__restrict__ slot_nn, int *__restrict__ slot_toff, int *__restrict__ slot_cov,
-    int *__restrict__ ovf)
+    int *__restrict__ ovf, const int *__restrict__ order, int *__restrict__ ticket)
 {
-    __shared__ int s_lo, s_hi, s_cov, s_base;
+    __shared__ int s_lo, s_hi, s_cov, s_base, s_next;
     __shared__ int ws[4];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id();
     unsigned long long *mb = bm + static_cast<size_t>(blockIdx.x) * PW;
-    for (int s = blockIdx.x; s < NS; s += gridDim.x) {
+    while (true) {  // slots from a ticket, largest first (k_bp_vox_order)
+        if (t == 0) s_next = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int idx = s_next;
+        __syncthreads();  // every thread has read it before thread 0 can take the next one
+        if (idx >= NS) break;
+        const int s = order[idx];
         const int ns = slot_ns[s];
         if (ns < pr.few) {  // :109 (uniform)
             if (t == 0) {

@@ -27,6 +27,8 @@ import itertools
 import numpy as np
 
 from .. import _device
+from .._hostutil import no_gc
+from .. import _native
 from .._native import MC_ERR_EMPTY_OBSERVERS, MC_ERR_INVALID, McError
 from ..pipeline import bits_to_bool, bool_to_bits
 from ..utils import mask_backprojection as _mb
@@ -42,7 +44,7 @@ class PointFrameMatrix(np.ndarray):
 
     @classmethod
     def from_bits(cls, words, F):
-        a = bits_to_bool(words, F).view(cls)
+        a = _native.bits_unpack(words, F).view(cls)
         a._mc_bits = np.ascontiguousarray(words)
         a.flags.writeable = False
         return a
@@ -248,6 +250,11 @@ def _build(args, scene_points, frame_list, dataset):
 
 
 def mask_graph_construction(args, scene_points, frame_list, dataset):
+    with no_gc():
+        return _mask_graph_construction(args, scene_points, frame_list, dataset)
+
+
+def _mask_graph_construction(args, scene_points, frame_list, dataset):
     if args.debug:
         print('start building point in mask matrix')
     ctx, gi, gl, keys, mpc = _build(args, scene_points, frame_list, dataset)

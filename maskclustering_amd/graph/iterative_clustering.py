@@ -37,6 +37,7 @@ import os
 import numpy as np
 
 from .. import _device
+from .._hostutil import no_gc
 from ..pipeline import bits_to_bool, bool_to_bits
 from .node import Node, level0_masks
 
@@ -132,6 +133,11 @@ def _replay(nodes, T, sizes, edges, parts):
 
 
 def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay=None):
+    with no_gc():
+        return _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay)
+
+
+def _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay):
     replay = REPLAY_SET_ORDER if replay is None else bool(replay)
     if debug:
         print('====> Start iterative clustering')
@@ -176,12 +182,15 @@ def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debu
         return [Node.compact(ml, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M, pts, (T, k), sons)
                 for k, (ml, pts, sons) in enumerate(rep)]
     out = []
+    son_order = np.argsort(last, kind="stable")                   # last-level nodes grouped by object
+    son_off = np.searchsorted(last[son_order], np.arange(ci.num_objects + 1))
+    son_ids = son_order.tolist()
     for k in range(ci.num_objects):
         members = obj["mask_idx"][obj["mask_off"][k]:obj["mask_off"][k + 1]]
         mask_list = []
         for i in members.tolist():
             mask_list += level0_masks(nodes[i])
-        sons = {(T - 1, int(j)) for j in np.nonzero(last == k)[0].tolist()}
+        sons = {(T - 1, j) for j in son_ids[son_off[k]:son_off[k + 1]]}
         out.append(Node.compact_lazy_points(mask_list, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M,
                                             obj["pt_idx"][obj["pt_off"][k]:obj["pt_off"][k + 1]], (T, k), sons))
     return out

@@ -20,7 +20,7 @@ import os
 
 import numpy as np
 
-from .. import _device
+from maskclustering_amd import _device  # absolute: also run as `semantics.open-voc_query`
 
 TEMPERATURE = 100.0  # exp_sim = np.exp(raw_similarity * 100) (:42)
 
@@ -77,3 +77,8 @@ def main(args, dataset=None):
     os.makedirs(pred_dir, exist_ok=True)
     pred = query(object_dict, clip_feature, label_features_dict, label2id, total_point_num)
     np.savez(f"{pred_dir}/{args.seq_name}.npz", **pred)
+
+
+if __name__ == "__main__":  # python -m semantics.open-voc_query --config ... --seq_name ... (run.py:102)
+    from utils.config import get_args
+    main(get_args())

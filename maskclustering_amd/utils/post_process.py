@@ -26,6 +26,7 @@ import os
 import numpy as np
 
 from .. import _device
+from .._hostutil import no_gc
 from .._native import PPParams
 
 
@@ -55,6 +56,13 @@ def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame
     """post_process.py:180-194 on the device: returns (total_point_ids_list, total_mask_list) as the
     reference hands them to export (object point ids int64 in list order; [(frame_id, mask_id,
     coverage)] per object)."""
+    with no_gc():
+        return _post_process_objects(node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list,
+                                     point_filter_threshold, dbscan_eps, dbscan_min_points, overlapping_ratio)
+
+
+def _post_process_objects(node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list,
+                          point_filter_threshold, dbscan_eps, dbscan_min_points, overlapping_ratio):
     nodes = [n for n in node_list if len(n.mask_list) >= 2]   # :182
     frame_arr = np.array(frame_list)
     F = len(frame_list)

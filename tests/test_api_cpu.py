@@ -65,6 +65,7 @@ def test_install_routes_reference_module_names(tmp_path):
     (tmp_path / "utils").mkdir()
     (tmp_path / "utils" / "__init__.py").write_text("")
     (tmp_path / "utils" / "geometry.py").write_text("MARK = 'reference'\n")
+    (tmp_path / "semantics").mkdir()
     code = textwrap.dedent(f"""
         import sys
         sys.path.insert(0, {str(tmp_path)!r})  # the reference checkout (cwd of main.py)
@@ -76,6 +77,9 @@ def test_install_routes_reference_module_names(tmp_path):
         assert iterative_clustering.__module__ == 'maskclustering_amd.graph.iterative_clustering'
         assert frame_backprojection.__module__ == 'maskclustering_amd.utils.mask_backprojection'
         assert MARK == 'reference'
+        import importlib.util
+        spec = importlib.util.find_spec('semantics.open-voc_query')   # what `python -m` runs (run.py:102)
+        assert spec.origin.endswith('maskclustering_amd/semantics/open_voc_query.py'), spec.origin
         print('ok')
     """)
     import os

@@ -99,3 +99,49 @@ def test_random_against_oracle(num_objects, dim, num_labels):
     bad = [k for k in np.nonzero(got != want)[0] if not _near_tie(probs[k])]
     assert not bad, f"{len(bad)} labels differ beyond a near-tie, e.g. object {bad[0]}"
     assert (got == want).mean() > 0.99
+
+
+def test_run_py_command_routes_to_device(tmp_path):
+    """run.py:102's `python -m semantics.open-voc_query --config C --seq_name S`, in a
+    reference-shaped tree whose utils.config serves the fixture, with the integration hook on
+    PYTHONPATH: the drop-in runs and writes the reference's file."""
+    import subprocess
+    import sys
+    import textwrap
+    from conftest import REPO
+    z = dict(np.load(GOLD))
+    od, clip, lab, label2id = _inputs(z)
+    (tmp_path / "semantics").mkdir()
+    (tmp_path / "utils").mkdir()
+    (tmp_path / "utils" / "__init__.py").write_text("")
+    obj_dir = tmp_path / "objects"
+    (obj_dir / "cfg").mkdir(parents=True)
+    np.save(obj_dir / "cfg" / "object_dict.npy", od, allow_pickle=True)
+    np.save(obj_dir / "cfg" / "open-vocabulary_features.npy", clip, allow_pickle=True)
+    np.save(tmp_path / "labels.npy", {"lab": lab, "label2id": label2id}, allow_pickle=True)
+    (tmp_path / "utils" / "config.py").write_text(textwrap.dedent(f"""
+        import argparse
+        import numpy as np
+        def get_args():
+            p = argparse.ArgumentParser()
+            p.add_argument('--config'); p.add_argument('--seq_name')
+            return p.parse_args()
+        class _DS:
+            object_dict_dir = {str(obj_dir)!r}
+            def __init__(self):
+                self.d = np.load({str(tmp_path / "labels.npy")!r}, allow_pickle=True).item()
+            def get_scene_points(self):
+                return np.zeros(({int(z["num_points"])}, 3))
+            def get_label_features(self):
+                return self.d['lab']
+            def get_label_id(self):
+                return self.d['label2id'], None
+        def get_dataset(args):
+            return _DS()
+    """))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(REPO, "integration"), REPO]))
+    out = subprocess.run([sys.executable, "-m", "semantics.open-voc_query", "--config", "cfg", "--seq_name", "scene"],
+                         capture_output=True, text=True, cwd=str(tmp_path), env=env, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    got = np.load(tmp_path / "data" / "prediction" / "cfg" / "scene.npz")
+    np.testing.assert_array_equal(got["pred_classes"], z["pred_classes"])
