@@ -551,15 +551,93 @@ def run_post_process(a):
     print(json.dumps(res), flush=True)
 
 
+def run_sweep(a):
+    """--variant sweep: BASELINE configs[4], the full ScanNet val sweep, scene-parallel as the reference's
+    run.py:33-50 runs it (one process per GPU, scene i on rank i mod N, no data-path collective).
+    A scene = S1-S6 from its RGB-D frames resident in HBM (the e2e variant's step: set_points builds the
+    scene's ball-query grid, mc_backproject, mc_graph_build + mc_cluster_run); the rank's scenes are
+    cycled from a pool of --pool distinct synthetic ScanNet-shaped scenes rendered once (seeds
+    seed + rank * pool + j).  value = wall time of all --scenes scenes (max over ranks)."""
+    import torch
+    import torch.distributed as dist
+    from maskclustering_amd import _native
+    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    mine = list(range(rank, a.scenes, world))
+    pool = []
+    t0 = time.perf_counter()
+    for j in range(min(a.pool, max(len(mine), 1))):
+        fr = make_frames_shape(a.shape, seed=a.seed + rank * a.pool + j, device=f"cuda:{local}", out="torch")
+        pool.append((fr, torch.tensor(fr.scene_points, dtype=torch.float32, device=dev),
+                     torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev),
+                     torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)))
+    log(f"rank {rank}: {len(mine)} scenes from a pool of {len(pool)} rendered in {time.perf_counter() - t0:.1f} s")
+    run = GraphRun(local)
+    ctx = run.ctx
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    prm = _native.bp_params()
+    objects = []
+
+    def scene(j):
+        fr, pts, K, T = pool[j % len(pool)]
+        ctx.set_points(device_ptr=pts.data_ptr(), num_points=fr.num_points)
+        ctx.backproject(None, None, None, None, prm, shape=tuple(fr.depth.shape),
+                        device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), K.data_ptr(), T.data_ptr()))
+        ctx.use_backprojection()
+        run.step(**CFG)
+        return int(ctx.cluster_info().num_objects)
+
+    for j in range(min(len(pool), max(a.warmup, 1))):
+        scene(j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(len(mine)):
+        objects.append(scene(j))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    wall = float(elapsed.item())
+    if rank == 0:
+        fr = pool[0][0]
+        res = {"metric": "full-sweep end-to-end wall time (BASELINE configs[4]: 312 ScanNet val scenes, scene-parallel)",
+               "value": round(wall, 3), "unit": "s", "n_gpus": world, "steps": a.scenes, "warmup": a.warmup,
+               "ms_per_step": round(1e3 * wall / max(a.scenes, 1) * world, 3), "higher_is_better": False,
+               "scaling": "strong", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+               "config": {"workload": f"{a.scenes} scenes of {a.shape} ({fr.num_frames} frames {fr.depth.shape[2]}x"
+                                      f"{fr.depth.shape[1]}, P={fr.num_points}), S1-S6 per scene, scene i on rank "
+                                      f"i mod {world}, each rank cycling {len(pool)} distinct rendered scenes",
+                          "variant": "sweep", "parallelism": f"scene-parallel x{world}",
+                          "scenes_per_s": round(a.scenes / wall, 3),
+                          "rank0_objects_per_scene": round(float(np.mean(objects)), 1) if objects else 0}}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--variant", choices=["g", "e2e", "pp", "api"], default="e2e")
+    ap.add_argument("--variant", choices=["g", "e2e", "pp", "api", "sweep"], default="e2e")
+    ap.add_argument("--scenes", type=int, default=312, help="sweep: scenes of the whole job (ScanNet val: 312)")
+    ap.add_argument("--pool", type=int, default=4, help="sweep: distinct rendered scenes per rank")
     ap.add_argument("--with-pp", action="store_true", help="api: include post_process's compute")
     ap.add_argument("--profile", action="store_true", help="api: cProfile one extra step to stderr")
-    ap.add_argument("--shape", default="c3")
+    ap.add_argument("--shape", default=None, help="default: c3 (g, e2e), c2 (api, pp, sweep)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", choices=["scene", "frames"], default="frames",
@@ -567,10 +645,14 @@ def main():
                          "scaling; the north_star's ScanNet++-sized C3 by default); scene: every rank its own "
                          "scene (weak scaling, the reference's run.py sweep, BASELINE configs[4])")
     args = ap.parse_args()
+    if args.shape is None:
+        args.shape = "c3" if args.variant in ("g", "e2e") else "c2"
     if args.variant == "pp":
         return run_post_process(args)
     if args.variant == "api":
         return run_api(args)
+    if args.variant == "sweep":
+        return run_sweep(args)
 
     import torch
     import torch.distributed as dist

@@ -312,16 +312,26 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
 }
 
 // ---------------------------------------------------------------------------------------------
-// (a3) voxel_down_sample(0.01) (:105), workgroup per slot
+// (a3) voxel_down_sample(0.01) (:105), pixel-parallel over the whole batch
 // ---------------------------------------------------------------------------------------------
 // Open3D: min bound - voxel/2, index = floor((p - vmin) / voxel), per-voxel sum in input order,
-// mean = sum / count.  Output order (u2): first occurrence in pixel order.  Chunks of 256 pixels
-// in list order: voxel keys go into the slot's hash (2 entries per pixel, empty at rest); new
-// voxels get ids in order of their first pixel (atomicMin of the pixel rank, then an ordered
-// scan); the sums are added wave by wave, lane by lane, i.e. in pixel order.
-// Largest slots first for k_bp_voxel (its per-slot time grows with the pixel count; a static
-// round-robin left a few workgroups with several large slots): slots binned by floor(log2(pixels)),
-// bins in descending order.  One workgroup.
+// mean = sum / count.  Output order (u2): first occurrence in pixel order.
+// Only the additions inside one voxel are ordered, so nothing walks a slot's pixels in sequence:
+// every slot's pixel list is cut into chunks of kVxChunk pixels (one workgroup each, any order),
+//   k_vx_nch / scan / k_vx_chunks   chunk table (chunk -> slot), per-slot min bound reset
+//   k_vx_bound      per-slot min bound (order-free: atomicMin on order-preserving u64 images)
+//   k_vx_hash       voxel key -> the slot's hash (2 entries per pixel, empty at rest); per entry
+//                   the first pixel (atomicMin) and the pixel count (wave-aggregated)
+//   k_vx_alloc      first pixels: the voxel's list range (bump per slot); firsts per chunk
+//   scan            voxel ids = first pixels in pixel order (chunk prefix - the slot's first chunk)
+//   k_vx_scatter    pixel -> its voxel's list (unordered); first pixel -> voxel id -> entry
+//   k_vx_fold       lane per voxel (<= kVxSmall pixels): sort the list (bitonic network in
+//                   registers), then add the points in pixel order; larger voxels -> k_vx_big
+//   k_vx_big        workgroup per large voxel: the list ordered through bitmaps of 1024-pixel
+//                   windows, points staged in LDS, one lane adds them in order
+// The hash entries and per-entry counters return to empty / zero in the fold kernels.
+// Largest slots first for k_bp_query (its per-slot time grows with the slot size): slots binned
+// by floor(log2(pixels)), bins in descending order.  One workgroup.
 __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ dNS, const int *__restrict__ slot_np,
                                                        int *__restrict__ order)
 {
@@ -343,154 +353,422 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
     for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1)] = s;
 }
 
-__global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, const int *__restrict__ order,
-                                                  int *__restrict__ ticket, const int *__restrict__ slot_frame,
-                                                  const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
-                                                  const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
-                                                  const double *__restrict__ intr, const double *__restrict__ pose, BpDev pr,
-                                                  unsigned long long *__restrict__ hkey, int *__restrict__ hvid,
-                                                  int *__restrict__ hfirst, int *__restrict__ vox_entry,
-                                                  double *__restrict__ acc, double *__restrict__ vpts,
-                                                  int *__restrict__ slot_nv, int *__restrict__ errflag)
+constexpr int kVxChunk = 256;  // pixels per chunk (= threads of the chunk kernels)
+constexpr int kVxSmall = 32;   // largest voxel (in pixels) folded by one lane
+constexpr int kVxWin = 1024;   // pixel window of the large-voxel bitmaps
+
+// order-preserving u64 image of a double (a < b <=> img(a) < img(b), NaN aside)
+__device__ __forceinline__ unsigned long long dbl_ord(double v)
 {
-    __shared__ double sp[256 * 3];
-    __shared__ double red[24];
-    __shared__ int ws[4];
-    __shared__ int s_next;
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ double dbl_unord(unsigned long long u)
+{
+    return __longlong_as_double(static_cast<long long>((u >> 63) ? (u & ~(1ull << 63)) : ~u));
+}
+
+// chunks per slot; min-bound images and list bumps reset
+__global__ __launch_bounds__(256) void k_vx_nch(const int *__restrict__ dNS, const int *__restrict__ slot_np,
+                                                int *__restrict__ nch, unsigned long long *__restrict__ vmin,
+                                                int *__restrict__ bump)
+{
     const int NS = *dNS;
-    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-    const int W = pr.W;
-    while (true) {  // slots from a ticket, largest first (k_bp_vox_order)
-        if (t == 0) s_next = atomicAdd(ticket, 1);
-        __syncthreads();
-        const int idx = s_next;  // (rewritten only after the barrier that ends this iteration)
-        if (idx >= NS) break;
-        const int s = order[idx];
-        const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
-        const double *K = intr + 4 * static_cast<size_t>(f);
-        const double *T = pose + 16 * static_cast<size_t>(f);
-        const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
-        const unsigned *pl = pix_list + base;
-        // min bound (order-free)
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < NS; s += gridDim.x * 256) {
+        nch[s] = (slot_np[s] + kVxChunk - 1) / kVxChunk;
+        vmin[3 * s] = vmin[3 * s + 1] = vmin[3 * s + 2] = ~0ull;
+        bump[s] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vx_chunks(const int *__restrict__ dNS, const int *__restrict__ nch,
+                                                   const int *__restrict__ choff, int *__restrict__ chslot)
+{
+    const int NS = *dNS;
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < NS; s += gridDim.x * 256) {
+        const int o = choff[s], n = nch[s];
+        for (int j = 0; j < n; j++) chslot[o + j] = s;
+    }
+}
+
+// the pixel of chunk c handled by this thread: slot, index k within the slot's list, validity
+struct VxPix {
+    int s, j, k, n, base;
+    bool valid;
+};
+__device__ __forceinline__ VxPix vx_pix(int c, const int *__restrict__ chslot, const int *__restrict__ choff,
+                                        const int *__restrict__ slot_np, const int *__restrict__ slot_pix)
+{
+    VxPix q;
+    q.s = chslot[c];
+    q.j = c - choff[q.s];
+    q.n = slot_np[q.s];
+    q.base = slot_pix[q.s];
+    q.k = q.j * kVxChunk + static_cast<int>(threadIdx.x);
+    q.valid = q.k < q.n;
+    return q;
+}
+
+// world point of list entry k of slot s (frame f)
+__device__ __forceinline__ void vx_point(int s, int k, int base, const int *__restrict__ slot_frame,
+                                         const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
+                                         const double *__restrict__ intr, const double *__restrict__ pose, int H, int W,
+                                         double &x, double &y, double &z)
+{
+    const int f = slot_frame[s];
+    const unsigned i = pix_list[base + k];
+    bp_world(intr + 4 * static_cast<size_t>(f), pose + 16 * static_cast<size_t>(f), static_cast<int>(i % W),
+             static_cast<int>(i / W), depth[static_cast<size_t>(f) * H * W + i], x, y, z);
+}
+
+__global__ __launch_bounds__(kVxChunk) void k_vx_bound(const int *__restrict__ dNCH, const int *__restrict__ chslot,
+                                                       const int *__restrict__ choff, const int *__restrict__ slot_frame,
+                                                       const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                       const unsigned *__restrict__ pix_list,
+                                                       const float *__restrict__ depth, const double *__restrict__ intr,
+                                                       const double *__restrict__ pose, BpDev pr,
+                                                       unsigned long long *__restrict__ vmin)
+{
+    __shared__ double red[24];
+    const int NCH = *dNCH;
+    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
+        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        for (int k = t; k < n; k += 256) {
-            const unsigned i = pl[k];
-            double p[3];
-            bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
-#pragma unroll
-            for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
-        }
+        if (q.valid) vx_point(q.s, q.k, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, mn[0], mn[1], mn[2]);
         block_minmax3(mn, mx, red);
-        double vmin[3];
+        const int d = threadIdx.x;
+        if (d < 3) atomicMin(&vmin[3 * q.s + d], dbl_ord(d == 0 ? mn[0] : d == 1 ? mn[1] : mn[2]));
+    }
+}
+
+__device__ __forceinline__ void vx_vmin(const unsigned long long *__restrict__ vmin, int s, double vs, double v[3])
+{
 #pragma unroll
-        for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
-        const unsigned C = 2u * static_cast<unsigned>(n);
-        unsigned long long *hk = hkey + 2 * static_cast<size_t>(base);
-        int *hv = hvid + 2 * static_cast<size_t>(base);
-        int *hf = hfirst + 2 * static_cast<size_t>(base);
-        double *ac = acc + 4 * static_cast<size_t>(base);
-        int nv = 0;
-        for (int c0 = 0; c0 < n; c0 += 256) {
-            const int k = c0 + t;
-            const bool valid = k < n;
-            double p[3] = {0.0, 0.0, 0.0};
-            unsigned e = 0;
-            if (valid) {
-                const unsigned i = pl[k];
-                bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
-                long long ix[3];
+    for (int c = 0; c < 3; c++) v[c] = dbl_unord(vmin[3 * s + c]) - vs * 0.5;
+}
+
+__global__ __launch_bounds__(kVxChunk) void k_vx_hash(const int *__restrict__ dNCH, const int *__restrict__ chslot,
+                                                      const int *__restrict__ choff, const int *__restrict__ slot_frame,
+                                                      const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                      const unsigned *__restrict__ pix_list,
+                                                      const float *__restrict__ depth, const double *__restrict__ intr,
+                                                      const double *__restrict__ pose, BpDev pr,
+                                                      const unsigned long long *__restrict__ vmin,
+                                                      unsigned long long *__restrict__ hkey, int *__restrict__ hfirst,
+                                                      int *__restrict__ ecnt, int *__restrict__ pent,
+                                                      int *__restrict__ errflag)
+{
+    const int NCH = *dNCH;
+    const int lane = lane_id();
+    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
+        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
+        int e = -1;
+        if (q.valid) {
+            double vm[3], p[3];
+            vx_vmin(vmin, q.s, pr.vs, vm);
+            vx_point(q.s, q.k, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, p[0], p[1], p[2]);
+            long long ix[3];
 #pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    ix[c] = static_cast<long long>(floor((p[c] - vmin[c]) / pr.vs));
-                    if (ix[c] < 0 || ix[c] >= (1ll << 21)) {
-                        atomicOr(errflag, 1);
-                        ix[c] = ix[c] < 0 ? 0 : (1ll << 21) - 1;
-                    }
-                }
-                const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
-                e = mod_mul(bp_hash64(key), C);
-                while (true) {
-                    unsigned long long cur = hk[e];
-                    if (cur == kEmptyKey) {
-                        cur = atomicCAS(&hk[e], kEmptyKey, key);
-                        if (cur == kEmptyKey) cur = key;
-                    }
-                    if (cur == key) break;
-                    e = e + 1 == C ? 0 : e + 1;
-                }
-                if (ld_agent(&hv[e]) < 0) atomicMin(&hf[e], k);
-            }
-            __syncthreads();
-            const bool first = valid && ld_agent(&hv[e]) < 0 && ld_agent(&hf[e]) == k;
-            int tot;
-            const int pos = block_excl_scan<256>(first ? 1 : 0, ws, tot);
-            if (first) {
-                const int v = nv + pos;
-                st_agent(&hv[e], v);
-                vox_entry[base + v] = static_cast<int>(e);
-                ac[4 * v] = 0.0;
-                ac[4 * v + 1] = 0.0;
-                ac[4 * v + 2] = 0.0;
-                ac[4 * v + 3] = 0.0;
-            }
-            __syncthreads();
-            const int vid = valid ? ld_agent(&hv[e]) : -1;
-            sp[3 * t] = p[0];
-            sp[3 * t + 1] = p[1];
-            sp[3 * t + 2] = p[2];
-            __syncthreads();
-            // group lanes by voxel (ballots only), then every group leader of the wave adds its
-            // group's points in lane order to the running sum at once (one round trip per wave)
-            unsigned long long gm = 0;
-            {
-                unsigned long long act = __ballot(vid >= 0);
-                while (act) {
-                    const int L = __ffsll(static_cast<long long>(act)) - 1;
-                    const int kk = __shfl(vid, L, 64);
-                    const unsigned long long m = __ballot(vid == kk);
-                    if (lane == L) gm = m;
-                    act &= ~m;
+            for (int d = 0; d < 3; d++) {
+                ix[d] = static_cast<long long>(floor((p[d] - vm[d]) / pr.vs));
+                if (ix[d] < 0 || ix[d] >= (1ll << 21)) {
+                    atomicOr(errflag, 1);
+                    ix[d] = ix[d] < 0 ? 0 : (1ll << 21) - 1;
                 }
             }
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                if (wv == w && gm) {  // AccumulatedPoint::AddPoint, lane (= pixel) order
-                    double ax = ac[4 * vid], ay = ac[4 * vid + 1], az = ac[4 * vid + 2], an = ac[4 * vid + 3];
-                    unsigned long long mm = gm;
-                    while (mm) {
-                        const int l = __ffsll(static_cast<long long>(mm)) - 1;
-                        mm &= mm - 1;
-                        const double *q = sp + 3 * (w * 64 + l);
-                        ax = ax + q[0];
-                        ay = ay + q[1];
-                        az = az + q[2];
-                        an = an + 1.0;
-                    }
-                    ac[4 * vid] = ax;
-                    ac[4 * vid + 1] = ay;
-                    ac[4 * vid + 2] = az;
-                    ac[4 * vid + 3] = an;
+            const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
+            const unsigned C = 2u * static_cast<unsigned>(q.n);
+            unsigned long long *hk = hkey + 2 * static_cast<size_t>(q.base);
+            unsigned h = mod_mul(bp_hash64(key), C);
+            while (true) {
+                unsigned long long cur = hk[h];
+                if (cur == kEmptyKey) {
+                    cur = atomicCAS(&hk[h], kEmptyKey, key);
+                    if (cur == kEmptyKey) cur = key;
                 }
-                __syncthreads();
+                if (cur == key) break;
+                h = h + 1 == C ? 0 : h + 1;
             }
-            nv += tot;
+            e = static_cast<int>(2 * static_cast<unsigned>(q.base) + h);
+            pent[q.base + q.k] = e;
         }
-        // means; the hash entries of this slot return to empty
-        for (int v = t; v < nv; v += 256) {
-            const double cnt = ac[4 * v + 3];
-            vpts[3 * (static_cast<size_t>(base) + v)] = ac[4 * v] / cnt;
-            vpts[3 * (static_cast<size_t>(base) + v) + 1] = ac[4 * v + 1] / cnt;
-            vpts[3 * (static_cast<size_t>(base) + v) + 2] = ac[4 * v + 2] / cnt;
-            const int e = vox_entry[base + v];
-            hk[e] = kEmptyKey;
-            st_agent(&hv[e], -1);
-            st_agent(&hf[e], INT_MAX);
+        // lanes of one entry (consecutive pixels mostly share voxels): the lowest lane (smallest
+        // k) records the group's first pixel and count
+        unsigned long long act = __ballot(e >= 0);
+        while (act) {
+            const int L = __ffsll(static_cast<long long>(act)) - 1;
+            const int ee = __shfl(e, L, 64);
+            const unsigned long long m = __ballot(e == ee);
+            if (lane == L) {
+                atomicMin(&hfirst[ee], q.k);
+                atomicAdd(&ecnt[ee], __popcll(m));
+            }
+            act &= ~m;
         }
-        if (t == 0) slot_nv[s] = nv;
+    }
+}
+
+// first pixel of a voxel: its list range [estart, estart + ecnt) inside the slot's pixel range;
+// first pixels per chunk -> chnf
+__global__ __launch_bounds__(kVxChunk) void k_vx_alloc(const int *__restrict__ dNCH, const int *__restrict__ chslot,
+                                                       const int *__restrict__ choff, const int *__restrict__ slot_np,
+                                                       const int *__restrict__ slot_pix, const int *__restrict__ pent,
+                                                       const int *__restrict__ hfirst, const int *__restrict__ ecnt,
+                                                       int *__restrict__ bump, int *__restrict__ estart,
+                                                       int *__restrict__ chnf)
+{
+    __shared__ int ws[kVxChunk / 64];
+    __shared__ int s_off;
+    const int NCH = *dNCH;
+    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
+        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
+        int e = -1, cnt = 0;
+        if (q.valid) {
+            e = pent[q.base + q.k];
+            if (hfirst[e] == q.k) cnt = ecnt[e];
+        }
+        int tot;
+        const int ex = block_excl_scan<kVxChunk>(cnt, ws, tot);
+        const int nf = block_sum<kVxChunk>(cnt > 0 ? 1 : 0, ws);
+        if (threadIdx.x == 0) {
+            s_off = tot ? atomicAdd(&bump[q.s], tot) : 0;
+            chnf[c] = nf;
+        }
+        __syncthreads();
+        if (cnt > 0) estart[e] = q.base + s_off + ex;
         __syncthreads();
     }
 }
 
+__global__ __launch_bounds__(kVxChunk) void k_vx_scatter(const int *__restrict__ dNCH, const int *__restrict__ chslot,
+                                                         const int *__restrict__ choff, const int *__restrict__ nch,
+                                                         const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                         const int *__restrict__ pent, const int *__restrict__ hfirst,
+                                                         const int *__restrict__ estart, int *__restrict__ efill,
+                                                         const int *__restrict__ chfx, int *__restrict__ vlist,
+                                                         int *__restrict__ vox_entry, int *__restrict__ slot_nv)
+{
+    __shared__ int ws[kVxChunk / 64];
+    const int NCH = *dNCH;
+    const int lane = lane_id();
+    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
+        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
+        const int e = q.valid ? pent[q.base + q.k] : -1;
+        const bool first = q.valid && hfirst[e] == q.k;
+        unsigned long long act = __ballot(e >= 0);
+        while (act) {
+            const int L = __ffsll(static_cast<long long>(act)) - 1;
+            const int ee = __shfl(e, L, 64);
+            const unsigned long long m = __ballot(e == ee);
+            int b = 0;
+            if (lane == L) b = estart[ee] + atomicAdd(&efill[ee], __popcll(m));
+            b = __shfl(b, L, 64);
+            if (e == ee) vlist[b + __popcll(m & ((1ull << lane) - 1))] = q.k;
+            act &= ~m;
+        }
+        int tot;
+        const int ex = block_excl_scan<kVxChunk>(first ? 1 : 0, ws, tot);
+        const int c0 = choff[q.s];
+        if (first) vox_entry[q.base + chfx[c] - chfx[c0] + ex] = e;
+        if (threadIdx.x == 0 && q.j == nch[q.s] - 1) slot_nv[q.s] = chfx[c0 + nch[q.s]] - chfx[c0];
+    }
+}
+
+// ascending bitonic sort of S register values (S a power of two)
+template <int S>
+__device__ __forceinline__ void bitonic_sort_regs(int (&a)[S])
+{
+#pragma unroll
+    for (int k = 2; k <= S; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < S; i++) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const int x = a[i], y = a[l];
+                    const int lo = min(x, y), hi = max(x, y);
+                    const bool up = (i & k) == 0;
+                    a[i] = up ? lo : hi;
+                    a[l] = up ? hi : lo;
+                }
+            }
+}
+
+// one lane: the cnt (<= S) list entries of a voxel, sorted, points added in that order
+template <int S>
+__device__ __forceinline__ void vx_fold_lane(const int *__restrict__ vl, int cnt, int s, int base,
+                                             const int *__restrict__ slot_frame, const unsigned *__restrict__ pix_list,
+                                             const float *__restrict__ depth, const double *__restrict__ intr,
+                                             const double *__restrict__ pose, int H, int W, double acc[3])
+{
+    int key[S];
+#pragma unroll
+    for (int i = 0; i < S; i++) key[i] = i < cnt ? vl[i] : INT_MAX;
+    bitonic_sort_regs<S>(key);
+    double ax = 0.0, ay = 0.0, az = 0.0;
+#pragma unroll
+    for (int i = 0; i < S; i++) {
+        if (i < cnt) {
+            double x, y, z;
+            vx_point(s, key[i], base, slot_frame, pix_list, depth, intr, pose, H, W, x, y, z);
+            ax = ax + x;
+            ay = ay + y;
+            az = az + z;
+        }
+    }
+    acc[0] = ax;
+    acc[1] = ay;
+    acc[2] = az;
+}
+
+__device__ __forceinline__ void vx_reset(int e, unsigned long long *__restrict__ hkey, int *__restrict__ hfirst,
+                                         int *__restrict__ ecnt, int *__restrict__ efill)
+{
+    hkey[e] = kEmptyKey;
+    hfirst[e] = INT_MAX;
+    ecnt[e] = 0;
+    efill[e] = 0;
+}
+
+// lane per voxel of up to small_max (<= kVxSmall) pixels (sorting network sized by the wave's largest
+// voxel); larger voxels -> big list
+__global__ __launch_bounds__(kVxChunk) void k_vx_fold(const int *__restrict__ dNCH, const int *__restrict__ chslot,
+                                                      const int *__restrict__ choff, const int *__restrict__ slot_frame,
+                                                      const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                      const int *__restrict__ slot_nv, const unsigned *__restrict__ pix_list,
+                                                      const float *__restrict__ depth, const double *__restrict__ intr,
+                                                      const double *__restrict__ pose, BpDev pr,
+                                                      const int *__restrict__ vox_entry, const int *__restrict__ estart,
+                                                      const int *__restrict__ vlist, unsigned long long *__restrict__ hkey,
+                                                      int *__restrict__ hfirst, int *__restrict__ ecnt,
+                                                      int *__restrict__ efill, double *__restrict__ vpts,
+                                                      int2 *__restrict__ big, int *__restrict__ nbig, int small_max)
+{
+    const int NCH = *dNCH;
+    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
+        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
+        const int v = q.k;  // voxel index in the slot (voxels <= pixels)
+        const bool live = v < slot_nv[q.s];
+        int e = -1, cnt = 0;
+        if (live) {
+            e = vox_entry[q.base + v];
+            cnt = ecnt[e];
+            if (cnt > small_max) {
+                big[atomicAdd(nbig, 1)] = make_int2(q.s, v);
+                cnt = 0;
+            }
+        }
+        const int cmax = wave_max_i(cnt);
+        if (cmax == 0) continue;
+        double acc[3];
+        const int *vl = vlist + (cnt ? estart[e] : 0);
+        if (cmax <= 4) vx_fold_lane<4>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
+        else if (cmax <= 8) vx_fold_lane<8>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
+        else if (cmax <= 16) vx_fold_lane<16>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
+        else vx_fold_lane<32>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
+        if (cnt) {
+            const double dn = static_cast<double>(cnt);
+            double *o = vpts + 3 * (static_cast<size_t>(q.base) + v);
+            o[0] = acc[0] / dn;
+            o[1] = acc[1] / dn;
+            o[2] = acc[2] / dn;
+            vx_reset(e, hkey, hfirst, ecnt, efill);
+        }
+    }
+}
+
+// workgroup per voxel of more than kVxSmall pixels: windows of kVxWin list positions, the
+// window's entries ordered through a bitmap, their points staged in LDS and added by one lane
+__global__ __launch_bounds__(kVxChunk) void k_vx_big(const int *__restrict__ nbig, const int2 *__restrict__ big,
+                                                     const int *__restrict__ slot_frame,
+                                                     const int *__restrict__ slot_pix, const unsigned *__restrict__ pix_list,
+                                                     const float *__restrict__ depth, const double *__restrict__ intr,
+                                                     const double *__restrict__ pose, BpDev pr,
+                                                     const int *__restrict__ vox_entry, const int *__restrict__ estart,
+                                                     const int *__restrict__ vlist, unsigned long long *__restrict__ hkey,
+                                                     int *__restrict__ hfirst, int *__restrict__ ecnt,
+                                                     int *__restrict__ efill, double *__restrict__ vpts)
+{
+    __shared__ unsigned bm[kVxWin / 32];
+    __shared__ int sk[kVxWin];
+    __shared__ double sp[3 * kVxWin];
+    __shared__ int ws[kVxChunk / 64];
+    __shared__ int s_next;
+    const int NB = *nbig;
+    const int t = threadIdx.x;
+    for (int b = blockIdx.x; b < NB; b += gridDim.x) {
+        const int s = big[b].x, v = big[b].y;
+        const int base = slot_pix[s];
+        const int e = vox_entry[base + v];
+        const int cnt = ecnt[e];
+        const int *vl = vlist + estart[e];
+        double ax = 0.0, ay = 0.0, az = 0.0;  // thread 0's running sums
+        int w0 = -1;                          // entries < w0 are done
+        while (true) {
+            // next window: from the smallest entry >= w0
+            int mn = INT_MAX;
+            for (int i = t; i < cnt; i += kVxChunk) {
+                const int k = vl[i];
+                if (k >= w0) mn = min(mn, k);
+            }
+            mn = wave_min_i(mn);
+            if ((t & 63) == 0) ws[t >> 6] = mn;
+            if (t < kVxWin / 32) bm[t] = 0u;
+            __syncthreads();
+            if (t == 0) s_next = min(min(ws[0], ws[1]), min(ws[2], ws[3]));
+            __syncthreads();
+            const int lo = s_next;
+            if (lo == INT_MAX) break;
+            for (int i = t; i < cnt; i += kVxChunk) {
+                const int k = vl[i];
+                if (k >= lo && k - lo < kVxWin) atomicOr(&bm[(k - lo) >> 5], 1u << ((k - lo) & 31));
+            }
+            __syncthreads();
+            // ordered extraction: word popcounts scanned by wave 0 (kVxWin / 32 <= 64 words)
+            if (t < 64) {
+                const unsigned w = t < kVxWin / 32 ? bm[t] : 0u;
+                int x = __popc(w);
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int y = __shfl_up(x, d, 64);
+                    if (t >= d) x += y;
+                }
+                int pos = x - __popc(w);
+                unsigned ww = w;
+                while (ww) {
+                    const int bit = __ffs(ww) - 1;
+                    ww &= ww - 1;
+                    sk[pos++] = lo + 32 * t + bit;
+                }
+                if (t == 63) s_next = x;  // entries in the window
+            }
+            __syncthreads();
+            const int nw = s_next;
+            for (int i = t; i < nw; i += kVxChunk)
+                vx_point(s, sk[i], base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, sp[3 * i], sp[3 * i + 1],
+                         sp[3 * i + 2]);
+            __syncthreads();
+            if (t == 0)
+                for (int i = 0; i < nw; i++) {
+                    ax = ax + sp[3 * i];
+                    ay = ay + sp[3 * i + 1];
+                    az = az + sp[3 * i + 2];
+                }
+            w0 = lo + kVxWin;
+            __syncthreads();
+        }
+        if (t == 0) {
+            const double dn = static_cast<double>(cnt);
+            double *o = vpts + 3 * (static_cast<size_t>(base) + v);
+            o[0] = ax / dn;
+            o[1] = ay / dn;
+            o[2] = az / dn;
+            vx_reset(e, hkey, hfirst, ecnt, efill);
+        }
+        __syncthreads();
+    }
+}
 // ---------------------------------------------------------------------------------------------
 // (a4) denoise (geometry.py:9-24), workgroup per slot
 // ---------------------------------------------------------------------------------------------
@@ -1659,19 +1937,14 @@ __global__ __launch_bounds__(256) void k_bp_query(
     const int *__restrict__ gidx, const unsigned long long *__restrict__ gcell, const int *__restrict__ gstart,
     unsigned gnb, unsigned long long *__restrict__ bm, int PW, int *__restrict__ tmp, int tmp_cap,
     int *__restrict__ tmp_top, int *__restrict__ slot_nn, int *__restrict__ slot_toff, int *__restrict__ slot_cov,
-    int *__restrict__ ovf, const int *__restrict__ order, int *__restrict__ ticket)
+    int *__restrict__ ovf, const int *__restrict__ order)
 {
-    __shared__ int s_lo, s_hi, s_cov, s_base, s_next;
+    __shared__ int s_lo, s_hi, s_cov, s_base;
     __shared__ int ws[4];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id();
     unsigned long long *mb = bm + static_cast<size_t>(blockIdx.x) * PW;
-    while (true) {  // slots from a ticket, largest first (k_bp_vox_order)
-        if (t == 0) s_next = atomicAdd(ticket, 1);
-        __syncthreads();
-        const int idx = s_next;
-        __syncthreads();  // every thread has read it before thread 0 can take the next one
-        if (idx >= NS) break;
+    for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {  // largest slots first (k_bp_vox_order)
         const int s = order[idx];
         const int ns = slot_ns[s];
         if (ns < pr.few) {  // :109 (uniform)
