@@ -111,14 +111,12 @@ struct mc_ctx {
     DevBuf d_band, d_present, d_fflags, d_cand, d_npix, d_csidx, d_poff, d_slot_of, d_bpstat;
     DevBuf d_slot_frame, d_slot_id, d_slot_np, d_slot_pix, d_slot_nv, d_slot_m, d_slot_ns, d_slot_box, d_slot_nn,
         d_slot_toff, d_slot_cov;
-    DevBuf d_pix_list, d_hkey, d_hfirst, d_vox_entry, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
+    DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
         d_blist, d_ncnt, d_par, d_droot, d_rnk, d_lab, d_ccnt, d_ssidx, d_avg, d_qpts;
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
-    // voxel_down_sample: per hash entry pixel counts / fill counters (zero at rest) and list starts;
-    // per pixel its entry and the voxel lists; chunk table; per slot min-bound images and list bumps
-    DevBuf d_vx_ecnt, d_vx_efill, d_vx_estart, d_vx_pent, d_vx_list, d_vx_nch, d_vx_choff, d_vx_chslot, d_vx_chnf,
-        d_vx_chfx, d_vx_min, d_vx_bump, d_vx_big;
+    // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
+    DevBuf d_vx_pvid, d_vx_list, d_vx_fb;
     int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
@@ -335,9 +333,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
-                         &ctx->d_vx_ecnt, &ctx->d_vx_efill, &ctx->d_vx_estart, &ctx->d_vx_pent, &ctx->d_vx_list,
-                         &ctx->d_vx_nch, &ctx->d_vx_choff, &ctx->d_vx_chslot, &ctx->d_vx_chnf, &ctx->d_vx_chfx,
-                         &ctx->d_vx_min, &ctx->d_vx_bump, &ctx->d_vx_big};
+                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_acc, &ctx->d_hvid};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (int b = 0; b < 2; b++) {
@@ -1504,8 +1500,7 @@ enum BpStat : int {
     BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
     BS_CLS,             // 5 denoise size-class counts (4 LDS classes + the global-memory kernel)
     BS_TK = BS_CLS + 5,  // ticket counters of the LDS classes
-    BS_VXCH = BS_TK + 4,  // voxel chunks of the batch
-    BS_VXBIG,            // voxels of more than kVxSmall pixels
+    BS_VXFB = BS_TK + 4,  // slots k_bp_voxel_lds hands to k_bp_voxel
     BS_COUNT
 };
 
@@ -1546,32 +1541,21 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_slot_box.reserve(slots * 6 * 4);
     ctx->d_cls_list.reserve(5 * slots * 4);
     ctx->d_vox_order.reserve(slots * 4);
-    const size_t chunks = px / mc::kVxChunk + slots + 2;
-    ctx->d_vx_nch.reserve((slots + 1) * 4);
-    ctx->d_vx_choff.reserve((slots + 2) * 4);
-    ctx->d_vx_chslot.reserve(chunks * 4);
-    ctx->d_vx_chnf.reserve(chunks * 4);
-    ctx->d_vx_chfx.reserve((chunks + 1) * 4);
-    ctx->d_vx_min.reserve(slots * 3 * 8);
-    ctx->d_vx_bump.reserve(slots * 4);
+    ctx->d_vx_fb.reserve(slots * 4);
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
     ctx->d_nbl.reserve(nbl_offset(ctx, 4) * 2);
     ctx->d_lean.reserve(static_cast<size_t>(ctx->num_cu) * mc::kBpLeanInts<3072> * 4);
     if (ctx->bp_px_cap < px) {
         ctx->d_pix_list.reserve(px * 4);
         ctx->d_hkey.reserve(2 * px * 8);
+        ctx->d_hvid.reserve(2 * px * 4);
         ctx->d_hfirst.reserve(2 * px * 4);
-        ctx->d_vx_ecnt.reserve(2 * px * 4);
-        ctx->d_vx_efill.reserve(2 * px * 4);
-        // empty key, INT_MAX first pixel, zero counts: restored by k_vx_fold / k_vx_big
-        fill_u32(s, ctx->d_hkey.ptr, 4 * px, 0xFFFFFFFFu);
-        fill_u32(s, ctx->d_hfirst.ptr, 2 * px, 0x7FFFFFFFu);
-        fill_u32(s, ctx->d_vx_ecnt.ptr, 2 * px, 0u);
-        fill_u32(s, ctx->d_vx_efill.ptr, 2 * px, 0u);
-        ctx->d_vx_estart.reserve(2 * px * 4);
-        ctx->d_vx_pent.reserve(px * 4);
+        fill_u32(s, ctx->d_hkey.ptr, 4 * px, 0xFFFFFFFFu);  // empty key, kept empty by k_bp_voxel
+        fill_u32(s, ctx->d_hvid.ptr, 2 * px, 0xFFFFFFFFu);  // -1
+        fill_u32(s, ctx->d_hfirst.ptr, 2 * px, 0x7FFFFFFFu);  // INT_MAX
+        ctx->d_acc.reserve(px * 4 * 8);
+        ctx->d_vx_pvid.reserve(px * 4);
         ctx->d_vx_list.reserve(px * 4);
-        ctx->d_vx_big.reserve(px * 8);  // (slot, voxel) of every voxel folded by k_vx_big (MC_VX_SMALL=0: all)
         ctx->d_vox_entry.reserve(px * 4);
         ctx->d_vpts.reserve(px * 3 * 8);
         ctx->d_pcell.reserve(px * 8);
@@ -1832,9 +1816,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // global-memory kernel for every slot)
         int min_cls = 0;
         if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(4, std::max(0, atoi(e)));
-        // test knob: largest voxel folded by one lane (smaller values send more voxels to k_vx_big)
-        int vx_small = mc::kVxSmall;
-        if (const char *e = getenv("MC_VX_SMALL")) vx_small = std::min(mc::kVxSmall, std::max(0, atoi(e)));
+        // test knob: MC_VX_GLOBAL=1 hands every slot to the global-hash voxel kernel
+        const bool vx_global = getenv("MC_VX_GLOBAL") && atoi(getenv("MC_VX_GLOBAL")) != 0;
         // frames per batch: bounded pixel capacity of the per-slot arrays
         // (≈ 180 B of per-batch arrays per pixel: 192 M pixels ≈ 35 GB of HBM; a C3 frame is 2.76 M
         // pixels, so a batch holds ~70 frames and the per-batch sync and slot tails amortise)
@@ -1900,46 +1883,19 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_voxel");
-                hipLaunchKernelGGL(mc::k_vx_nch, grid_for(nslot), dim3(256), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
-                                   ctx->d_vx_nch.as<int>(), ctx->d_vx_min.as<unsigned long long>(), ctx->d_vx_bump.as<int>());
-                mc::scan_device_n(s, ctx->d_vx_nch.as<int>(), ctx->d_vx_choff.as<int>(), st + BS_NS, 0, st + BS_VXCH);
-                hipLaunchKernelGGL(mc::k_vx_chunks, grid_for(nslot), dim3(256), 0, s, st + BS_NS, ctx->d_vx_nch.as<int>(),
-                                   ctx->d_vx_choff.as<int>(), ctx->d_vx_chslot.as<int>());
-                const dim3 vg(ctx->num_cu * 8);
-                const int *nch = st + BS_VXCH, *chs = ctx->d_vx_chslot.as<int>(), *cho = ctx->d_vx_choff.as<int>();
-                unsigned long long *vmin = ctx->d_vx_min.as<unsigned long long>();
-                hipLaunchKernelGGL(mc::k_vx_bound, vg, dim3(mc::kVxChunk), 0, s, nch, chs, cho, ctx->d_slot_frame.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
-                                   KB, TB, dv, vmin);
-                hipLaunchKernelGGL(mc::k_vx_hash, vg, dim3(mc::kVxChunk), 0, s, nch, chs, cho, ctx->d_slot_frame.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
-                                   KB, TB, dv, vmin, ctx->d_hkey.as<unsigned long long>(), ctx->d_hfirst.as<int>(),
-                                   ctx->d_vx_ecnt.as<int>(), ctx->d_vx_pent.as<int>(), st + BS_VOXERR);
-                hipLaunchKernelGGL(mc::k_vx_alloc, vg, dim3(mc::kVxChunk), 0, s, nch, chs, cho, ctx->d_slot_np.as<int>(),
-                                   ctx->d_slot_pix.as<int>(), ctx->d_vx_pent.as<int>(), ctx->d_hfirst.as<int>(),
-                                   ctx->d_vx_ecnt.as<int>(), ctx->d_vx_bump.as<int>(), ctx->d_vx_estart.as<int>(),
-                                   ctx->d_vx_chnf.as<int>());
-                mc::scan_device_n(s, ctx->d_vx_chnf.as<int>(), ctx->d_vx_chfx.as<int>(), nch, 0, nullptr);
-                hipLaunchKernelGGL(mc::k_vx_scatter, vg, dim3(mc::kVxChunk), 0, s, nch, chs, cho, ctx->d_vx_nch.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_vx_pent.as<int>(),
-                                   ctx->d_hfirst.as<int>(), ctx->d_vx_estart.as<int>(), ctx->d_vx_efill.as<int>(),
-                                   ctx->d_vx_chfx.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vox_entry.as<int>(),
-                                   ctx->d_slot_nv.as<int>());
-                hipLaunchKernelGGL(mc::k_vx_fold, vg, dim3(mc::kVxChunk), 0, s, nch, chs, cho, ctx->d_slot_frame.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(),
-                                   ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv, ctx->d_vox_entry.as<int>(),
-                                   ctx->d_vx_estart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_hkey.as<unsigned long long>(),
-                                   ctx->d_hfirst.as<int>(), ctx->d_vx_ecnt.as<int>(), ctx->d_vx_efill.as<int>(),
-                                   ctx->d_vpts.as<double>(), ctx->d_vx_big.as<int2>(), st + BS_VXBIG, vx_small);
-                hipLaunchKernelGGL(mc::k_vx_big, dim3(ctx->num_cu * 4), dim3(mc::kVxChunk), 0, s, st + BS_VXBIG,
-                                   ctx->d_vx_big.as<int2>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_pix.as<int>(),
-                                   ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv, ctx->d_vox_entry.as<int>(),
-                                   ctx->d_vx_estart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_hkey.as<unsigned long long>(),
-                                   ctx->d_hfirst.as<int>(), ctx->d_vx_ecnt.as<int>(), ctx->d_vx_efill.as<int>(),
-                                   ctx->d_vpts.as<double>());
-                // largest slots first for k_bp_query
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
                                    ctx->d_vox_order.as<int>());
+                hipLaunchKernelGGL(mc::k_bp_voxel_lds, dim3(ctx->num_cu * 2), dim3(mc::kVxT), 0, s, st + BS_NS,
+                                   ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
+                                   ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
+                                   ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
+                                   ctx->d_slot_nv.as<int>(), ctx->d_vx_fb.as<int>(), st + BS_VXFB, vx_global ? 1 : 0);
+                hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB,
+                                   ctx->d_vx_fb.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
+                                   ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
+                                   ctx->d_hkey.as<unsigned long long>(), ctx->d_hvid.as<int>(), ctx->d_hfirst.as<int>(),
+                                   ctx->d_vox_entry.as<int>(), ctx->d_acc.as<double>(), ctx->d_vpts.as<double>(),
+                                   ctx->d_slot_nv.as<int>(), st + BS_VOXERR);
                 bp_debug_sync(s, "bp_voxel");
             }
             {

@@ -124,6 +124,32 @@ __device__ __forceinline__ void block_minmax3(double mn[3], double mx[3], double
     __syncthreads();
 }
 
+template <int NW>
+__device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], double *red)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const double a = wave_min_d(mn[c]), b = wave_max_d(mx[c]);
+        if (lane == 0) {
+            red[c * NW + wv] = a;
+            red[3 * NW + c * NW + wv] = b;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        double a = red[c * NW], b = red[3 * NW + c * NW];
+        for (int w = 1; w < NW; w++) {
+            a = fmin(a, red[c * NW + w]);
+            b = fmax(b, red[3 * NW + c * NW + w]);
+        }
+        mn[c] = a;
+        mx[c] = b;
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------------------------------------
 // scene grid (built once per scene): points bucketed by cells of 2r, sorted copy as float4
 // ---------------------------------------------------------------------------------------------
@@ -312,26 +338,24 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
 }
 
 // ---------------------------------------------------------------------------------------------
-// (a3) voxel_down_sample(0.01) (:105), pixel-parallel over the whole batch
+// (a3) voxel_down_sample(0.01) (:105), workgroup per slot
 // ---------------------------------------------------------------------------------------------
 // Open3D: min bound - voxel/2, index = floor((p - vmin) / voxel), per-voxel sum in input order,
 // mean = sum / count.  Output order (u2): first occurrence in pixel order.
-// Only the additions inside one voxel are ordered, so nothing walks a slot's pixels in sequence:
-// every slot's pixel list is cut into chunks of kVxChunk pixels (one workgroup each, any order),
-//   k_vx_nch / scan / k_vx_chunks   chunk table (chunk -> slot), per-slot min bound reset
-//   k_vx_bound      per-slot min bound (order-free: atomicMin on order-preserving u64 images)
-//   k_vx_hash       voxel key -> the slot's hash (2 entries per pixel, empty at rest); per entry
-//                   the first pixel (atomicMin) and the pixel count (wave-aggregated)
-//   k_vx_alloc      first pixels: the voxel's list range (bump per slot); firsts per chunk
-//   scan            voxel ids = first pixels in pixel order (chunk prefix - the slot's first chunk)
-//   k_vx_scatter    pixel -> its voxel's list (unordered); first pixel -> voxel id -> entry
-//   k_vx_fold       lane per voxel (<= kVxSmall pixels): sort the list (bitonic network in
-//                   registers), then add the points in pixel order; larger voxels -> k_vx_big
-//   k_vx_big        workgroup per large voxel: the list ordered through bitmaps of 1024-pixel
-//                   windows, points staged in LDS, one lane adds them in order
-// The hash entries and per-entry counters return to empty / zero in the fold kernels.
-// Largest slots first for k_bp_query (its per-slot time grows with the slot size): slots binned
-// by floor(log2(pixels)), bins in descending order.  One workgroup.
+// k_bp_voxel_lds (every slot, largest first): the slot's voxel hash and per-voxel counters in LDS.
+//   0. min bound (order-free block reduction)
+//   1. chunks of kVxT pixels in list order: relative voxel key (10 bits per axis) -> LDS hash; a
+//      new voxel's id = rank of its first pixel (LDS atomicMin of the lane, ordered block scan);
+//      per pixel its voxel id (global scratch), per voxel its pixel count
+//   2. counts -> list offsets (block scan)
+//   3. chunks again: every pixel to its voxel's list at a stable position (ranks within a wave by
+//      ballot groups, waves in order), so each voxel's list is in pixel order
+//   4. a thread per voxel adds its list's points in order; mean
+// Only LDS between the chunk barriers: no global atomics, no global read-modify-write chains.
+// A slot whose voxel coordinates span >= 1024 voxels on an axis or that has more than kVxV voxels
+// is listed for k_bp_voxel (the global-hash kernel below) instead.
+// Largest slots first (their per-slot time grows with the pixel count): slots binned by
+// floor(log2(pixels)), bins in descending order.  One workgroup.
 __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ dNS, const int *__restrict__ slot_np,
                                                        int *__restrict__ order)
 {
@@ -353,422 +377,353 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
     for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1)] = s;
 }
 
-constexpr int kVxChunk = 256;  // pixels per chunk (= threads of the chunk kernels)
-constexpr int kVxSmall = 32;   // largest voxel (in pixels) folded by one lane
-constexpr int kVxWin = 1024;   // pixel window of the large-voxel bitmaps
+constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
+constexpr int kVxH = 6144;       // LDS hash entries (load <= 2/3)
+constexpr int kVxV = 4096;       // voxels per slot in LDS (hash + counters: 64 KB, two workgroups per CU)
+constexpr unsigned kVxEmpty = ~0u;
 
-// order-preserving u64 image of a double (a < b <=> img(a) < img(b), NaN aside)
-__device__ __forceinline__ unsigned long long dbl_ord(double v)
-{
-    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
-    return (b >> 63) ? ~b : (b | (1ull << 63));
-}
-__device__ __forceinline__ double dbl_unord(unsigned long long u)
-{
-    return __longlong_as_double(static_cast<long long>((u >> 63) ? (u & ~(1ull << 63)) : ~u));
-}
-
-// chunks per slot; min-bound images and list bumps reset
-__global__ __launch_bounds__(256) void k_vx_nch(const int *__restrict__ dNS, const int *__restrict__ slot_np,
-                                                int *__restrict__ nch, unsigned long long *__restrict__ vmin,
-                                                int *__restrict__ bump)
-{
-    const int NS = *dNS;
-    for (int s = blockIdx.x * 256 + threadIdx.x; s < NS; s += gridDim.x * 256) {
-        nch[s] = (slot_np[s] + kVxChunk - 1) / kVxChunk;
-        vmin[3 * s] = vmin[3 * s + 1] = vmin[3 * s + 2] = ~0ull;
-        bump[s] = 0;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_vx_chunks(const int *__restrict__ dNS, const int *__restrict__ nch,
-                                                   const int *__restrict__ choff, int *__restrict__ chslot)
-{
-    const int NS = *dNS;
-    for (int s = blockIdx.x * 256 + threadIdx.x; s < NS; s += gridDim.x * 256) {
-        const int o = choff[s], n = nch[s];
-        for (int j = 0; j < n; j++) chslot[o + j] = s;
-    }
-}
-
-// the pixel of chunk c handled by this thread: slot, index k within the slot's list, validity
-struct VxPix {
-    int s, j, k, n, base;
-    bool valid;
-};
-__device__ __forceinline__ VxPix vx_pix(int c, const int *__restrict__ chslot, const int *__restrict__ choff,
-                                        const int *__restrict__ slot_np, const int *__restrict__ slot_pix)
-{
-    VxPix q;
-    q.s = chslot[c];
-    q.j = c - choff[q.s];
-    q.n = slot_np[q.s];
-    q.base = slot_pix[q.s];
-    q.k = q.j * kVxChunk + static_cast<int>(threadIdx.x);
-    q.valid = q.k < q.n;
-    return q;
-}
-
-// world point of list entry k of slot s (frame f)
-__device__ __forceinline__ void vx_point(int s, int k, int base, const int *__restrict__ slot_frame,
-                                         const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
-                                         const double *__restrict__ intr, const double *__restrict__ pose, int H, int W,
+__device__ __forceinline__ void vx_point(const unsigned *__restrict__ pl, const float *__restrict__ dep,
+                                         const double *__restrict__ K, const double *__restrict__ T, int W, int k,
                                          double &x, double &y, double &z)
 {
-    const int f = slot_frame[s];
-    const unsigned i = pix_list[base + k];
-    bp_world(intr + 4 * static_cast<size_t>(f), pose + 16 * static_cast<size_t>(f), static_cast<int>(i % W),
-             static_cast<int>(i / W), depth[static_cast<size_t>(f) * H * W + i], x, y, z);
+    const unsigned i = pl[k];
+    bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], x, y, z);
 }
 
-__global__ __launch_bounds__(kVxChunk) void k_vx_bound(const int *__restrict__ dNCH, const int *__restrict__ chslot,
-                                                       const int *__restrict__ choff, const int *__restrict__ slot_frame,
-                                                       const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
-                                                       const unsigned *__restrict__ pix_list,
-                                                       const float *__restrict__ depth, const double *__restrict__ intr,
-                                                       const double *__restrict__ pose, BpDev pr,
-                                                       unsigned long long *__restrict__ vmin)
+__global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
+                                                       const int *__restrict__ slot_frame, const int *__restrict__ slot_np,
+                                                       const int *__restrict__ slot_pix,
+                                                       const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
+                                                       const double *__restrict__ intr, const double *__restrict__ pose,
+                                                       BpDev pr, int *__restrict__ pvid, int *__restrict__ vlist,
+                                                       double *__restrict__ vpts, int *__restrict__ slot_nv,
+                                                       int *__restrict__ fb_list, int *__restrict__ fb_cnt, int force_fb)
 {
-    __shared__ double red[24];
-    const int NCH = *dNCH;
-    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
-        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
+    constexpr int NW = kVxT / 64;
+    __shared__ unsigned hkey[kVxH];
+    __shared__ unsigned hval[kVxH];  // (voxel id << 16) | lowest lane of the chunk; 0xFFFF: none yet
+    __shared__ int vcur[kVxV];       // counts, then list cursors (end of each voxel's list after 3.)
+    __shared__ int gb[NW][64];
+    __shared__ double red[6 * NW];
+    __shared__ int ws[NW];
+    __shared__ int s_flag;
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    const int W = pr.W;
+    for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
+        const int s = order[idx];
+        if (force_fb) {  // test knob: every slot to the global-hash kernel
+            if (t == 0) fb_list[atomicAdd(fb_cnt, 1)] = s;
+            continue;
+        }
+        const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
+        const double *K = intr + 4 * static_cast<size_t>(f);
+        const double *T = pose + 16 * static_cast<size_t>(f);
+        const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
+        const unsigned *pl = pix_list + base;
+        for (int i = t; i < kVxH; i += kVxT) {
+            hkey[i] = kVxEmpty;
+            hval[i] = ~0u;
+        }
+        for (int i = t; i < kVxV; i += kVxT) vcur[i] = 0;
+        if (t == 0) s_flag = 0;
+        // 0. min bound
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        if (q.valid) vx_point(q.s, q.k, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, mn[0], mn[1], mn[2]);
-        block_minmax3(mn, mx, red);
-        const int d = threadIdx.x;
-        if (d < 3) atomicMin(&vmin[3 * q.s + d], dbl_ord(d == 0 ? mn[0] : d == 1 ? mn[1] : mn[2]));
-    }
-}
-
-__device__ __forceinline__ void vx_vmin(const unsigned long long *__restrict__ vmin, int s, double vs, double v[3])
-{
+        for (int k = t; k < n; k += kVxT) {
+            double p[3];
+            vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
 #pragma unroll
-    for (int c = 0; c < 3; c++) v[c] = dbl_unord(vmin[3 * s + c]) - vs * 0.5;
-}
-
-__global__ __launch_bounds__(kVxChunk) void k_vx_hash(const int *__restrict__ dNCH, const int *__restrict__ chslot,
-                                                      const int *__restrict__ choff, const int *__restrict__ slot_frame,
-                                                      const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
-                                                      const unsigned *__restrict__ pix_list,
-                                                      const float *__restrict__ depth, const double *__restrict__ intr,
-                                                      const double *__restrict__ pose, BpDev pr,
-                                                      const unsigned long long *__restrict__ vmin,
-                                                      unsigned long long *__restrict__ hkey, int *__restrict__ hfirst,
-                                                      int *__restrict__ ecnt, int *__restrict__ pent,
-                                                      int *__restrict__ errflag)
-{
-    const int NCH = *dNCH;
-    const int lane = lane_id();
-    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
-        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
-        int e = -1;
-        if (q.valid) {
-            double vm[3], p[3];
-            vx_vmin(vmin, q.s, pr.vs, vm);
-            vx_point(q.s, q.k, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, p[0], p[1], p[2]);
-            long long ix[3];
+            for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
+        }
+        block_minmax3_nw<NW>(mn, mx, red);
+        double vmin[3];
 #pragma unroll
-            for (int d = 0; d < 3; d++) {
-                ix[d] = static_cast<long long>(floor((p[d] - vm[d]) / pr.vs));
-                if (ix[d] < 0 || ix[d] >= (1ll << 21)) {
-                    atomicOr(errflag, 1);
-                    ix[d] = ix[d] < 0 ? 0 : (1ll << 21) - 1;
+        for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
+        // 1. voxel ids in first-occurrence order, per-pixel ids, per-voxel counts
+        int nv = 0;
+        for (int c0 = 0; c0 < n; c0 += kVxT) {
+            const int k = c0 + t;
+            int h = -1;
+            if (k < n) {
+                double p[3];
+                vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
+                unsigned key = 0;
+                bool fits = true;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const double r = floor((p[c] - vmin[c]) / pr.vs);
+                    fits = fits && r >= 0.0 && r < 1024.0;
+                    key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
+                }
+                if (!fits) {
+                    s_flag = 1;
+                } else {
+                    unsigned e = mod_mul(key * 0x9E3779B1u, kVxH);
+                    for (int probe = 0; probe < kVxH; probe++) {
+                        unsigned cur = hkey[e];
+                        if (cur == kVxEmpty) {
+                            cur = atomicCAS(&hkey[e], kVxEmpty, key);
+                            if (cur == kVxEmpty) cur = key;
+                        }
+                        if (cur == key) {
+                            h = static_cast<int>(e);
+                            break;
+                        }
+                        e = e + 1 == kVxH ? 0u : e + 1;
+                    }
+                    if (h < 0) s_flag = 1;
+                    else if ((hval[h] >> 16) == 0xFFFFu) atomicMin(&hval[h], 0xFFFF0000u | static_cast<unsigned>(t));
                 }
             }
-            const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
-            const unsigned C = 2u * static_cast<unsigned>(q.n);
-            unsigned long long *hk = hkey + 2 * static_cast<size_t>(q.base);
-            unsigned h = mod_mul(bp_hash64(key), C);
-            while (true) {
-                unsigned long long cur = hk[h];
-                if (cur == kEmptyKey) {
-                    cur = atomicCAS(&hk[h], kEmptyKey, key);
-                    if (cur == kEmptyKey) cur = key;
+            __syncthreads();
+            const bool first = h >= 0 && hval[h] == (0xFFFF0000u | static_cast<unsigned>(t));
+            int tot;
+            const int ex = block_excl_scan<kVxT>(first ? 1 : 0, ws, tot);
+            if (first) {
+                const int v = nv + ex;
+                if (v < kVxV) hval[h] = (static_cast<unsigned>(v) << 16) | 0xFFFFu;
+                else s_flag = 1;
+            }
+            __syncthreads();
+            if (h >= 0) {
+                const unsigned v = hval[h] >> 16;
+                if (v < static_cast<unsigned>(kVxV)) {
+                    pvid[base + k] = static_cast<int>(v);
+                    atomicAdd(&vcur[v], 1);
                 }
-                if (cur == key) break;
-                h = h + 1 == C ? 0 : h + 1;
             }
-            e = static_cast<int>(2 * static_cast<unsigned>(q.base) + h);
-            pent[q.base + q.k] = e;
-        }
-        // lanes of one entry (consecutive pixels mostly share voxels): the lowest lane (smallest
-        // k) records the group's first pixel and count
-        unsigned long long act = __ballot(e >= 0);
-        while (act) {
-            const int L = __ffsll(static_cast<long long>(act)) - 1;
-            const int ee = __shfl(e, L, 64);
-            const unsigned long long m = __ballot(e == ee);
-            if (lane == L) {
-                atomicMin(&hfirst[ee], q.k);
-                atomicAdd(&ecnt[ee], __popcll(m));
-            }
-            act &= ~m;
-        }
-    }
-}
-
-// first pixel of a voxel: its list range [estart, estart + ecnt) inside the slot's pixel range;
-// first pixels per chunk -> chnf
-__global__ __launch_bounds__(kVxChunk) void k_vx_alloc(const int *__restrict__ dNCH, const int *__restrict__ chslot,
-                                                       const int *__restrict__ choff, const int *__restrict__ slot_np,
-                                                       const int *__restrict__ slot_pix, const int *__restrict__ pent,
-                                                       const int *__restrict__ hfirst, const int *__restrict__ ecnt,
-                                                       int *__restrict__ bump, int *__restrict__ estart,
-                                                       int *__restrict__ chnf)
-{
-    __shared__ int ws[kVxChunk / 64];
-    __shared__ int s_off;
-    const int NCH = *dNCH;
-    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
-        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
-        int e = -1, cnt = 0;
-        if (q.valid) {
-            e = pent[q.base + q.k];
-            if (hfirst[e] == q.k) cnt = ecnt[e];
-        }
-        int tot;
-        const int ex = block_excl_scan<kVxChunk>(cnt, ws, tot);
-        const int nf = block_sum<kVxChunk>(cnt > 0 ? 1 : 0, ws);
-        if (threadIdx.x == 0) {
-            s_off = tot ? atomicAdd(&bump[q.s], tot) : 0;
-            chnf[c] = nf;
+            nv += tot;
         }
         __syncthreads();
-        if (cnt > 0) estart[e] = q.base + s_off + ex;
+        if (s_flag) {  // (uniform) overflow: the global-hash kernel takes the slot
+            if (t == 0) fb_list[atomicAdd(fb_cnt, 1)] = s;
+            __syncthreads();
+            continue;
+        }
+        // 2. counts -> exclusive offsets
+        {
+            int carry = 0;
+            for (int v0 = 0; v0 < nv; v0 += kVxT) {
+                const int v = v0 + t;
+                const int c = v < nv ? vcur[v] : 0;
+                int tot;
+                const int ex = block_excl_scan<kVxT>(c, ws, tot);
+                if (v < nv) vcur[v] = carry + ex;
+                carry += tot;
+            }
+        }
         __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kVxChunk) void k_vx_scatter(const int *__restrict__ dNCH, const int *__restrict__ chslot,
-                                                         const int *__restrict__ choff, const int *__restrict__ nch,
-                                                         const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
-                                                         const int *__restrict__ pent, const int *__restrict__ hfirst,
-                                                         const int *__restrict__ estart, int *__restrict__ efill,
-                                                         const int *__restrict__ chfx, int *__restrict__ vlist,
-                                                         int *__restrict__ vox_entry, int *__restrict__ slot_nv)
-{
-    __shared__ int ws[kVxChunk / 64];
-    const int NCH = *dNCH;
-    const int lane = lane_id();
-    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
-        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
-        const int e = q.valid ? pent[q.base + q.k] : -1;
-        const bool first = q.valid && hfirst[e] == q.k;
-        unsigned long long act = __ballot(e >= 0);
-        while (act) {
-            const int L = __ffsll(static_cast<long long>(act)) - 1;
-            const int ee = __shfl(e, L, 64);
-            const unsigned long long m = __ballot(e == ee);
-            int b = 0;
-            if (lane == L) b = estart[ee] + atomicAdd(&efill[ee], __popcll(m));
-            b = __shfl(b, L, 64);
-            if (e == ee) vlist[b + __popcll(m & ((1ull << lane) - 1))] = q.k;
-            act &= ~m;
+        // 3. stable scatter: list positions in pixel order within every voxel
+        for (int c0 = 0; c0 < n; c0 += kVxT) {
+            const int k = c0 + t;
+            const int v = k < n ? pvid[base + k] : -1;
+            int rank = 0, leader = 0, cnt = 0;
+            unsigned long long act = __ballot(v >= 0);
+            while (act) {
+                const int L = __ffsll(static_cast<long long>(act)) - 1;
+                const int vv = __shfl(v, L, 64);
+                const unsigned long long m = __ballot(v == vv);
+                if (v == vv) {
+                    rank = __popcll(m & ((1ull << lane) - 1ull));
+                    leader = L;
+                    cnt = __popcll(m);
+                }
+                act &= ~m;
+            }
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                if (wv == w && v >= 0 && lane == leader) {
+                    gb[w][lane] = vcur[v];
+                    vcur[v] += cnt;
+                }
+                __syncthreads();
+            }
+            if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
         }
-        int tot;
-        const int ex = block_excl_scan<kVxChunk>(first ? 1 : 0, ws, tot);
-        const int c0 = choff[q.s];
-        if (first) vox_entry[q.base + chfx[c] - chfx[c0] + ex] = e;
-        if (threadIdx.x == 0 && q.j == nch[q.s] - 1) slot_nv[q.s] = chfx[c0 + nch[q.s]] - chfx[c0];
-    }
-}
-
-// ascending bitonic sort of S register values (S a power of two)
-template <int S>
-__device__ __forceinline__ void bitonic_sort_regs(int (&a)[S])
-{
+        __syncthreads();
+        // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
+        for (int v = t; v < nv; v += kVxT) {
+            const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
+            const int *vl = vlist + base;
+            double ax = 0.0, ay = 0.0, az = 0.0;
+            int j = b0;
+            for (; j + 4 <= b1; j += 4) {
+                double q[4][3];
 #pragma unroll
-    for (int k = 2; k <= S; k <<= 1)
+                for (int u = 0; u < 4; u++) vx_point(pl, dep, K, T, W, vl[j + u], q[u][0], q[u][1], q[u][2]);
 #pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < S; i++) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const int x = a[i], y = a[l];
-                    const int lo = min(x, y), hi = max(x, y);
-                    const bool up = (i & k) == 0;
-                    a[i] = up ? lo : hi;
-                    a[l] = up ? hi : lo;
+                for (int u = 0; u < 4; u++) {
+                    ax = ax + q[u][0];
+                    ay = ay + q[u][1];
+                    az = az + q[u][2];
                 }
             }
-}
-
-// one lane: the cnt (<= S) list entries of a voxel, sorted, points added in that order
-template <int S>
-__device__ __forceinline__ void vx_fold_lane(const int *__restrict__ vl, int cnt, int s, int base,
-                                             const int *__restrict__ slot_frame, const unsigned *__restrict__ pix_list,
-                                             const float *__restrict__ depth, const double *__restrict__ intr,
-                                             const double *__restrict__ pose, int H, int W, double acc[3])
-{
-    int key[S];
-#pragma unroll
-    for (int i = 0; i < S; i++) key[i] = i < cnt ? vl[i] : INT_MAX;
-    bitonic_sort_regs<S>(key);
-    double ax = 0.0, ay = 0.0, az = 0.0;
-#pragma unroll
-    for (int i = 0; i < S; i++) {
-        if (i < cnt) {
-            double x, y, z;
-            vx_point(s, key[i], base, slot_frame, pix_list, depth, intr, pose, H, W, x, y, z);
-            ax = ax + x;
-            ay = ay + y;
-            az = az + z;
-        }
-    }
-    acc[0] = ax;
-    acc[1] = ay;
-    acc[2] = az;
-}
-
-__device__ __forceinline__ void vx_reset(int e, unsigned long long *__restrict__ hkey, int *__restrict__ hfirst,
-                                         int *__restrict__ ecnt, int *__restrict__ efill)
-{
-    hkey[e] = kEmptyKey;
-    hfirst[e] = INT_MAX;
-    ecnt[e] = 0;
-    efill[e] = 0;
-}
-
-// lane per voxel of up to small_max (<= kVxSmall) pixels (sorting network sized by the wave's largest
-// voxel); larger voxels -> big list
-__global__ __launch_bounds__(kVxChunk) void k_vx_fold(const int *__restrict__ dNCH, const int *__restrict__ chslot,
-                                                      const int *__restrict__ choff, const int *__restrict__ slot_frame,
-                                                      const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
-                                                      const int *__restrict__ slot_nv, const unsigned *__restrict__ pix_list,
-                                                      const float *__restrict__ depth, const double *__restrict__ intr,
-                                                      const double *__restrict__ pose, BpDev pr,
-                                                      const int *__restrict__ vox_entry, const int *__restrict__ estart,
-                                                      const int *__restrict__ vlist, unsigned long long *__restrict__ hkey,
-                                                      int *__restrict__ hfirst, int *__restrict__ ecnt,
-                                                      int *__restrict__ efill, double *__restrict__ vpts,
-                                                      int2 *__restrict__ big, int *__restrict__ nbig, int small_max)
-{
-    const int NCH = *dNCH;
-    for (int c = blockIdx.x; c < NCH; c += gridDim.x) {
-        const VxPix q = vx_pix(c, chslot, choff, slot_np, slot_pix);
-        const int v = q.k;  // voxel index in the slot (voxels <= pixels)
-        const bool live = v < slot_nv[q.s];
-        int e = -1, cnt = 0;
-        if (live) {
-            e = vox_entry[q.base + v];
-            cnt = ecnt[e];
-            if (cnt > small_max) {
-                big[atomicAdd(nbig, 1)] = make_int2(q.s, v);
-                cnt = 0;
+            for (; j < b1; j++) {
+                double x, y, z;
+                vx_point(pl, dep, K, T, W, vl[j], x, y, z);
+                ax = ax + x;
+                ay = ay + y;
+                az = az + z;
             }
-        }
-        const int cmax = wave_max_i(cnt);
-        if (cmax == 0) continue;
-        double acc[3];
-        const int *vl = vlist + (cnt ? estart[e] : 0);
-        if (cmax <= 4) vx_fold_lane<4>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
-        else if (cmax <= 8) vx_fold_lane<8>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
-        else if (cmax <= 16) vx_fold_lane<16>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
-        else vx_fold_lane<32>(vl, cnt, q.s, q.base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, acc);
-        if (cnt) {
-            const double dn = static_cast<double>(cnt);
-            double *o = vpts + 3 * (static_cast<size_t>(q.base) + v);
-            o[0] = acc[0] / dn;
-            o[1] = acc[1] / dn;
-            o[2] = acc[2] / dn;
-            vx_reset(e, hkey, hfirst, ecnt, efill);
-        }
-    }
-}
-
-// workgroup per voxel of more than kVxSmall pixels: windows of kVxWin list positions, the
-// window's entries ordered through a bitmap, their points staged in LDS and added by one lane
-__global__ __launch_bounds__(kVxChunk) void k_vx_big(const int *__restrict__ nbig, const int2 *__restrict__ big,
-                                                     const int *__restrict__ slot_frame,
-                                                     const int *__restrict__ slot_pix, const unsigned *__restrict__ pix_list,
-                                                     const float *__restrict__ depth, const double *__restrict__ intr,
-                                                     const double *__restrict__ pose, BpDev pr,
-                                                     const int *__restrict__ vox_entry, const int *__restrict__ estart,
-                                                     const int *__restrict__ vlist, unsigned long long *__restrict__ hkey,
-                                                     int *__restrict__ hfirst, int *__restrict__ ecnt,
-                                                     int *__restrict__ efill, double *__restrict__ vpts)
-{
-    __shared__ unsigned bm[kVxWin / 32];
-    __shared__ int sk[kVxWin];
-    __shared__ double sp[3 * kVxWin];
-    __shared__ int ws[kVxChunk / 64];
-    __shared__ int s_next;
-    const int NB = *nbig;
-    const int t = threadIdx.x;
-    for (int b = blockIdx.x; b < NB; b += gridDim.x) {
-        const int s = big[b].x, v = big[b].y;
-        const int base = slot_pix[s];
-        const int e = vox_entry[base + v];
-        const int cnt = ecnt[e];
-        const int *vl = vlist + estart[e];
-        double ax = 0.0, ay = 0.0, az = 0.0;  // thread 0's running sums
-        int w0 = -1;                          // entries < w0 are done
-        while (true) {
-            // next window: from the smallest entry >= w0
-            int mn = INT_MAX;
-            for (int i = t; i < cnt; i += kVxChunk) {
-                const int k = vl[i];
-                if (k >= w0) mn = min(mn, k);
-            }
-            mn = wave_min_i(mn);
-            if ((t & 63) == 0) ws[t >> 6] = mn;
-            if (t < kVxWin / 32) bm[t] = 0u;
-            __syncthreads();
-            if (t == 0) s_next = min(min(ws[0], ws[1]), min(ws[2], ws[3]));
-            __syncthreads();
-            const int lo = s_next;
-            if (lo == INT_MAX) break;
-            for (int i = t; i < cnt; i += kVxChunk) {
-                const int k = vl[i];
-                if (k >= lo && k - lo < kVxWin) atomicOr(&bm[(k - lo) >> 5], 1u << ((k - lo) & 31));
-            }
-            __syncthreads();
-            // ordered extraction: word popcounts scanned by wave 0 (kVxWin / 32 <= 64 words)
-            if (t < 64) {
-                const unsigned w = t < kVxWin / 32 ? bm[t] : 0u;
-                int x = __popc(w);
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int y = __shfl_up(x, d, 64);
-                    if (t >= d) x += y;
-                }
-                int pos = x - __popc(w);
-                unsigned ww = w;
-                while (ww) {
-                    const int bit = __ffs(ww) - 1;
-                    ww &= ww - 1;
-                    sk[pos++] = lo + 32 * t + bit;
-                }
-                if (t == 63) s_next = x;  // entries in the window
-            }
-            __syncthreads();
-            const int nw = s_next;
-            for (int i = t; i < nw; i += kVxChunk)
-                vx_point(s, sk[i], base, slot_frame, pix_list, depth, intr, pose, pr.H, pr.W, sp[3 * i], sp[3 * i + 1],
-                         sp[3 * i + 2]);
-            __syncthreads();
-            if (t == 0)
-                for (int i = 0; i < nw; i++) {
-                    ax = ax + sp[3 * i];
-                    ay = ay + sp[3 * i + 1];
-                    az = az + sp[3 * i + 2];
-                }
-            w0 = lo + kVxWin;
-            __syncthreads();
-        }
-        if (t == 0) {
-            const double dn = static_cast<double>(cnt);
+            const double dn = static_cast<double>(b1 - b0);
             double *o = vpts + 3 * (static_cast<size_t>(base) + v);
             o[0] = ax / dn;
             o[1] = ay / dn;
             o[2] = az / dn;
-            vx_reset(e, hkey, hfirst, ecnt, efill);
         }
+        if (t == 0) slot_nv[s] = nv;
         __syncthreads();
     }
 }
+
+// k_bp_voxel: the global-hash form for the slots k_bp_voxel_lds lists (voxel coordinates spanning
+// >= 1024 voxels, or more than kVxV voxels).  Chunks of 256 pixels in list order: voxel keys go into
+// the slot's hash (2 entries per pixel, empty at rest); new voxels get ids in order of their first
+// pixel (atomicMin of the pixel rank, then an ordered scan); the sums are added wave by wave, lane
+// by lane, i.e. in pixel order.
+__global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, const int *__restrict__ order,
+                                                  const int *__restrict__ slot_frame,
+                                                  const int *__restrict__ slot_np, const int *__restrict__ slot_pix,
+                                                  const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
+                                                  const double *__restrict__ intr, const double *__restrict__ pose, BpDev pr,
+                                                  unsigned long long *__restrict__ hkey, int *__restrict__ hvid,
+                                                  int *__restrict__ hfirst, int *__restrict__ vox_entry,
+                                                  double *__restrict__ acc, double *__restrict__ vpts,
+                                                  int *__restrict__ slot_nv, int *__restrict__ errflag)
+{
+    __shared__ double sp[256 * 3];
+    __shared__ double red[24];
+    __shared__ int ws[4];
+    const int NS = *dNS;
+    const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+    const int W = pr.W;
+    for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
+        const int s = order[idx];
+        const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
+        const double *K = intr + 4 * static_cast<size_t>(f);
+        const double *T = pose + 16 * static_cast<size_t>(f);
+        const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
+        const unsigned *pl = pix_list + base;
+        // min bound (order-free)
+        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (int k = t; k < n; k += 256) {
+            const unsigned i = pl[k];
+            double p[3];
+            bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+#pragma unroll
+            for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
+        }
+        block_minmax3(mn, mx, red);
+        double vmin[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
+        const unsigned C = 2u * static_cast<unsigned>(n);
+        unsigned long long *hk = hkey + 2 * static_cast<size_t>(base);
+        int *hv = hvid + 2 * static_cast<size_t>(base);
+        int *hf = hfirst + 2 * static_cast<size_t>(base);
+        double *ac = acc + 4 * static_cast<size_t>(base);
+        int nv = 0;
+        for (int c0 = 0; c0 < n; c0 += 256) {
+            const int k = c0 + t;
+            const bool valid = k < n;
+            double p[3] = {0.0, 0.0, 0.0};
+            unsigned e = 0;
+            if (valid) {
+                const unsigned i = pl[k];
+                bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+                long long ix[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    ix[c] = static_cast<long long>(floor((p[c] - vmin[c]) / pr.vs));
+                    if (ix[c] < 0 || ix[c] >= (1ll << 21)) {
+                        atomicOr(errflag, 1);
+                        ix[c] = ix[c] < 0 ? 0 : (1ll << 21) - 1;
+                    }
+                }
+                const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
+                e = mod_mul(bp_hash64(key), C);
+                while (true) {
+                    unsigned long long cur = hk[e];
+                    if (cur == kEmptyKey) {
+                        cur = atomicCAS(&hk[e], kEmptyKey, key);
+                        if (cur == kEmptyKey) cur = key;
+                    }
+                    if (cur == key) break;
+                    e = e + 1 == C ? 0 : e + 1;
+                }
+                if (ld_agent(&hv[e]) < 0) atomicMin(&hf[e], k);
+            }
+            __syncthreads();
+            const bool first = valid && ld_agent(&hv[e]) < 0 && ld_agent(&hf[e]) == k;
+            int tot;
+            const int pos = block_excl_scan<256>(first ? 1 : 0, ws, tot);
+            if (first) {
+                const int v = nv + pos;
+                st_agent(&hv[e], v);
+                vox_entry[base + v] = static_cast<int>(e);
+                ac[4 * v] = 0.0;
+                ac[4 * v + 1] = 0.0;
+                ac[4 * v + 2] = 0.0;
+                ac[4 * v + 3] = 0.0;
+            }
+            __syncthreads();
+            const int vid = valid ? ld_agent(&hv[e]) : -1;
+            sp[3 * t] = p[0];
+            sp[3 * t + 1] = p[1];
+            sp[3 * t + 2] = p[2];
+            __syncthreads();
+            // group lanes by voxel (ballots only), then every group leader of the wave adds its
+            // group's points in lane order to the running sum at once (one round trip per wave)
+            unsigned long long gm = 0;
+            {
+                unsigned long long act = __ballot(vid >= 0);
+                while (act) {
+                    const int L = __ffsll(static_cast<long long>(act)) - 1;
+                    const int kk = __shfl(vid, L, 64);
+                    const unsigned long long m = __ballot(vid == kk);
+                    if (lane == L) gm = m;
+                    act &= ~m;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                if (wv == w && gm) {  // AccumulatedPoint::AddPoint, lane (= pixel) order
+                    double ax = ac[4 * vid], ay = ac[4 * vid + 1], az = ac[4 * vid + 2], an = ac[4 * vid + 3];
+                    unsigned long long mm = gm;
+                    while (mm) {
+                        const int l = __ffsll(static_cast<long long>(mm)) - 1;
+                        mm &= mm - 1;
+                        const double *q = sp + 3 * (w * 64 + l);
+                        ax = ax + q[0];
+                        ay = ay + q[1];
+                        az = az + q[2];
+                        an = an + 1.0;
+                    }
+                    ac[4 * vid] = ax;
+                    ac[4 * vid + 1] = ay;
+                    ac[4 * vid + 2] = az;
+                    ac[4 * vid + 3] = an;
+                }
+                __syncthreads();
+            }
+            nv += tot;
+        }
+        // means; the hash entries of this slot return to empty
+        for (int v = t; v < nv; v += 256) {
+            const double cnt = ac[4 * v + 3];
+            vpts[3 * (static_cast<size_t>(base) + v)] = ac[4 * v] / cnt;
+            vpts[3 * (static_cast<size_t>(base) + v) + 1] = ac[4 * v + 1] / cnt;
+            vpts[3 * (static_cast<size_t>(base) + v) + 2] = ac[4 * v + 2] / cnt;
+            const int e = vox_entry[base + v];
+            hk[e] = kEmptyKey;
+            st_agent(&hv[e], -1);
+            st_agent(&hf[e], INT_MAX);
+        }
+        if (t == 0) slot_nv[s] = nv;
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // (a4) denoise (geometry.py:9-24), workgroup per slot
 // ---------------------------------------------------------------------------------------------
@@ -1026,32 +981,6 @@ constexpr bool kBpLean = N > 2048;
 template <int N>
 constexpr size_t kBpLeanInts = kBpLean<N> ? 6 * static_cast<size_t>(N) + 2 : 0;
 
-template <int NW>
-__device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], double *red)
-{
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        const double a = wave_min_d(mn[c]), b = wave_max_d(mx[c]);
-        if (lane == 0) {
-            red[c * NW + wv] = a;
-            red[3 * NW + c * NW + wv] = b;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        double a = red[c * NW], b = red[3 * NW + c * NW];
-        for (int w = 1; w < NW; w++) {
-            a = fmin(a, red[c * NW + w]);
-            b = fmax(b, red[3 * NW + c * NW + w]);
-        }
-        mn[c] = a;
-        mx[c] = b;
-    }
-    __syncthreads();
-}
-
 struct BpLdsGrid {
     const double4 *pt;  // x, y, z, cell key bits (bit 63: kept by the class filter) per sorted position
     const int *bs;      // bucket starts (2n + 1)
@@ -1137,6 +1066,35 @@ __device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nbw, 
     // k is the same in every active lane (lanes only leave), so w[k >> 1] is a uniform index
 #pragma unroll 1
     for (int k = 0; k < cnt; k++) fn(static_cast<int>((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu));
+}
+
+// nb_list over the entries' records: the record of entry k + 1 is loaded from LDS before fn runs
+// on entry k's, so the load latency hides behind fn (the k-NN's sorted insert) without a second
+// copy of fn's code
+template <int N, typename Fn>
+__device__ __forceinline__ void nb_list_pts(const unsigned short *__restrict__ nbw, const double4 *spt, int q, int cnt,
+                                            Fn &&fn)
+{
+    static_assert(kBpNbCap == 64, "eight uint4 per point");
+    const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
+    unsigned w[32];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
+        w[4 * u] = v.x;
+        w[4 * u + 1] = v.y;
+        w[4 * u + 2] = v.z;
+        w[4 * u + 3] = v.w;
+    }
+    double4 nxt = cnt > 0 ? spt[w[0] & 0xFFFFu] : make_double4(0.0, 0.0, 0.0, 0.0);
+#pragma unroll 1
+    for (int k = 0; k < cnt; k++) {
+        const double4 cur = nxt;
+        const int k1 = k + 1;
+        if (k1 < cnt) nxt = spt[(w[k1 >> 1] >> (16 * (k1 & 1))) & 0xFFFFu];
+        fn(cur);
+    }
 }
 
 __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, int &z)
@@ -1492,8 +1450,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
             int found = 0;
-            nb_list<N>(nbw, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](int q2) {
-                const double4 p = spt[q2];
+            nb_list_pts<N>(nbw, spt, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](const double4 &p) {
                 if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
                 const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
                 if (MC_ABLATE_BP == 3) best[0] += ((ex * ex) + (ey * ey)) + (ez * ez);

@@ -146,16 +146,14 @@ def test_denoise_size_classes_agree(ctx, monkeypatch, min_cls):
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("small", [0, 3])
-def test_voxel_fold_paths_agree(ctx, monkeypatch, small):
-    """voxel_down_sample's two fold paths (a lane per voxel with a sorting network; a workgroup per
-    large voxel ordering its pixels through window bitmaps) give the same voxels: every voxel of more
-    than `small` pixels forced onto the workgroup path."""
+def test_voxel_kernels_agree(ctx, monkeypatch):
+    """voxel_down_sample's two kernels (the LDS-resident one every slot starts in; the global-hash one
+    it hands overflowing slots to) give the same voxels: every slot forced onto the global kernel."""
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
     a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
     sa = ctx.bp_candidates()
-    monkeypatch.setenv("MC_VX_SMALL", str(small))
+    monkeypatch.setenv("MC_VX_GLOBAL", "1")
     b = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
     np.testing.assert_array_equal(sa, ctx.bp_candidates())
     for x, y in zip(a, b):
@@ -163,8 +161,8 @@ def test_voxel_fold_paths_agree(ctx, monkeypatch, small):
 
 
 def test_high_resolution_frame_matches_oracle(ctx):
-    """A ScanNet++-resolution frame (1920x1440): voxels of hundreds of pixels (the workgroup fold
-    path without any knob) against the CPU restatement."""
+    """A ScanNet++-resolution frame (1920x1440): slots of tens of thousands of pixels and voxels of
+    hundreds, against the CPU restatement."""
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=7, H=1440, W=1920, num_frames=1)
     _check_against_oracle(ctx, fr)
