@@ -51,8 +51,8 @@ struct mc_ctx {
     bool own_stream = false;
     hipStream_t side = nullptr;                 // S3: workgroup-per-mask kernel beside the wave kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipStream_t cls_stream[4] = {};             // S1 denoise: the LDS size classes run side by side
-    hipEvent_t ev_cls[4] = {};
+    hipStream_t cls_stream[mc::kBpClasses] = {};  // S1 denoise: the LDS size classes run side by side
+    hipEvent_t ev_cls[mc::kBpClasses] = {};
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
@@ -282,7 +282,7 @@ int mc_ctx_create(int device, mc_ctx **out)
         MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-        for (int c = 0; c < 4; c++) {
+        for (int c = 0; c < mc::kBpClasses; c++) {
             MC_HIP(hipStreamCreateWithFlags(&ctx->cls_stream[c], hipStreamNonBlocking));
             MC_HIP(hipEventCreateWithFlags(&ctx->ev_cls[c], hipEventDisableTiming));
         }
@@ -344,7 +344,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     if (ctx->side) (void)hipStreamSynchronize(ctx->side), (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    for (int c = 0; c < 4; c++) {
+    for (int c = 0; c < mc::kBpClasses; c++) {
         if (ctx->cls_stream[c]) (void)hipStreamSynchronize(ctx->cls_stream[c]), (void)hipStreamDestroy(ctx->cls_stream[c]);
         if (ctx->ev_cls[c]) (void)hipEventDestroy(ctx->ev_cls[c]);
     }
@@ -1498,9 +1498,9 @@ void grow_keep(DevBuf &b, size_t bytes, size_t used, hipStream_t s)
 
 enum BpStat : int {
     BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
-    BS_CLS,             // 5 denoise size-class counts (4 LDS classes + the global-memory kernel)
-    BS_TK = BS_CLS + 5,  // ticket counters of the LDS classes
-    BS_VXFB = BS_TK + 4,  // slots k_bp_voxel_lds hands to k_bp_voxel
+    BS_CLS,             // denoise size-class counts (kBpClasses LDS classes + the global-memory kernel)
+    BS_TK = BS_CLS + mc::kBpClasses + 1,  // ticket counters of the LDS classes
+    BS_VXFB = BS_TK + mc::kBpClasses,     // slots k_bp_voxel_lds hands to k_bp_voxel
     BS_COUNT
 };
 
@@ -1510,13 +1510,23 @@ size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (fram
 // u16 entries of per-workgroup eps-neighbour lists before class cls's region
 inline size_t nbl_offset(const mc_ctx *ctx, int cls)
 {
-    const size_t per_cls[4] = {static_cast<size_t>(mc::BpLdsClass<512>::kWgPerCu) * 512,
-                               static_cast<size_t>(mc::BpLdsClass<1024>::kWgPerCu) * 1024,
-                               static_cast<size_t>(mc::BpLdsClass<2048>::kWgPerCu) * 2048,
-                               static_cast<size_t>(mc::BpLdsClass<3072>::kWgPerCu) * 3072};
+    const size_t per_cls[mc::kBpClasses] = {static_cast<size_t>(mc::BpLdsClass<512>::kWgPerCu) * 512,
+                                            static_cast<size_t>(mc::BpLdsClass<1024>::kWgPerCu) * 1024,
+                                            static_cast<size_t>(mc::BpLdsClass<2048>::kWgPerCu) * 2048,
+                                            static_cast<size_t>(mc::BpLdsClass<3072>::kWgPerCu) * 3072,
+                                            static_cast<size_t>(mc::BpLdsClass<4096>::kWgPerCu) * 4096};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
     return o * static_cast<size_t>(ctx->num_cu) * mc::kBpNbCap;
+}
+
+// ints of per-workgroup lean scratch before class cls's region
+inline size_t lean_offset(const mc_ctx *ctx, int cls)
+{
+    const size_t per_cls[mc::kBpClasses] = {0, 0, 0, mc::kBpLeanInts<3072>, mc::kBpLeanInts<4096>};
+    size_t o = 0;
+    for (int c = 0; c < cls; c++) o += per_cls[c];
+    return o * static_cast<size_t>(ctx->num_cu);
 }
 
 void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
@@ -1539,12 +1549,12 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_midx.reserve((slots + 1) * 4);
     ctx->d_moff.reserve((slots + 1) * 4);
     ctx->d_slot_box.reserve(slots * 6 * 4);
-    ctx->d_cls_list.reserve(5 * slots * 4);
+    ctx->d_cls_list.reserve((mc::kBpClasses + 1) * slots * 4);
     ctx->d_vox_order.reserve(slots * 4);
     ctx->d_vx_fb.reserve(slots * 4);
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
-    ctx->d_nbl.reserve(nbl_offset(ctx, 4) * 2);
-    ctx->d_lean.reserve(static_cast<size_t>(ctx->num_cu) * mc::kBpLeanInts<3072> * 4);
+    ctx->d_nbl.reserve(nbl_offset(ctx, mc::kBpClasses) * 2);
+    ctx->d_lean.reserve(lean_offset(ctx, mc::kBpClasses) * 4);
     if (ctx->bp_px_cap < px) {
         ctx->d_pix_list.reserve(px * 4);
         ctx->d_hkey.reserve(2 * px * 8);
@@ -1619,7 +1629,7 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
     hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
-                       ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>(),
+                       ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
                        ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
                        ctx->d_slot_box.as<float>());
 }
@@ -1815,7 +1825,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // test knob: smallest denoise size class (0 = by size; 3 = the lean LDS class, 4 = the
         // global-memory kernel for every slot)
         int min_cls = 0;
-        if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(4, std::max(0, atoi(e)));
+        if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(mc::kBpClasses, std::max(0, atoi(e)));
         // test knob: MC_VX_GLOBAL=1 hands every slot to the global-hash voxel kernel
         const bool vx_global = getenv("MC_VX_GLOBAL") && atoi(getenv("MC_VX_GLOBAL")) != 0;
         // frames per batch: bounded pixel capacity of the per-slot arrays
@@ -1906,8 +1916,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
                 MC_HIP(hipEventRecord(ctx->ev_fork, s));
                 MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + 4,
-                                   ctx->d_cls_list.as<int>() + 4 * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
+                hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + mc::kBpClasses,
+                                   ctx->d_cls_list.as<int>() + mc::kBpClasses * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                                    ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
                                    ctx->d_bstart.as<int>(), ctx->d_blist.as<int>(), ctx->d_ncnt.as<int>(),
                                    ctx->d_par.as<int>(), ctx->d_droot.as<int>(), ctx->d_rnk.as<int>(),
@@ -1917,12 +1927,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
                 // the LDS classes side by side, each on its own stream: a class with few slots
                 // (the large ones) leaves most CUs to the others instead of serialising the batch
-                for (int c = 0; c < 4; c++) MC_HIP(hipStreamWaitEvent(ctx->cls_stream[c], ctx->ev_fork, 0));
+                for (int c = 0; c < mc::kBpClasses; c++) MC_HIP(hipStreamWaitEvent(ctx->cls_stream[c], ctx->ev_fork, 0));
                 bp_denoise_class<3072>(ctx, ctx->cls_stream[3], 3, ncap, st, dv);
+                bp_denoise_class<4096>(ctx, ctx->cls_stream[4], 4, ncap, st, dv);
                 bp_denoise_class<2048>(ctx, ctx->cls_stream[2], 2, ncap, st, dv);
                 bp_denoise_class<1024>(ctx, ctx->cls_stream[1], 1, ncap, st, dv);
                 bp_denoise_class<512>(ctx, ctx->cls_stream[0], 0, ncap, st, dv);
-                for (int c = 0; c < 4; c++) {
+                for (int c = 0; c < mc::kBpClasses; c++) {
                     MC_HIP(hipEventRecord(ctx->ev_cls[c], ctx->cls_stream[c]));
                     MC_HIP(hipStreamWaitEvent(s, ctx->ev_cls[c], 0));
                 }

@@ -949,7 +949,8 @@ __device__ __forceinline__ double seq_add64_pos(double acc, double v)
 
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
-constexpr int kBpLdsN = 3072;  // largest LDS class
+constexpr int kBpLdsN = 4096;  // largest LDS class
+constexpr int kBpClasses = 5;  // LDS classes (512, 1024, 2048, 3072, 4096); class kBpClasses = k_bp_denoise
 constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
 template <int N>
 struct BpLdsClass;
@@ -975,11 +976,18 @@ template <>  // lean: one bucket per point; sort/rank/label/statistics arrays in
 struct BpLdsClass<3072> {
     static constexpr int T = 512, kWgPerCu = 1;
 };
+template <>  // leaner: also the neighbour counts and the union-find array in global scratch
+struct BpLdsClass<4096> {
+    static constexpr int T = 512, kWgPerCu = 1;
+};
 template <int N>
 constexpr bool kBpLean = N > 2048;
-// global scratch ints per workgroup of a lean class: savg (2N), sB (2N + 2), sX (N), sorig + spos (N)
 template <int N>
-constexpr size_t kBpLeanInts = kBpLean<N> ? 6 * static_cast<size_t>(N) + 2 : 0;
+constexpr bool kBpLean2 = N > 3072;
+// global scratch ints per workgroup of a lean class: savg (2N), sB (2N + 2), sX (N), sorig + spos (N)
+// [+ sflag (N), spar (N)]
+template <int N>
+constexpr size_t kBpLeanInts = kBpLean<N> ? (kBpLean2<N> ? 8 : 6) * static_cast<size_t>(N) + 2 : 0;
 
 struct BpLdsGrid {
     const double4 *pt;  // x, y, z, cell key bits (bit 63: kept by the class filter) per sorted position
@@ -1104,9 +1112,9 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
     z = static_cast<int>(k & 0x1FFFFF);
 }
 
-// Slots of each size class (unordered: every slot is processed independently); class 4 = more than
-// kBpLdsN voxels (the global-memory kernel).  min_cls > 0 sends small slots to a larger class (tests:
-// every class gives the same results).  cls_cnt[5] must be zero.
+// Slots of each size class (unordered: every slot is processed independently); class kBpClasses =
+// more than kBpLdsN voxels (the global-memory kernel).  min_cls > 0 sends small slots to a larger
+// class (tests: every class gives the same results).  cls_cnt[kBpClasses + 1] must be zero.
 __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
                                                      int cap, int min_cls, int *__restrict__ cls_cnt,
                                                      int *__restrict__ cls_list)
@@ -1115,9 +1123,9 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
     for (int s = blockIdx.x * 256 + threadIdx.x; s - static_cast<int>(threadIdx.x) < NS; s += gridDim.x * 256) {
         const bool live = s < NS;
         const int n = live ? slot_nv[s] : 0;
-        const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= kBpLdsN ? 3 : 4);
+        const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 3072 ? 3 : n <= kBpLdsN ? 4 : 5);
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k <= kBpClasses; k++) {
             const unsigned long long b = __ballot(live && c == k);
             if (!b) continue;
             const int leader = __ffsll(static_cast<long long>(b)) - 1;
@@ -1165,8 +1173,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     __shared__ int sB_l[2 * NL + 2];     // bucket counts; then min original index per root [0, n) +
                                          // class counts [N, ..); then the k-NN fallback list
     __shared__ short sorig_l[NL], spos_l[NL];  // sorted position <-> original index
-    __shared__ int sflag[N];             // eps-neighbour count | kept bit 30
-    __shared__ int spar[N];              // union-find over positions, then roots, then kept ranks
+    constexpr int NL2 = kBpLean2<N> ? 1 : N;
+    __shared__ int sflag_l[NL2];         // eps-neighbour count | kept bit 30
+    __shared__ int spar_l[NL2];          // union-find over positions, then roots, then kept ranks
     __shared__ int sX_l[NL];             // bucket per point; rank per root; S list
     __shared__ double savg_l[NL];        // labels (int view); then mean distances
     int *const gs = lean_scr + static_cast<size_t>(blockIdx.x) * kBpLeanInts<N>;
@@ -1175,6 +1184,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     int *const sX = kLean ? gs + 4 * N + 2 : sX_l;
     short *const sorig = kLean ? reinterpret_cast<short *>(gs + 5 * N + 2) : sorig_l;
     short *const spos = kLean ? sorig + N : spos_l;
+    int *const sflag = kBpLean2<N> ? gs + 6 * N + 2 : sflag_l;
+    int *const spar = kBpLean2<N> ? gs + 7 * N + 2 : spar_l;
     __shared__ double red[6 * NW];
     __shared__ float fred[6 * NW];
     __shared__ int ws[NW];

@@ -6,6 +6,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+import maskclustering_amd  # noqa: E402,F401  (HIP queue setting before the first HIP call)
 
 
 def pytest_configure(config):
