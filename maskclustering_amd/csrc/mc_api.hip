@@ -1507,6 +1507,9 @@ enum BpStat : int {
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
+// Workgroups per resident slot of a denoise class (the classes take slots from tickets): the extra
+// ones start on CUs that other classes free, so no class keeps only its initial share of the chip.
+constexpr int kBpOversub = 2;
 // u16 entries of per-workgroup eps-neighbour lists before class cls's region
 inline size_t nbl_offset(const mc_ctx *ctx, int cls)
 {
@@ -1517,7 +1520,7 @@ inline size_t nbl_offset(const mc_ctx *ctx, int cls)
                                             static_cast<size_t>(mc::BpLdsClass<4096>::kWgPerCu) * 4096};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
-    return o * static_cast<size_t>(ctx->num_cu) * mc::kBpNbCap;
+    return o * static_cast<size_t>(ctx->num_cu) * kBpOversub * mc::kBpNbCap;
 }
 
 // ints of per-workgroup lean scratch before class cls's region
@@ -1526,7 +1529,7 @@ inline size_t lean_offset(const mc_ctx *ctx, int cls)
     const size_t per_cls[mc::kBpClasses] = {0, 0, 0, mc::kBpLeanInts<3072>, mc::kBpLeanInts<4096>};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
-    return o * static_cast<size_t>(ctx->num_cu);
+    return o * static_cast<size_t>(ctx->num_cu) * kBpOversub;
 }
 
 void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
@@ -1626,7 +1629,7 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
 {
     using C = mc::BpLdsClass<N>;
     // the classes run concurrently: each has its own region of per-workgroup neighbour lists
-    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu), dim3(C::T), 0, s, st + BS_CLS + cls,
+    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * kBpOversub), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
