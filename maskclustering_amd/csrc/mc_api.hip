@@ -1526,7 +1526,10 @@ inline size_t nbl_offset(const mc_ctx *ctx, int cls)
 // ints of per-workgroup lean scratch before class cls's region
 inline size_t lean_offset(const mc_ctx *ctx, int cls)
 {
-    const size_t per_cls[mc::kBpClasses] = {0, 0, 0, mc::kBpLeanInts<3072>, mc::kBpLeanInts<4096>};
+    const size_t per_cls[mc::kBpClasses] = {
+        mc::kBpLeanInts<512> * mc::BpLdsClass<512>::kWgPerCu, mc::kBpLeanInts<1024> * mc::BpLdsClass<1024>::kWgPerCu,
+        mc::kBpLeanInts<2048> * mc::BpLdsClass<2048>::kWgPerCu, mc::kBpLeanInts<3072> * mc::BpLdsClass<3072>::kWgPerCu,
+        mc::kBpLeanInts<4096> * mc::BpLdsClass<4096>::kWgPerCu};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
     return o * static_cast<size_t>(ctx->num_cu) * kBpOversub;
@@ -1536,7 +1539,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
 {
     const size_t px = static_cast<size_t>(fb) * H * W + 1;
     const size_t slots = slots_cap(fb);
-    ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * 256 * 4);
+    ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * mc::kBpWaves * 256 * 4);
     ctx->d_present.reserve(static_cast<size_t>(fb) * 8 * 4);
     ctx->d_fflags.reserve(static_cast<size_t>(fb) * 4);
     ctx->d_cand.reserve(slots * 4);

@@ -187,20 +187,24 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const float *__restrict__ 
 // ---------------------------------------------------------------------------------------------
 // (a2) pixels -> masks
 // ---------------------------------------------------------------------------------------------
-// One block per (band of kBpBand rows, frame).  band_cnt[f][band][id]: valid-depth pixels of id in
-// the band (0 < d < trunc: Open3D keeps d < trunc, :22; ids != 0, :94); present[f]: ids in the
-// image (torch.unique, :77); fflags[f]: 1 = a pixel with d == trunc (the reference's IndexError
-// at :100), 2 = inf in the pose (:73-74, frame skipped).
+// One block per (band of kBpBand rows, frame); wave w of the block owns sub-band w (kBpSub rows).
+// band_cnt[f][sub-band][id]: valid-depth pixels of id in the sub-band (0 < d < trunc: Open3D keeps
+// d < trunc, :22; ids != 0, :94); present[f]: ids in the image (torch.unique, :77); fflags[f]: 1 =
+// a pixel with d == trunc (the reference's IndexError at :100), 2 = inf in the pose (:73-74, frame
+// skipped).
+constexpr int kBpWaves = 4;                   // waves (= sub-bands) per band block
+constexpr int kBpSub = kBpBand / kBpWaves;    // rows per sub-band
 __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
                                                   const double *__restrict__ pose, BpDev pr, int *__restrict__ band_cnt,
                                                   unsigned *__restrict__ present, int *__restrict__ fflags)
 {
-    __shared__ int cnt[256];
+    __shared__ int cnt[kBpWaves][256];
     __shared__ unsigned pres[8];
     __shared__ int sflag;
-    const int f = blockIdx.y, band = blockIdx.x, t = threadIdx.x, lane = lane_id();
+    const int f = blockIdx.y, band = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
-    cnt[t] = 0;
+#pragma unroll
+    for (int w = 0; w < kBpWaves; w++) cnt[w][t] = 0;
     if (t < 8) pres[t] = 0u;
     if (t == 0) sflag = 0;
     __syncthreads();
@@ -208,10 +212,11 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
     __syncthreads();
     const bool skip = (sflag & 2) != 0;
     const size_t fb = static_cast<size_t>(f) * pr.H * W;
-    const int i0 = band * kBpBand * W, i1 = min(pr.H, (band + 1) * kBpBand) * W;
+    const int sb = band * kBpWaves + wv;  // this wave's sub-band
+    const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int trunc = 0, lastp = -1;
-    for (int ib = i0; ib < i1; ib += 256) {
-        const int i = ib + t;
+    for (int ib = i0; ib < i1; ib += 64) {
+        const int i = ib + lane;
         int id = -1;
         if (i < i1) {
             const int sid = seg[fb + i];
@@ -228,19 +233,21 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
             const int leader = __ffsll(static_cast<long long>(act)) - 1;
             const int k = __shfl(id, leader, 64);
             const unsigned long long m = __ballot(id == k);
-            if (lane == leader) atomicAdd(&cnt[k], __popcll(m));
+            if (lane == leader) cnt[wv][k] += __popcll(m);  // the wave's own row
             act &= ~m;
         }
     }
     if (trunc) atomicOr(&sflag, 1);
     __syncthreads();
-    band_cnt[(static_cast<size_t>(f) * pr.nbands + band) * 256 + t] = cnt[t];
+    const size_t nsb = static_cast<size_t>(pr.nbands) * kBpWaves;
+#pragma unroll
+    for (int w = 0; w < kBpWaves; w++) band_cnt[(static_cast<size_t>(f) * nsb + band * kBpWaves + w) * 256 + t] = cnt[w][t];
     if (t < 8 && pres[t]) atomicOr(&present[f * 8 + t], pres[t]);
     if (t == 0 && sflag) atomicOr(&fflags[f], sflag);
 }
 
-// One block per frame, thread = id: band counts -> band offsets within the id's pixel list;
-// candidate = id != 0 with >= few_points valid pixels (:101) in a frame that neither returns
+// One block per frame, thread = id: sub-band counts -> sub-band offsets within the id's pixel
+// list; candidate = id != 0 with >= few_points valid pixels (:101) in a frame that neither returns
 // early (inf pose) nor raises (d == trunc with ids present; *err_frame = first such frame).
 __global__ __launch_bounds__(256) void k_bp_frames(int *__restrict__ band_cnt, const unsigned *__restrict__ present,
                                                    const int *__restrict__ fflags, BpDev pr, int *__restrict__ cand,
@@ -254,8 +261,9 @@ __global__ __launch_bounds__(256) void k_bp_frames(int *__restrict__ band_cnt, c
     const bool err = !inf_pose && any_id && (fl & 1);
     if (err && id == 0) atomicMin(err_frame, f);
     int tot = 0;
-    int *bc = band_cnt + static_cast<size_t>(f) * pr.nbands * 256 + id;
-    for (int b = 0; b < pr.nbands; b++) {
+    const int nsb = pr.nbands * kBpWaves;
+    int *bc = band_cnt + static_cast<size_t>(f) * nsb * 256 + id;
+    for (int b = 0; b < nsb; b++) {
         const int c = bc[static_cast<size_t>(b) * 256];
         bc[static_cast<size_t>(b) * 256] = tot;
         tot += c;
@@ -286,54 +294,53 @@ __global__ __launch_bounds__(256) void k_bp_slots(const int *__restrict__ cand, 
 }
 
 // Stable compaction: every slot's pixels in row-major order (the order of view_points[valid_mask],
-// :96-100).  Per 256-pixel chunk, ranks within a wave by ballot groups; the four waves take their
-// positions in wave order (one barrier per wave), so the list order is the pixel order.
+// :96-100).  Each wave walks its own sub-band with its own per-id cursors (the sub-band offsets of
+// k_bp_frames), ranks within a 64-pixel step by ballot groups: no barrier after the set-up.
 __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
                                                     const int *__restrict__ band_off, const int *__restrict__ slot_of,
                                                     const int *__restrict__ slot_pix, BpDev pr,
                                                     unsigned *__restrict__ pix_list)
 {
-    __shared__ int cur[256];
-    __shared__ int gb[4][64];
+    __shared__ int cur[kBpWaves][256];
     const int f = blockIdx.y, band = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
+    const size_t nsb = static_cast<size_t>(pr.nbands) * kBpWaves;
     {
         const int s = slot_of[f * 256 + t];
-        cur[t] = s >= 0 ? slot_pix[s] + band_off[(static_cast<size_t>(f) * pr.nbands + band) * 256 + t] : -1;
+        const int sp = s >= 0 ? slot_pix[s] : -1;
+#pragma unroll
+        for (int w = 0; w < kBpWaves; w++)
+            cur[w][t] = s >= 0 ? sp + band_off[(static_cast<size_t>(f) * nsb + band * kBpWaves + w) * 256 + t] : -1;
     }
     __syncthreads();
     const size_t fb = static_cast<size_t>(f) * pr.H * W;
-    const int i0 = band * kBpBand * W, i1 = min(pr.H, (band + 1) * kBpBand) * W;
-    for (int ib = i0; ib < i1; ib += 256) {
-        const int i = ib + t;
+    const int sb = band * kBpWaves + wv;
+    const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
+    int *mycur = cur[wv];
+    for (int ib = i0; ib < i1; ib += 64) {
+        const int i = ib + lane;
         int id = -1;
         if (i < i1) {
             const int sid = seg[fb + i];
             const float d = depth[fb + i];
-            if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && cur[sid] >= 0) id = sid;
+            if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && mycur[sid] >= 0) id = sid;
         }
-        int rank = 0, leader = 0, n = 0;
         unsigned long long act = __ballot(id >= 0);
+        int pos = 0;
         while (act) {
             const int L = __ffsll(static_cast<long long>(act)) - 1;
             const int k = __shfl(id, L, 64);
             const unsigned long long m = __ballot(id == k);
-            if (id == k) {
-                rank = __popcll(m & ((1ull << lane) - 1ull));
-                leader = L;
-                n = __popcll(m);
+            int b = 0;
+            if (lane == L) {
+                b = mycur[k];
+                mycur[k] = b + __popcll(m);
             }
+            b = __shfl(b, L, 64);
+            if (id == k) pos = b + __popcll(m & ((1ull << lane) - 1ull));
             act &= ~m;
         }
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            if (wv == w && id >= 0 && lane == leader) {
-                gb[w][lane] = cur[id];
-                cur[id] += n;
-            }
-            __syncthreads();
-        }
-        if (id >= 0) pix_list[gb[wv][leader] + rank] = static_cast<unsigned>(i);
+        if (id >= 0) pix_list[pos] = static_cast<unsigned>(i);
     }
 }
 
@@ -960,30 +967,35 @@ struct BpLdsClass;
 #ifndef MC_BP_WG1024
 #define MC_BP_WG1024 2
 #endif
+// kLean: 0 = everything in LDS; 1 = one bucket per point, sort/rank/label/statistics arrays in global
+// scratch; 2 = also the neighbour counts and the union-find array in global scratch
+#ifndef MC_BP_LEAN2048
+#define MC_BP_LEAN2048 0
+#endif
 template <>
 struct BpLdsClass<512> {
-    static constexpr int T = 256, kWgPerCu = MC_BP_WG512;
+    static constexpr int T = 256, kWgPerCu = MC_BP_WG512, kLean = 0;
 };
 template <>
 struct BpLdsClass<1024> {
-    static constexpr int T = 512, kWgPerCu = MC_BP_WG1024;
+    static constexpr int T = 512, kWgPerCu = MC_BP_WG1024, kLean = 0;
 };
 template <>
 struct BpLdsClass<2048> {
-    static constexpr int T = 512, kWgPerCu = 1;
+    static constexpr int T = 512, kWgPerCu = MC_BP_LEAN2048 ? 2 : 1, kLean = MC_BP_LEAN2048;
 };
-template <>  // lean: one bucket per point; sort/rank/label/statistics arrays in global scratch
+template <>
 struct BpLdsClass<3072> {
-    static constexpr int T = 512, kWgPerCu = 1;
+    static constexpr int T = 512, kWgPerCu = 1, kLean = 1;
 };
-template <>  // leaner: also the neighbour counts and the union-find array in global scratch
+template <>
 struct BpLdsClass<4096> {
-    static constexpr int T = 512, kWgPerCu = 1;
+    static constexpr int T = 512, kWgPerCu = 1, kLean = 2;
 };
 template <int N>
-constexpr bool kBpLean = N > 2048;
+constexpr bool kBpLean = BpLdsClass<N>::kLean >= 1;
 template <int N>
-constexpr bool kBpLean2 = N > 3072;
+constexpr bool kBpLean2 = BpLdsClass<N>::kLean >= 2;
 // global scratch ints per workgroup of a lean class: savg (2N), sB (2N + 2), sX (N), sorig + spos (N)
 // [+ sflag (N), spar (N)]
 template <int N>
@@ -1945,21 +1957,31 @@ __global__ __launch_bounds__(256) void k_bp_query(
             int best[kBpBallMax];
 #pragma unroll
             for (int x = 0; x < kBpBallMax; x++) best[x] = INT_MAX;
-            for (int dz = -1; dz <= 1; dz++)
-                for (int dy = -1; dy <= 1; dy++)
-                    for (int dx = -1; dx <= 1; dx++) {
-                        const unsigned long long key = pack3(cx + dx, cy + dy, cz + dz);
-                        const unsigned b = mod_mul(bp_hash3(cx + dx, cy + dy, cz + dz), gnb);
-                        for (int k = gstart[b]; k < gstart[b + 1]; k++) {
-                            if (gcell[k] != key) continue;
-                            const float4 p = gpts[k];
-                            if (!(p.x > lo[0] && p.x < hi[0] && p.y > lo[1] && p.y < hi[1] && p.z > lo[2] && p.z < hi[2]))
-                                continue;
-                            const float ex = qx - p.x, ey = qy - p.y, ez = qz - p.z;
-                            const float d2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, __fmul_rn(ex, ex)));
-                            if (d2 < pr.r2) sorted_insert(best, gidx[k]);
-                        }
-                    }
+            // the 27 cells; the next cell's bucket range is loaded while this cell's points are
+            // scanned (one dependent global round trip less per cell)
+            auto cell_range = [&](int d, unsigned long long &key) {
+                const int x = cx + d % 3 - 1, y = cy + (d / 3) % 3 - 1, z = cz + d / 9 - 1;
+                key = pack3(x, y, z);
+                const unsigned b = mod_mul(bp_hash3(x, y, z), gnb);
+                return make_int2(gstart[b], gstart[b + 1]);
+            };
+            unsigned long long nkey;
+            int2 nrng = cell_range(0, nkey);
+#pragma unroll 1
+            for (int d = 0; d < 27; d++) {
+                const unsigned long long key = nkey;
+                const int2 rng = nrng;
+                if (d + 1 < 27) nrng = cell_range(d + 1, nkey);
+                for (int k = rng.x; k < rng.y; k++) {
+                    if (gcell[k] != key) continue;
+                    const float4 p = gpts[k];
+                    if (!(p.x > lo[0] && p.x < hi[0] && p.y > lo[1] && p.y < hi[1] && p.z > lo[2] && p.z < hi[2]))
+                        continue;
+                    const float ex = qx - p.x, ey = qy - p.y, ez = qz - p.z;
+                    const float d2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, __fmul_rn(ex, ex)));
+                    if (d2 < pr.r2) sorted_insert(best, gidx[k]);
+                }
+            }
             int got = 0;
 #pragma unroll
             for (int x = 0; x < kBpBallMax; x++) {
