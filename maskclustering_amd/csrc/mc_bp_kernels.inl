@@ -194,6 +194,7 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const float *__restrict__ 
 // skipped).
 constexpr int kBpWaves = 4;                   // waves (= sub-bands) per band block
 constexpr int kBpSub = kBpBand / kBpWaves;    // rows per sub-band
+constexpr int kBpPix = 4;                     // 64-pixel steps whose loads a wave issues together
 __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
                                                   const double *__restrict__ pose, BpDev pr, int *__restrict__ band_cnt,
                                                   unsigned *__restrict__ present, int *__restrict__ fflags)
@@ -215,12 +216,23 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
     const int sb = band * kBpWaves + wv;  // this wave's sub-band
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int trunc = 0, lastp = -1;
-    for (int ib = i0; ib < i1; ib += 64) {
-        const int i = ib + lane;
+    for (int ib0 = i0; ib0 < i1; ib0 += 64 * kBpPix) {
+      // kBpPix steps' loads issued before the first is used
+      int sidv[kBpPix];
+      float dv[kBpPix];
+#pragma unroll
+      for (int u = 0; u < kBpPix; u++) {
+        const int i = ib0 + 64 * u + lane;
+        sidv[u] = i < i1 ? seg[fb + i] : 0;
+        dv[u] = i < i1 ? depth[fb + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kBpPix; u++) {
+        const int i = ib0 + 64 * u + lane;
         int id = -1;
         if (i < i1) {
-            const int sid = seg[fb + i];
-            const float d = depth[fb + i];
+            const int sid = sidv[u];
+            const float d = dv[u];
             if (sid != lastp) {
                 atomicOr(&pres[sid >> 5], 1u << (sid & 31));
                 lastp = sid;
@@ -236,6 +248,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
             if (lane == leader) cnt[wv][k] += __popcll(m);  // the wave's own row
             act &= ~m;
         }
+      }
     }
     if (trunc) atomicOr(&sflag, 1);
     __syncthreads();
@@ -317,12 +330,22 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
     const int sb = band * kBpWaves + wv;
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int *mycur = cur[wv];
-    for (int ib = i0; ib < i1; ib += 64) {
-        const int i = ib + lane;
+    for (int ib0 = i0; ib0 < i1; ib0 += 64 * kBpPix) {
+      int sidv[kBpPix];
+      float dv[kBpPix];
+#pragma unroll
+      for (int u = 0; u < kBpPix; u++) {
+        const int i = ib0 + 64 * u + lane;
+        sidv[u] = i < i1 ? seg[fb + i] : 0;
+        dv[u] = i < i1 ? depth[fb + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kBpPix; u++) {
+        const int i = ib0 + 64 * u + lane;
         int id = -1;
         if (i < i1) {
-            const int sid = seg[fb + i];
-            const float d = depth[fb + i];
+            const int sid = sidv[u];
+            const float d = dv[u];
             if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && mycur[sid] >= 0) id = sid;
         }
         unsigned long long act = __ballot(id >= 0);
@@ -341,6 +364,7 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
             act &= ~m;
         }
         if (id >= 0) pix_list[pos] = static_cast<unsigned>(i);
+      }
     }
 }
 
@@ -980,17 +1004,20 @@ template <>
 struct BpLdsClass<1024> {
     static constexpr int T = 512, kWgPerCu = MC_BP_WG1024, kLean = 0;
 };
+#ifndef MC_BP_TBIG
+#define MC_BP_TBIG 1024  // threads of the one-workgroup-per-CU classes (2048, 3072, 4096)
+#endif
 template <>
 struct BpLdsClass<2048> {
-    static constexpr int T = 512, kWgPerCu = MC_BP_LEAN2048 ? 2 : 1, kLean = MC_BP_LEAN2048;
+    static constexpr int T = MC_BP_TBIG, kWgPerCu = MC_BP_LEAN2048 ? 2 : 1, kLean = MC_BP_LEAN2048;
 };
 template <>
 struct BpLdsClass<3072> {
-    static constexpr int T = 512, kWgPerCu = 1, kLean = 1;
+    static constexpr int T = MC_BP_TBIG, kWgPerCu = 1, kLean = 1;
 };
 template <>
 struct BpLdsClass<4096> {
-    static constexpr int T = 512, kWgPerCu = 1, kLean = 2;
+    static constexpr int T = MC_BP_TBIG, kWgPerCu = 1, kLean = 2;
 };
 template <int N>
 constexpr bool kBpLean = BpLdsClass<N>::kLean >= 1;
