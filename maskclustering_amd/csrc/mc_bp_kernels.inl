@@ -1069,15 +1069,46 @@ __device__ __forceinline__ void lds_cell(const BpLdsGrid &g, int x, int y, int z
     }
 }
 
-// the 27 cells around (x, y, z)
+// the 27 cells around (x, y, z); the next cell's bucket range is read from LDS while this cell's
+// records are scanned (one dependent LDS round trip less per cell)
 template <typename Fn>
 __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
                                             double ay, double az, Fn &&fn)
 {
+    const unsigned long long mask = ~0ull ^ (with ? 0ull : kKeptBit);
+    auto range = [&](int d, unsigned long long &key) {
+        const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
+        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        key = pack3(cx, cy, cz) | with;
+        const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
+        return make_int2(g.bs[b], g.bs[b + 1]);
+    };
+    unsigned long long nkey = 0;
+    int2 nr = range(0, nkey);
 #pragma unroll 1
     for (int d = 0; d < 27; d++) {  // rolled: one copy of fn (instruction cache)
-        const int dz = d / 9 - 1, dy = (d / 3) % 3 - 1, dx = d % 3 - 1;
-        lds_cell(g, x + dx, y + dy, z + dz, with, ax, ay, az, fn);
+        const unsigned long long key = nkey;
+        const int2 r = nr;
+        if (d + 1 < 27) nr = range(d + 1, nkey);
+        int q = r.x;
+        const int e = r.y;
+        for (; q + kLdsCellUnroll <= e; q += kLdsCellUnroll) {
+            double4 p[kLdsCellUnroll];
+#pragma unroll
+            for (int u = 0; u < kLdsCellUnroll; u++) p[u] = g.pt[q + u];
+#pragma unroll
+            for (int u = 0; u < kLdsCellUnroll; u++) {
+                if ((static_cast<unsigned long long>(__double_as_longlong(p[u].w)) & mask) != key) continue;
+                const double dx = ax - p[u].x, dy = ay - p[u].y, dz = az - p[u].z;
+                fn(q + u, ((dx * dx) + (dy * dy)) + (dz * dz));
+            }
+        }
+        for (; q < e; q++) {
+            const double4 p = g.pt[q];
+            if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & mask) != key) continue;
+            const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
+            fn(q, ((dx * dx) + (dy * dy)) + (dz * dz));
+        }
     }
 }
 
