@@ -1834,10 +1834,17 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(mc::kBpClasses, std::max(0, atoi(e)));
         // test knob: MC_VX_GLOBAL=1 hands every slot to the global-hash voxel kernel
         const bool vx_global = getenv("MC_VX_GLOBAL") && atoi(getenv("MC_VX_GLOBAL")) != 0;
-        // frames per batch: bounded pixel capacity of the per-slot arrays
-        // (≈ 180 B of per-batch arrays per pixel: 192 M pixels ≈ 35 GB of HBM; a C3 frame is 2.76 M
-        // pixels, so a batch holds ~70 frames and the per-batch sync and slot tails amortise)
-        size_t budget = static_cast<size_t>(192) << 20;
+        // frames per batch: bounded pixel capacity of the per-slot arrays (≈ 200 B of per-batch arrays
+        // per pixel).  Large batches amortise every group's slot tail and the per-batch sync (C3 E2E:
+        // 192 M pixels 215 ms, 400 M 184 ms, 600 M 175 ms per scene), so the batch takes up to 640 M
+        // pixels (≈ 130 GB of the 288 GB) or 45 % of the free HBM, whichever is less.
+        size_t budget = static_cast<size_t>(640) << 20;
+        if (ctx->bp_px_cap < budget) {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+                budget = std::max<size_t>(static_cast<size_t>(16) << 20,
+                                          std::min(budget, (free_b + ctx->bp_px_cap * 200) / 100 * 45 / 200));
+        }
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         const int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
         bp_reserve(ctx, FB, H, W, nbands, s);
