@@ -51,8 +51,8 @@ struct mc_ctx {
     bool own_stream = false;
     hipStream_t side = nullptr;                 // S3: workgroup-per-mask kernel beside the wave kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipStream_t cls_stream[mc::kBpClasses] = {};  // S1 denoise: the LDS size classes run side by side
-    hipEvent_t ev_cls[mc::kBpClasses] = {};
+    hipStream_t cls_stream[mc::kBpStreamClasses] = {};  // S1 denoise: the LDS size classes run side by side
+    hipEvent_t ev_cls[mc::kBpStreamClasses] = {};
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
@@ -282,7 +282,7 @@ int mc_ctx_create(int device, mc_ctx **out)
         MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-        for (int c = 0; c < mc::kBpClasses; c++) {
+        for (int c = 0; c < mc::kBpStreamClasses; c++) {
             MC_HIP(hipStreamCreateWithFlags(&ctx->cls_stream[c], hipStreamNonBlocking));
             MC_HIP(hipEventCreateWithFlags(&ctx->ev_cls[c], hipEventDisableTiming));
         }
@@ -344,7 +344,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     if (ctx->side) (void)hipStreamSynchronize(ctx->side), (void)hipStreamDestroy(ctx->side);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    for (int c = 0; c < mc::kBpClasses; c++) {
+    for (int c = 0; c < mc::kBpStreamClasses; c++) {
         if (ctx->cls_stream[c]) (void)hipStreamSynchronize(ctx->cls_stream[c]), (void)hipStreamDestroy(ctx->cls_stream[c]);
         if (ctx->ev_cls[c]) (void)hipEventDestroy(ctx->ev_cls[c]);
     }
@@ -1517,7 +1517,8 @@ inline size_t nbl_offset(const mc_ctx *ctx, int cls)
                                             static_cast<size_t>(mc::BpLdsClass<1024>::kWgPerCu) * 1024,
                                             static_cast<size_t>(mc::BpLdsClass<2048>::kWgPerCu) * 2048,
                                             static_cast<size_t>(mc::BpLdsClass<3072>::kWgPerCu) * 3072,
-                                            static_cast<size_t>(mc::BpLdsClass<4096>::kWgPerCu) * 4096};
+                                            static_cast<size_t>(mc::BpLdsClass<4096>::kWgPerCu) * 4096,
+                                            static_cast<size_t>(mc::BpLdsClass<16384>::kWgPerCu) * 16384};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
     return o * static_cast<size_t>(ctx->num_cu) * kBpOversub * mc::kBpNbCap;
@@ -1529,7 +1530,8 @@ inline size_t lean_offset(const mc_ctx *ctx, int cls)
     const size_t per_cls[mc::kBpClasses] = {
         mc::kBpLeanInts<512> * mc::BpLdsClass<512>::kWgPerCu, mc::kBpLeanInts<1024> * mc::BpLdsClass<1024>::kWgPerCu,
         mc::kBpLeanInts<2048> * mc::BpLdsClass<2048>::kWgPerCu, mc::kBpLeanInts<3072> * mc::BpLdsClass<3072>::kWgPerCu,
-        mc::kBpLeanInts<4096> * mc::BpLdsClass<4096>::kWgPerCu};
+        mc::kBpLeanInts<4096> * mc::BpLdsClass<4096>::kWgPerCu,
+        mc::kBpLeanInts<16384> * mc::BpLdsClass<16384>::kWgPerCu};
     size_t o = 0;
     for (int c = 0; c < cls; c++) o += per_cls[c];
     return o * static_cast<size_t>(ctx->num_cu) * kBpOversub;
@@ -1929,6 +1931,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
                 MC_HIP(hipEventRecord(ctx->ev_fork, s));
                 MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+                bp_denoise_class<16384>(ctx, ctx->side, 5, ncap, st, dv);  // few, large slots
                 hipLaunchKernelGGL(mc::k_bp_denoise, dim3(ctx->num_cu), dim3(256), 0, ctx->side, st + BS_CLS + mc::kBpClasses,
                                    ctx->d_cls_list.as<int>() + mc::kBpClasses * static_cast<size_t>(ncap), ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                                    ctx->d_pcell.as<unsigned long long>(), ctx->d_pbkt.as<int>(), ctx->d_bcnt.as<int>(),
@@ -1940,13 +1943,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 MC_HIP(hipEventRecord(ctx->ev_join, ctx->side));
                 // the LDS classes side by side, each on its own stream: a class with few slots
                 // (the large ones) leaves most CUs to the others instead of serialising the batch
-                for (int c = 0; c < mc::kBpClasses; c++) MC_HIP(hipStreamWaitEvent(ctx->cls_stream[c], ctx->ev_fork, 0));
+                for (int c = 0; c < mc::kBpStreamClasses; c++) MC_HIP(hipStreamWaitEvent(ctx->cls_stream[c], ctx->ev_fork, 0));
                 bp_denoise_class<3072>(ctx, ctx->cls_stream[3], 3, ncap, st, dv);
                 bp_denoise_class<4096>(ctx, ctx->cls_stream[4], 4, ncap, st, dv);
                 bp_denoise_class<2048>(ctx, ctx->cls_stream[2], 2, ncap, st, dv);
                 bp_denoise_class<1024>(ctx, ctx->cls_stream[1], 1, ncap, st, dv);
                 bp_denoise_class<512>(ctx, ctx->cls_stream[0], 0, ncap, st, dv);
-                for (int c = 0; c < mc::kBpClasses; c++) {
+                for (int c = 0; c < mc::kBpStreamClasses; c++) {
                     MC_HIP(hipEventRecord(ctx->ev_cls[c], ctx->cls_stream[c]));
                     MC_HIP(hipStreamWaitEvent(s, ctx->ev_cls[c], 0));
                 }

@@ -980,8 +980,9 @@ __device__ __forceinline__ double seq_add64_pos(double acc, double v)
 
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
-constexpr int kBpLdsN = 4096;  // largest LDS class
-constexpr int kBpClasses = 5;  // LDS classes (512, 1024, 2048, 3072, 4096); class kBpClasses = k_bp_denoise
+constexpr int kBpLdsN = 16384;  // largest class of the LDS-kernel template
+constexpr int kBpClasses = 6;   // classes 512, 1024, 2048, 3072, 4096, 16384; class kBpClasses = k_bp_denoise
+constexpr int kBpStreamClasses = 5;  // classes with a stream of their own (the 16384 class shares the side stream)
 constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
 template <int N>
 struct BpLdsClass;
@@ -1019,14 +1020,24 @@ template <>
 struct BpLdsClass<4096> {
     static constexpr int T = MC_BP_TBIG, kWgPerCu = 1, kLean = 2;
 };
+template <>  // kLean 3: every per-point array in global scratch (large, rare slots)
+struct BpLdsClass<16384> {
+    static constexpr int T = 1024, kWgPerCu = 1, kLean = 3;
+};
 template <int N>
 constexpr bool kBpLean = BpLdsClass<N>::kLean >= 1;
 template <int N>
 constexpr bool kBpLean2 = BpLdsClass<N>::kLean >= 2;
-// global scratch ints per workgroup of a lean class: savg (2N), sB (2N + 2), sX (N), sorig + spos (N)
-// [+ sflag (N), spar (N)]
 template <int N>
-constexpr size_t kBpLeanInts = kBpLean<N> ? (kBpLean2<N> ? 8 : 6) * static_cast<size_t>(N) + 2 : 0;
+constexpr bool kBpLean3 = BpLdsClass<N>::kLean >= 3;
+// global scratch ints per workgroup of a lean class: [lean 3: cell-sorted points (8N), bucket starts
+// (N + 1, padded to N + 8)] savg (2N), sB (2N + 2), sX (N), sorig + spos (N) [lean 2: + sflag (N),
+// spar (N)]; a multiple of 8 ints, so every region stays 32-byte aligned
+template <int N>
+constexpr size_t kBpLean3Pre = kBpLean3<N> ? 9 * static_cast<size_t>(N) + 8 : 0;
+template <int N>
+constexpr size_t kBpLeanInts =
+    kBpLean<N> ? ((kBpLean3Pre<N> + (kBpLean2<N> ? 8 : 6) * static_cast<size_t>(N) + 2 + 7) / 8) * 8 : 0;
 
 struct BpLdsGrid {
     const double4 *pt;  // x, y, z, cell key bits (bit 63: kept by the class filter) per sorted position
@@ -1193,7 +1204,8 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
     for (int s = blockIdx.x * 256 + threadIdx.x; s - static_cast<int>(threadIdx.x) < NS; s += gridDim.x * 256) {
         const bool live = s < NS;
         const int n = live ? slot_nv[s] : 0;
-        const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 3072 ? 3 : n <= kBpLdsN ? 4 : 5);
+        const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 3072 ? 3 : n <= 4096 ? 4
+                                                                                                 : n <= kBpLdsN ? 5 : 6);
 #pragma unroll
         for (int k = 0; k <= kBpClasses; k++) {
             const unsigned long long b = __ballot(live && c == k);
@@ -1238,8 +1250,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     constexpr int NBK = kLean ? 1 : 2;   // hash buckets per point
     constexpr int kFbCount = 2 * N + 1;  // index of the fallback counter in sB
     constexpr int NL = kLean ? 1 : N;    // extent of the arrays a lean class keeps in global scratch
-    __shared__ double4 spt[N];           // cell-sorted points + cell keys
-    __shared__ int sA[NBK * N + 1];      // bucket starts
+    constexpr bool kLean3 = kBpLean3<N>;
+    __shared__ double4 spt_l[kLean3 ? 1 : N];  // cell-sorted points + cell keys
+    __shared__ int sA_l[kLean3 ? 1 : NBK * N + 1];  // bucket starts
     __shared__ int sB_l[2 * NL + 2];     // bucket counts; then min original index per root [0, n) +
                                          // class counts [N, ..); then the k-NN fallback list
     __shared__ short sorig_l[NL], spos_l[NL];  // sorted position <-> original index
@@ -1248,7 +1261,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     __shared__ int spar_l[NL2];          // union-find over positions, then roots, then kept ranks
     __shared__ int sX_l[NL];             // bucket per point; rank per root; S list
     __shared__ double savg_l[NL];        // labels (int view); then mean distances
-    int *const gs = lean_scr + static_cast<size_t>(blockIdx.x) * kBpLeanInts<N>;
+    int *const gs0 = lean_scr + static_cast<size_t>(blockIdx.x) * kBpLeanInts<N>;
+    double4 *const spt = kLean3 ? reinterpret_cast<double4 *>(gs0) : spt_l;
+    int *const sA = kLean3 ? gs0 + 8 * N : sA_l;
+    int *const gs = gs0 + kBpLean3Pre<N>;
     double *const savg = kLean ? reinterpret_cast<double *>(gs) : savg_l;
     int *const sB = kLean ? gs + 2 * N : sB_l;
     int *const sX = kLean ? gs + 4 * N + 2 : sX_l;

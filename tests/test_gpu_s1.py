@@ -131,10 +131,11 @@ def test_end_to_end_matches_oracle(ctx):
     assert_matches(run.canonical(), want)
 
 
-@pytest.mark.parametrize("min_cls", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("min_cls", [1, 2, 3, 4, 5, 6])
 def test_denoise_size_classes_agree(ctx, monkeypatch, min_cls):
     """Every denoise size class (LDS 512/1024/2048 points, the lean 3072- and 4096-point classes,
-    the global-memory kernel) gives the same masks: all slots forced into class >= min_cls."""
+    the 16384-point class with every array in global scratch, the global-memory kernel) gives the
+    same masks: all slots forced into class >= min_cls."""
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
     a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
