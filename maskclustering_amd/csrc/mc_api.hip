@@ -1500,7 +1500,8 @@ enum BpStat : int {
     BS_ERRF = 0, BS_VOXERR, BS_OVF, BS_TOP, BS_NS, BS_NPX, BS_M, BS_NNZ,
     BS_CLS,             // denoise size-class counts (kBpClasses LDS classes + the global-memory kernel)
     BS_TK = BS_CLS + mc::kBpClasses + 1,  // ticket counters of the LDS classes
-    BS_VXFB = BS_TK + mc::kBpClasses,     // slots k_bp_voxel_lds hands to k_bp_voxel
+    BS_VXFB = BS_TK + mc::kBpClasses,     // slots the first voxel tier hands to the second
+    BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
     BS_COUNT
 };
 
@@ -1559,7 +1560,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_slot_box.reserve(slots * 6 * 4);
     ctx->d_cls_list.reserve((mc::kBpClasses + 1) * slots * 4);
     ctx->d_vox_order.reserve(slots * 4);
-    ctx->d_vx_fb.reserve(slots * 4);
+    ctx->d_vx_fb.reserve(2 * slots * 4);  // the two tiers' overflow lists
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
     ctx->d_nbl.reserve(nbl_offset(ctx, mc::kBpClasses) * 2);
     ctx->d_lean.reserve(lean_offset(ctx, mc::kBpClasses) * 4);
@@ -1834,8 +1835,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // global-memory kernel for every slot)
         int min_cls = 0;
         if (const char *e = getenv("MC_BP_MIN_CLASS")) min_cls = std::min(mc::kBpClasses, std::max(0, atoi(e)));
-        // test knob: MC_VX_GLOBAL=1 hands every slot to the global-hash voxel kernel
-        const bool vx_global = getenv("MC_VX_GLOBAL") && atoi(getenv("MC_VX_GLOBAL")) != 0;
+        // test knob: MC_VX_GLOBAL=1 hands every slot to the global-hash voxel kernel, =2 to the second
+        // LDS tier
+        const int vx_global = getenv("MC_VX_GLOBAL") ? atoi(getenv("MC_VX_GLOBAL")) : 0;
         // frames per batch: bounded pixel capacity of the per-slot arrays (≈ 200 B of per-batch arrays
         // per pixel).  Large batches amortise every group's slot tail and the per-batch sync (C3 E2E:
         // 192 M pixels 215 ms, 400 M 184 ms, 600 M 175 ms per scene), so the batch takes up to 640 M
@@ -1910,13 +1912,19 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 TimedScope ts(ctx->timer, s, "bp_voxel");
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
                                    ctx->d_vox_order.as<int>());
-                hipLaunchKernelGGL(mc::k_bp_voxel_lds, dim3(ctx->num_cu * 2), dim3(mc::kVxT), 0, s, st + BS_NS,
-                                   ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
+                int *fb1 = ctx->d_vx_fb.as<int>(), *fb2 = fb1 + slots_cap(FB);
+                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH, mc::kVxV>), dim3(ctx->num_cu * 2), dim3(mc::kVxT), 0, s,
+                                   st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
+                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
+                                   KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
+                                   ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
+                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH2, mc::kVxV2>), dim3(ctx->num_cu), dim3(mc::kVxT), 0, s,
+                                   st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
                                    ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
-                                   ctx->d_slot_nv.as<int>(), ctx->d_vx_fb.as<int>(), st + BS_VXFB, vx_global ? 1 : 0);
-                hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB,
-                                   ctx->d_vx_fb.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
+                                   ctx->d_slot_nv.as<int>(), fb2, st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB2,
+                                   fb2, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
                                    ctx->d_hkey.as<unsigned long long>(), ctx->d_hvid.as<int>(), ctx->d_hfirst.as<int>(),
                                    ctx->d_vox_entry.as<int>(), ctx->d_acc.as<double>(), ctx->d_vpts.as<double>(),

@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
 //   4. a thread per voxel adds its list's points in order; mean
 // Only LDS between the chunk barriers: no global atomics, no global read-modify-write chains.
 // A slot whose voxel coordinates span >= 1024 voxels on an axis or that has more than kVxV voxels
-// is listed for k_bp_voxel (the global-hash kernel below) instead.
+// is listed for the next tier (the larger LDS tables, then k_bp_voxel, the global-hash kernel below).
 // Largest slots first (their per-slot time grows with the pixel count): slots binned by
 // floor(log2(pixels)), bins in descending order.  One workgroup.
 __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ dNS, const int *__restrict__ slot_np,
@@ -409,8 +409,10 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
 }
 
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
-constexpr int kVxH = 6144;       // LDS hash entries (load <= 2/3)
-constexpr int kVxV = 4096;       // voxels per slot in LDS (hash + counters: 64 KB, two workgroups per CU)
+// tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
+// (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
+constexpr int kVxH = 6144, kVxV = 4096;      // first tier: LDS hash entries (load <= 2/3), voxels
+constexpr int kVxH2 = 12288, kVxV2 = 8192;   // second tier
 constexpr unsigned kVxEmpty = ~0u;
 
 __device__ __forceinline__ void vx_point(const unsigned *__restrict__ pl, const float *__restrict__ dep,
@@ -421,6 +423,7 @@ __device__ __forceinline__ void vx_point(const unsigned *__restrict__ pl, const 
     bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], x, y, z);
 }
 
+template <int kVxH, int kVxV>
 __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
                                                        const int *__restrict__ slot_frame, const int *__restrict__ slot_np,
                                                        const int *__restrict__ slot_pix,

@@ -147,14 +147,16 @@ def test_denoise_size_classes_agree(ctx, monkeypatch, min_cls):
         np.testing.assert_array_equal(x, y)
 
 
-def test_voxel_kernels_agree(ctx, monkeypatch):
-    """voxel_down_sample's two kernels (the LDS-resident one every slot starts in; the global-hash one
-    it hands overflowing slots to) give the same voxels: every slot forced onto the global kernel."""
+@pytest.mark.parametrize("tier", [1, 2])
+def test_voxel_kernels_agree(ctx, monkeypatch, tier):
+    """voxel_down_sample's kernels (the LDS tier every slot starts in; the larger LDS tier and the
+    global-hash kernel it hands overflowing slots to) give the same voxels: every slot forced onto
+    the global kernel (tier 1) or the second LDS tier (tier 2)."""
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
     a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
     sa = ctx.bp_candidates()
-    monkeypatch.setenv("MC_VX_GLOBAL", "1")
+    monkeypatch.setenv("MC_VX_GLOBAL", str(tier))
     b = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
     np.testing.assert_array_equal(sa, ctx.bp_candidates())
     for x, y in zip(a, b):
