@@ -1865,6 +1865,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         dv.trunc = prm.depth_trunc;
         dv.vs = prm.voxel_size;
         dv.eps2 = prm.dbscan_eps * prm.dbscan_eps;
+        for (int i = 0; i < 3; i++) {
+            const double f = 0.6 + 0.15 * i;
+            dv.knn_r2[i] = (f * prm.dbscan_eps) * (f * prm.dbscan_eps);
+        }
         dv.ce = prm.dbscan_eps * 1.01;
         dv.frac = prm.component_min_fraction;
         dv.std_ratio = prm.sor_std_ratio;

@@ -33,6 +33,7 @@ constexpr int kCellBias = 1 << 20; // scene-grid cell coordinates in [-2^20, 2^2
 
 struct BpDev {
     double trunc, vs, eps2, ce, frac, std_ratio, cov;
+    double knn_r2[3];  // k-NN pre-selection radii^2 (0.6, 0.75, 0.9 eps)
     float r2, scene_inv;
     int minpts, knn, kball, few;
     int H, W, nbands;
@@ -1550,13 +1551,42 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
             int found = 0;
-            nb_list_pts<N>(nbw, spt, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](const double4 &p) {
-                if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
-                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                if (MC_ABLATE_BP == 3) best[0] += ((ex * ex) + (ey * ey)) + (ez * ez);
-                else sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
-                found++;
-            });
+            // count pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = list entry k);
+            // if >= k of them lie inside radius i, the k nearest are among those (every other kept
+            // candidate is farther than >= k others), so only they are inserted: each lane walks its
+            // own mask, and the wave's insert loop runs max-over-lanes of ~k + a few instead of the
+            // largest list
+            unsigned long long m1 = 0, m2 = 0, m3 = 0, mall = 0;
+            {
+                int k = 0;
+                nb_list_pts<N>(nbw, spt, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](const double4 &p) {
+                    const unsigned long long bit = 1ull << k;
+                    k++;
+                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    const double d2 = ((ex * ex) + (ey * ey)) + (ez * ez);
+                    mall |= bit;
+                    if (d2 < pr.knn_r2[0]) m1 |= bit;
+                    if (d2 < pr.knn_r2[1]) m2 |= bit;
+                    if (d2 < pr.knn_r2[2]) m3 |= bit;
+                });
+            }
+            found = __popcll(mall);
+            unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
+            if (found >= kk) {
+                const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // entry k: lst[(k / 8) * 8 * N + k % 8]
+                auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)]); };
+                int k = pm ? __ffsll(static_cast<long long>(pm)) - 1 : 0;
+                double4 nxt = pm ? spt[entry(k)] : make_double4(0.0, 0.0, 0.0, 0.0);
+                while (pm) {
+                    pm &= pm - 1;
+                    const double4 p = nxt;
+                    if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    if (MC_ABLATE_BP == 3) best[0] += ((ex * ex) + (ey * ey)) + (ez * ez);
+                    else sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+                }
+            }
 #if MC_ABLATE_BP == 3 || MC_ABLATE_BP == 4
             found = kk;
 #endif
