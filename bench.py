@@ -687,6 +687,10 @@ def main():
     calib = {g: ctx.kernel_time(g) for g in runner.groups}
     ctx.set_timing(False)
     work = runner.work()
+    for g in BP_GROUPS:  # S1 models are scene totals: per launch = total / the group's launches per scene
+        if g in work and calib.get(g, (0, 0))[1]:
+            b, tot, model, alt = work[g]
+            work[g] = (b, tot / calib[g][1], model + " per scene / launches per scene", alt)
     dominant = max((g for g in calib if g in work), key=lambda g: calib[g][0])
     log("calibration (ms):", json.dumps({k: round(v[0], 4) for k, v in calib.items()}), "dominant:", dominant)
 
@@ -749,6 +753,12 @@ def main():
                         "on the same synthetic scene, both on the 8-core build container (scripts/cpu_ratio.py)",
                 "reference_s": r["reference_s"], "port_s_container": r["port_s"],
                 "port_threads_container": r["port_threads"], "reference_over_port": r["reference_over_port"]}
+        elif args.variant == "e2e":
+            cpu["reference_context"] = {
+                "note": "the reference's own S1 (utils/mask_backprojection.py) calls Open3D and pytorch3d, which are not "
+                        "installed in the build container or on the box, so only its S2-S6 was timed against the C port "
+                        f"(profiles/cpu_ratio_c2.json: the reference over the port for S2-S6 on C2); S1 here is the "
+                        "port's restatement (oracle/s1_oracle.c) on one thread"}
 
     if rank == 0:
         line = {

@@ -549,7 +549,10 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
-        for (int c0 = 0; c0 < n; c0 += kVxT) {
+#ifndef MC_ABLATE_VX
+#define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
+#endif
+        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
             const int v = k < n ? pvid[base + k] : -1;
             int rank = 0, leader = 0, cnt = 0;
@@ -577,7 +580,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
-        for (int v = t; v < nv; v += kVxT) {
+        for (int v = t; v < (MC_ABLATE_VX ? 0 : nv); v += kVxT) {
             const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
