@@ -116,7 +116,7 @@ struct mc_ctx {
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
-    DevBuf d_vx_pvid, d_vx_list, d_vx_fb;
+    DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt;
     int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
@@ -333,7 +333,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
-                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_acc, &ctx->d_hvid};
+                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_acc, &ctx->d_hvid};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (int b = 0; b < 2; b++) {
@@ -1574,6 +1574,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
         fill_u32(s, ctx->d_hfirst.ptr, 2 * px, 0x7FFFFFFFu);  // INT_MAX
         ctx->d_acc.reserve(px * 4 * 8);
         ctx->d_vx_pvid.reserve(px * 4);
+        ctx->d_vx_ppt.reserve(px * 3 * 8);
         ctx->d_vx_list.reserve(px * 4);
         ctx->d_vox_entry.reserve(px * 4);
         ctx->d_vpts.reserve(px * 3 * 8);
@@ -1920,13 +1921,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH, mc::kVxV>), dim3(ctx->num_cu * 2), dim3(mc::kVxT), 0, s,
                                    st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
                                    ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
-                                   KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
+                                   KB, TB, dv, ctx->d_vx_ppt.as<double>(), ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
                                    ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
                 hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH2, mc::kVxV2>), dim3(ctx->num_cu), dim3(mc::kVxT), 0, s,
                                    st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
-                                   ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
-                                   ctx->d_slot_nv.as<int>(), fb2, st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                                   ctx->d_vx_ppt.as<double>(), ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(),
+                                   ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2, st + BS_VXFB2, vx_global == 1 ? 1 : 0);
                 hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB2,
                                    fb2, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,

@@ -430,7 +430,8 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                                                        const int *__restrict__ slot_pix,
                                                        const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
                                                        const double *__restrict__ intr, const double *__restrict__ pose,
-                                                       BpDev pr, int *__restrict__ pvid, int *__restrict__ vlist,
+                                                       BpDev pr, double *__restrict__ ppt, int *__restrict__ pvid,
+                                                       int *__restrict__ vlist,
                                                        double *__restrict__ vpts, int *__restrict__ slot_nv,
                                                        int *__restrict__ fb_list, int *__restrict__ fb_cnt, int force_fb)
 {
@@ -462,13 +463,30 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         for (int i = t; i < kVxV; i += kVxT) vcur[i] = 0;
         if (t == 0) s_flag = 0;
-        // 0. min bound
+        // 0. world points (stored at the list position for 1. and 4.) and the min bound; four pixels'
+        //    loads per thread in flight
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        for (int k = t; k < n; k += kVxT) {
-            double p[3];
-            vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
+        double *pp = ppt + 3 * static_cast<size_t>(base);
+        for (int k0 = t; k0 < n; k0 += 4 * kVxT) {
+            unsigned iv[4];
+            float dv[4];
 #pragma unroll
-            for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
+            for (int u = 0; u < 4; u++) iv[u] = k0 + u * kVxT < n ? pl[k0 + u * kVxT] : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; u++) dv[u] = k0 + u * kVxT < n ? dep[iv[u]] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * kVxT;
+                if (k < n) {
+                    double p[3];
+                    bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        pp[3 * k + c] = p[c];
+                        mn[c] = fmin(mn[c], p[c]);
+                    }
+                }
+            }
         }
         block_minmax3_nw<NW>(mn, mx, red);
         double vmin[3];
@@ -480,8 +498,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int k = c0 + t;
             int h = -1;
             if (k < n) {
-                double p[3];
-                vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
+                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
                 unsigned key = 0;
                 bool fits = true;
 #pragma unroll
@@ -586,9 +603,9 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
             for (; j + 4 <= b1; j += 4) {
-                double q[4][3];
+                const double *q[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) vx_point(pl, dep, K, T, W, vl[j + u], q[u][0], q[u][1], q[u][2]);
+                for (int u = 0; u < 4; u++) q[u] = pp + 3 * vl[j + u];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     ax = ax + q[u][0];
@@ -597,11 +614,10 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 }
             }
             for (; j < b1; j++) {
-                double x, y, z;
-                vx_point(pl, dep, K, T, W, vl[j], x, y, z);
-                ax = ax + x;
-                ay = ay + y;
-                az = az + z;
+                const double *q = pp + 3 * vl[j];
+                ax = ax + q[0];
+                ay = ay + q[1];
+                az = az + q[2];
             }
             const double dn = static_cast<double>(b1 - b0);
             double *o = vpts + 3 * (static_cast<size_t>(base) + v);
