@@ -409,6 +409,18 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
     for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1)] = s;
 }
 
+// Workgroup barrier that orders LDS only: this wave's LDS operations complete (lgkmcnt 0), global
+// loads stay in flight (vmcnt not waited, unlike __syncthreads' fence), then s_barrier; the empty
+// asm statements keep the compiler from moving memory operations across it.  For steps whose only
+// cross-wave traffic is LDS.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt 63 (no wait), expcnt 7, lgkmcnt 0
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
 // (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
@@ -569,9 +581,12 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
+        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the
+                                                  // LDS-only barriers below
         for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
-            const int v = k < n ? pvid[base + k] : -1;
+            const int v = vnext;
+            vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
             int rank = 0, leader = 0, cnt = 0;
             unsigned long long act = __ballot(v >= 0);
             while (act) {
@@ -591,7 +606,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                     gb[w][lane] = vcur[v];
                     vcur[v] += cnt;
                 }
-                __syncthreads();
+                lds_barrier();
             }
             if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
         }
