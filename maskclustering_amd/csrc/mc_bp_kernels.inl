@@ -1459,9 +1459,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         BP_STAMP(22);
         // 7. roots; every component keyed by its smallest original index; clusters ranked by it
         {
-            int rq[N / T];
+            int rq[(N + T - 1) / T];
 #pragma unroll
-            for (int k = 0; k < N / T; k++) {
+            for (int k = 0; k < (N + T - 1) / T; k++) {
                 const int q = t + k * T;
                 rq[k] = (q < n && sflag[q] >= pr.minpts) ? uf_find_s(spar, q) : -1;
             }
@@ -1469,7 +1469,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) sB[q] = INT_MAX;
             for (int x = t; x <= n; x += T) ccnt[x] = 0;
 #pragma unroll
-            for (int k = 0; k < N / T; k++) {
+            for (int k = 0; k < (N + T - 1) / T; k++) {
                 const int q = t + k * T;
                 if (q < n) spar[q] = rq[k];
             }
