@@ -217,6 +217,46 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
     const int sb = band * kBpWaves + wv;  // this wave's sub-band
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int trunc = 0, lastp = -1;
+    if ((W & 3) == 0) {  // four consecutive pixels per lane: one 4-byte seg load and one 16-byte depth load
+      for (int ib0 = i0; ib0 < i1; ib0 += 256 * 2) {
+        uchar4 sv[2];
+        float4 dq[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int i = ib0 + 256 * u + 4 * lane;
+          sv[u] = i < i1 ? *reinterpret_cast<const uchar4 *>(seg + fb + i) : make_uchar4(0, 0, 0, 0);
+          dq[u] = i < i1 ? *reinterpret_cast<const float4 *>(depth + fb + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int i = ib0 + 256 * u + 4 * lane;
+          const int sids[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+          const float ds[4] = {dq[u].x, dq[u].y, dq[u].z, dq[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            int id = -1;
+            if (i < i1) {
+                const int sid = sids[j];
+                const float d = ds[j];
+                if (sid != lastp) {
+                    atomicOr(&pres[sid >> 5], 1u << (sid & 31));
+                    lastp = sid;
+                }
+                if (static_cast<double>(d) == pr.trunc) trunc = 1;
+                if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id = sid;
+            }
+            unsigned long long act = __ballot(id >= 0);
+            while (act) {
+                const int leader = __ffsll(static_cast<long long>(act)) - 1;
+                const int k = __shfl(id, leader, 64);
+                const unsigned long long m = __ballot(id == k);
+                if (lane == leader) cnt[wv][k] += __popcll(m);
+                act &= ~m;
+            }
+          }
+        }
+      }
+    } else
     for (int ib0 = i0; ib0 < i1; ib0 += 64 * kBpPix) {
       // kBpPix steps' loads issued before the first is used
       int sidv[kBpPix];
@@ -331,6 +371,76 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
     const int sb = band * kBpWaves + wv;
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int *mycur = cur[wv];
+    if ((W & 3) == 0) {
+      // four consecutive pixels per lane (lane-major: pixel = 4 * lane + j of the 256-pixel step);
+      // per id: each lane counts its matching pixels, a wave exclusive scan of the counts gives
+      // the lanes' bases, the leader bumps the cursor by the total
+      for (int ib0 = i0; ib0 < i1; ib0 += 256 * 2) {
+        uchar4 sv[2];
+        float4 dq[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int i = ib0 + 256 * u + 4 * lane;
+          sv[u] = i < i1 ? *reinterpret_cast<const uchar4 *>(seg + fb + i) : make_uchar4(0, 0, 0, 0);
+          dq[u] = i < i1 ? *reinterpret_cast<const float4 *>(depth + fb + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int i = ib0 + 256 * u + 4 * lane;
+          const int sids[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+          const float ds[4] = {dq[u].x, dq[u].y, dq[u].z, dq[u].w};
+          int id[4];
+          unsigned pend = 0u;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            id[j] = -1;
+            if (i < i1) {
+                const int sid = sids[j];
+                const float d = ds[j];
+                if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && mycur[sid] >= 0) id[j] = sid;
+            }
+            if (id[j] >= 0) pend |= 1u << j;
+          }
+          int pos[4] = {0, 0, 0, 0};
+          while (true) {
+            const unsigned long long act = __ballot(pend != 0u);
+            if (!act) break;
+            const int L = __ffsll(static_cast<long long>(act)) - 1;
+            int mine = -1;
+#pragma unroll
+            for (int j = 3; j >= 0; j--)
+              if (pend & (1u << j)) mine = id[j];
+            const int k = __shfl(mine, L, 64);
+            unsigned mb = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if ((pend & (1u << j)) && id[j] == k) mb |= 1u << j;
+            const int c = __popc(mb);
+            int incl = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+              const int y = __shfl_up(incl, d, 64);
+              if (lane >= d) incl += y;
+            }
+            const int tot = __shfl(incl, 63, 64);
+            int b = 0;
+            if (lane == L) {
+              b = mycur[k];
+              mycur[k] = b + tot;
+            }
+            b = __shfl(b, L, 64) + incl - c;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (mb & (1u << j)) pos[j] = b + __popc(mb & ((1u << j) - 1u));
+            pend &= ~mb;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (id[j] >= 0) pix_list[pos[j]] = static_cast<unsigned>(i + j);
+        }
+      }
+      return;
+    }
     for (int ib0 = i0; ib0 < i1; ib0 += 64 * kBpPix) {
       int sidv[kBpPix];
       float dv[kBpPix];

@@ -169,3 +169,11 @@ def test_high_resolution_frame_matches_oracle(ctx):
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=7, H=1440, W=1920, num_frames=1)
     _check_against_oracle(ctx, fr)
+
+
+def test_odd_width_frames_match_oracle(ctx):
+    """Frames whose width is not a multiple of 4 take the pixel kernels' one-pixel-per-lane path
+    (the four-pixel loads need 4-pixel rows)."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("tiny", seed=11, H=90, W=122, num_frames=4)
+    _check_against_oracle(ctx, fr)
