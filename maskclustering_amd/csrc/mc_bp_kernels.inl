@@ -2208,10 +2208,30 @@ __global__ __launch_bounds__(256) void k_bp_query(
             int best[kBpBallMax];
 #pragma unroll
             for (int x = 0; x < kBpBallMax; x++) best[x] = INT_MAX;
-            // the 27 cells; the next cell's bucket range is loaded while this cell's points are
-            // scanned (one dependent global round trip less per cell)
+            // the cells the ball can reach: a scene point with d2 < r^2 (float, as below) has
+            // |dx|, |dy|, |dz| <= r, and the cells are 2r wide, so per axis the cells of
+            // [q - r, q + r] widened by a rounding margin (0.01 cell + the float error of q * inv):
+            // 2 per axis (8 cells) but where the margin crosses a cell border, instead of 27.  The
+            // next cell's bucket range is loaded while this cell's points are scanned.
+            int cl[3], cn[3];
+            {
+                const float qq[3] = {qx, qy, qz};
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const float c = qq[a] * pr.scene_inv;
+                    const float m = 0.01f + fabsf(c) * 2e-6f;
+                    const int lo_c = min(max(static_cast<int>(floorf(c - 0.5f - m)), -kCellBias), kCellBias - 1) + kCellBias;
+                    const int hi_c = min(max(static_cast<int>(floorf(c + 0.5f + m)), -kCellBias), kCellBias - 1) + kCellBias;
+                    cl[a] = lo_c;
+                    cn[a] = hi_c - lo_c + 1;
+                }
+            }
+            (void)cx;
+            (void)cy;
+            (void)cz;
+            const int ncell = cn[0] * cn[1] * cn[2];
             auto cell_range = [&](int d, unsigned long long &key) {
-                const int x = cx + d % 3 - 1, y = cy + (d / 3) % 3 - 1, z = cz + d / 9 - 1;
+                const int x = cl[0] + d % cn[0], y = cl[1] + (d / cn[0]) % cn[1], z = cl[2] + d / (cn[0] * cn[1]);
                 key = pack3(x, y, z);
                 const unsigned b = mod_mul(bp_hash3(x, y, z), gnb);
                 return make_int2(gstart[b], gstart[b + 1]);
@@ -2219,10 +2239,10 @@ __global__ __launch_bounds__(256) void k_bp_query(
             unsigned long long nkey;
             int2 nrng = cell_range(0, nkey);
 #pragma unroll 1
-            for (int d = 0; d < 27; d++) {
+            for (int d = 0; d < ncell; d++) {
                 const unsigned long long key = nkey;
                 const int2 rng = nrng;
-                if (d + 1 < 27) nrng = cell_range(d + 1, nkey);
+                if (d + 1 < ncell) nrng = cell_range(d + 1, nkey);
                 for (int k = rng.x; k < rng.y; k++) {
                     if (gcell[k] != key) continue;
                     const float4 p = gpts[k];
