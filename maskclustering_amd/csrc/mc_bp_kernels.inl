@@ -948,17 +948,21 @@ __device__ __forceinline__ void bp_shell(const BpCells &g, int cx, int cy, int c
         }
 }
 
-// sorted insert of v into the ascending array a[0..N) (drops the largest)
+// sorted insert of v into the ascending array a[0..N) (drops the largest): new a[q] =
+// min(a[q], max(a[q-1], v)) (a[q-1] if v < a[q-1], v if a[q-1] <= v < a[q], else a[q]), two native
+// min / max operations per step instead of two compares and four selects (no NaN reaches here:
+// squared distances and DBL_MAX / INT_MAX sentinels)
+__device__ __forceinline__ double ins_min(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double ins_max(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ int ins_min(int a, int b) { return min(a, b); }
+__device__ __forceinline__ int ins_max(int a, int b) { return max(a, b); }
 template <int N, typename V>
 __device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
 {
     if (!(v < a[N - 1])) return;
 #pragma unroll
-    for (int q = N - 1; q > 0; q--) {
-        const V prev = a[q - 1];
-        a[q] = (v < prev) ? prev : ((v < a[q]) ? v : a[q]);
-    }
-    a[0] = (v < a[0]) ? v : a[0];
+    for (int q = N - 1; q > 0; q--) a[q] = ins_min(a[q], ins_max(a[q - 1], v));
+    a[0] = ins_min(a[0], v);
 }
 
 // union-find over a workgroup's LDS parent array (root = smallest index)
