@@ -56,6 +56,9 @@ struct mc_ctx {
     std::string err;
     mc::KernelTimer timer;
     int *h_stats = nullptr;  // pinned
+    int *h_bppack = nullptr;   // pinned per-batch S1 readback (k_bp_pack), h_bppack_n ints
+    int *h_bpstat = nullptr;   // pinned per-batch statistics block
+    size_t h_bppack_n = 0;
     // pinned staging ring of mc_backproject_frames (two chunks, ping-pong)
     char *h_stage[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
@@ -116,7 +119,7 @@ struct mc_ctx {
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
-    DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt;
+    DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt, d_bppack;
     int num_cu = 256;
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
@@ -333,9 +336,11 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
-                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_acc, &ctx->d_hvid};
+                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    if (ctx->h_bppack) (void)hipHostFree(ctx->h_bppack);
+    if (ctx->h_bpstat) (void)hipHostFree(ctx->h_bpstat);
     for (int b = 0; b < 2; b++) {
         if (ctx->h_stage[b]) (void)hipHostFree(ctx->h_stage[b]);
         if (ctx->ev_stage[b]) (void)hipEventDestroy(ctx->ev_stage[b]);
@@ -1643,7 +1648,6 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
                        ctx->d_qpts.as<float>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
                        ctx->d_slot_box.as<float>());
 }
-const int kBpStatInit[BS_COUNT] = {INT_MAX};  // the rest zero
 // MC_BP_DEBUG_SYNC=1: synchronise and report after every S1 group (diagnostics of a stalled batch)
 void bp_debug_sync(hipStream_t s, const char *what)
 {
@@ -1885,7 +1889,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         dv.nbands = nbands;
 
         int *st = ctx->d_bpstat.as<int>();
-        std::vector<int> hs(BS_COUNT);
+        if (!ctx->h_bpstat) MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_bpstat), BS_COUNT * sizeof(int),
+                                                 hipHostMallocDefault));
+        int *const hs = ctx->h_bpstat;  // pinned
         for (int b0 = 0; b0 < F;) {
             const int fb = std::min(FB, F - b0);
             const float *dB = dep + b0 * HW;
@@ -1894,7 +1900,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             const int nslot = fb * 256;
             {
                 TimedScope ts(ctx->timer, s, "bp_pixels");
-                MC_HIP(hipMemcpyAsync(st, kBpStatInit, sizeof(kBpStatInit), hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(mc::k_bp_stat_init, dim3(1), dim3(64), 0, s, st, static_cast<int>(BS_COUNT));
                 MC_HIP(hipMemsetAsync(ctx->d_present.ptr, 0, fb * 8 * 4, s));
                 MC_HIP(hipMemsetAsync(ctx->d_fflags.ptr, 0, fb * 4, s));
                 hipLaunchKernelGGL(mc::k_bp_count, dim3(nbands, fb), dim3(256), 0, s, dB, sB, TB, dv,
@@ -1987,7 +1993,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                   ctx->d_ksize.as<int>(), ctx->d_moff.as<int>(), st + BS_NNZ);
                 bp_debug_sync(s, "bp_query");
             }
-            MC_HIP(hipMemcpyAsync(hs.data(), st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipMemcpyAsync(hs, st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));
             MC_HIP(hipStreamSynchronize(s));
             ctx->timer.collect();
             if (hs[BS_ERRF] != INT_MAX) {
@@ -2015,22 +2021,30 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_tmp.as<int>(), ctx->d_out_col.as<int>(), ctx->d_out_label.as<int>(),
                                    ctx->d_out_off.as<int>(), ctx->d_bp_pts.as<int>() + ctx->bp_nnz);
             }
-            std::vector<int> col(Mb), lab(Mb), off(Mb);
-            if (Mb) {
-                MC_HIP(hipMemcpyAsync(col.data(), ctx->d_out_col.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
-                MC_HIP(hipMemcpyAsync(lab.data(), ctx->d_out_label.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
-                MC_HIP(hipMemcpyAsync(off.data(), ctx->d_out_off.ptr, Mb * 4, hipMemcpyDeviceToHost, s));
+            // the kept masks' (col, label, off) and the 8 per-candidate statistics arrays: packed on
+            // the device, one copy into pinned memory
+            const size_t npack = 3 * static_cast<size_t>(Mb) + 8 * static_cast<size_t>(NS);
+            ctx->d_bppack.reserve((npack + 1) * 4);
+            if (ctx->h_bppack_n < npack) {
+                if (ctx->h_bppack) MC_HIP(hipHostFree(ctx->h_bppack));
+                ctx->h_bppack = nullptr;
+                ctx->h_bppack_n = 0;
+                const size_t n = npack + npack / 2 + 1024;
+                MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_bppack), n * 4, hipHostMallocDefault));
+                ctx->h_bppack_n = n;
             }
-            // per-candidate statistics
-            std::vector<int> sf(NS), sid(NS), snp(NS), snv(NS), sm(NS), sns(NS), scov(NS), snn(NS);
-            if (NS) {
-                const std::pair<void *, DevBuf *> cp[] = {{sf.data(), &ctx->d_slot_frame}, {sid.data(), &ctx->d_slot_id},
-                                                          {snp.data(), &ctx->d_slot_np},    {snv.data(), &ctx->d_slot_nv},
-                                                          {sm.data(), &ctx->d_slot_m},      {sns.data(), &ctx->d_slot_ns},
-                                                          {scov.data(), &ctx->d_slot_cov},  {snn.data(), &ctx->d_slot_nn}};
-                for (auto &c : cp) MC_HIP(hipMemcpyAsync(c.first, c.second->ptr, NS * 4, hipMemcpyDeviceToHost, s));
+            if (npack) {
+                hipLaunchKernelGGL(mc::k_bp_pack, grid_for(static_cast<int64_t>(npack)), dim3(256), 0, s, st + BS_NS, st + BS_M,
+                                   ctx->d_out_col.as<int>(), ctx->d_out_label.as<int>(), ctx->d_out_off.as<int>(),
+                                   ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(), ctx->d_slot_np.as<int>(),
+                                   ctx->d_slot_nv.as<int>(), ctx->d_slot_m.as<int>(), ctx->d_slot_ns.as<int>(),
+                                   ctx->d_slot_cov.as<int>(), ctx->d_slot_nn.as<int>(), ctx->d_bppack.as<int>());
+                MC_HIP(hipMemcpyAsync(ctx->h_bppack, ctx->d_bppack.ptr, npack * 4, hipMemcpyDeviceToHost, s));
             }
             MC_HIP(hipStreamSynchronize(s));
+            const int *col = ctx->h_bppack, *lab = col + Mb, *off = lab + Mb;
+            const int *sf = off + Mb, *sid = sf + NS, *snp = sid + NS, *snv = snp + NS, *sm = snv + NS,
+                      *sns = sm + NS, *scov = sns + NS, *snn = scov + NS;
             bp_debug_sync(s, "bp_emit");
             for (int g = 0; g < Mb; g++) {
                 ctx->bp_col.push_back(b0 + col[g]);

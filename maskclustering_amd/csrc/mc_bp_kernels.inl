@@ -2341,6 +2341,40 @@ __global__ __launch_bounds__(256) void k_bp_emit(const int *__restrict__ dNS, co
 }
 
 // per-slot nn >= 0 flags and sizes for the output scan
+// per-batch statistics block: the error frame at INT_MAX, every counter and ticket zero (a kernel
+// instead of a pageable host-to-device copy at every batch start)
+__global__ __launch_bounds__(64) void k_bp_stat_init(int *__restrict__ st, int n)
+{
+    for (int i = threadIdx.x; i < n; i += 64) st[i] = i == 0 ? INT_MAX : 0;
+}
+
+// Per-batch readback in one copy: [col | label | off] of the batch's Mb kept masks, then the 8
+// per-slot statistics arrays of its NS slots, contiguous in `out`
+__global__ __launch_bounds__(256) void k_bp_pack(const int *__restrict__ dNS, const int *__restrict__ dM,
+                                                 const int *__restrict__ col, const int *__restrict__ lab,
+                                                 const int *__restrict__ off, const int *__restrict__ s0,
+                                                 const int *__restrict__ s1, const int *__restrict__ s2,
+                                                 const int *__restrict__ s3, const int *__restrict__ s4,
+                                                 const int *__restrict__ s5, const int *__restrict__ s6,
+                                                 const int *__restrict__ s7, int *__restrict__ out)
+{
+    const int NS = *dNS, M = *dM;
+    const int *src[11] = {col, lab, off, s0, s1, s2, s3, s4, s5, s6, s7};
+    const size_t total = 3 * static_cast<size_t>(M) + 8 * static_cast<size_t>(NS);
+    for (size_t x = blockIdx.x * 256 + threadIdx.x; x < total; x += static_cast<size_t>(gridDim.x) * 256) {
+        int a, i;
+        if (x < 3 * static_cast<size_t>(M)) {
+            a = static_cast<int>(x / M);
+            i = static_cast<int>(x % M);
+        } else {
+            const size_t y = x - 3 * static_cast<size_t>(M);
+            a = 3 + static_cast<int>(y / NS);
+            i = static_cast<int>(y % NS);
+        }
+        out[x] = src[a][i];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_bp_keepflags(const int *__restrict__ dNS, const int *__restrict__ slot_nn,
                                                       int *__restrict__ kflag, int *__restrict__ ksize)
 {
