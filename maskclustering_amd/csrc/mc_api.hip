@@ -241,10 +241,27 @@ void build_s3_lists(mc_ctx *ctx, const std::vector<int32_t> &frame_start)
         const int sz = ctx->h_off[g + 1] - ctx->h_off[g];
         (wave_ok && sz <= mc::kS3SmallPts ? small : big).push_back(g);
     }
-    // largest masks first: the long waves start early instead of forming the tail
-    auto by_size = [&](int x, int y) { return ctx->h_off[x + 1] - ctx->h_off[x] > ctx->h_off[y + 1] - ctx->h_off[y]; };
-    std::stable_sort(small.begin(), small.end(), by_size);
-    std::stable_sort(big.begin(), big.end(), by_size);
+    // largest masks first: the long waves start early instead of forming the tail (a stable
+    // counting sort by size, descending: std::stable_sort of C3's 81k rows took ~4 ms of host time)
+    auto by_size_desc = [&](std::vector<int> &v) {
+        if (v.size() < 2) return;
+        int mx = 0;
+        for (int g : v) mx = std::max(mx, ctx->h_off[g + 1] - ctx->h_off[g]);
+        if (mx > (1 << 22)) {
+            std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
+                return ctx->h_off[x + 1] - ctx->h_off[x] > ctx->h_off[y + 1] - ctx->h_off[y];
+            });
+            return;
+        }
+        std::vector<int> start(mx + 2, 0);
+        for (int g : v) start[mx - (ctx->h_off[g + 1] - ctx->h_off[g]) + 1]++;
+        for (int i = 1; i <= mx + 1; i++) start[i] += start[i - 1];
+        std::vector<int> out(v.size());
+        for (int g : v) out[start[mx - (ctx->h_off[g + 1] - ctx->h_off[g])]++] = g;
+        v.swap(out);
+    };
+    by_size_desc(small);
+    by_size_desc(big);
     ctx->n_s3_small = static_cast<int>(small.size());
     ctx->n_s3_big = static_cast<int>(big.size());
     ctx->d_s3_small.reserve((small.size() + 1) * sizeof(int));

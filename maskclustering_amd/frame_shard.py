@@ -98,9 +98,20 @@ class FrameShardedScene:
         self.rank = dist.get_rank(group) if on else 0
         self.world = dist.get_world_size(group) if on else 1
         self.lo, self.hi = frame_slice(self.F, self.world, self.rank)
-        self.pts = None  # global point ids (kept alive until the graph input copy is done)
+        self._pts = None  # global point ids (kept alive until the graph input copy is done)
         # the graph stages row-block sharded over the same ranks (shard_graph=False: replicated)
         self.graph = ShardedGraph(run, group) if shard_graph else None
+
+    @property
+    def pts(self) -> torch.Tensor:
+        """The global mask point ids (int32); a single-process run reads them from the context."""
+        if self._pts is None and self.world == 1 and getattr(self, "mask_index", None) is not None:
+            self._pts = torch.from_numpy(np.ascontiguousarray(self.ctx.bp_masks()[3]))
+        return self._pts
+
+    @pts.setter
+    def pts(self, v):
+        self._pts = v
 
     def set_local_masks(self, mask_col, mask_label, mask_off, mask_pts: torch.Tensor):
         """This rank's frames' masks (mask_col relative to the slice) as the S1 output would
@@ -126,6 +137,15 @@ class FrameShardedScene:
             if t.dtype != dt or not t.is_contiguous() or t.device.type != "cuda":
                 raise ValueError("frame inputs must be contiguous device tensors (f32, u8, f64, f64)")
         _, H, W = depth.shape
+        if n and self.world == 1:  # one process: the back-projection result is the graph input as it is
+            self.ctx.backproject(None, None, None, None, params, shape=(n, H, W),
+                                 device_ptrs=(depth.data_ptr(), seg.data_ptr(), intrinsics.data_ptr(),
+                                              poses.data_ptr()))
+            col, lab, off = self.ctx.bp_mask_index()
+            self.mask_index = (col, lab, off)
+            self._pts = None
+            self.ctx.use_backprojection()
+            return col, lab, off
         if n:
             self.ctx.backproject(None, None, None, None, params, shape=(n, H, W),
                                  device_ptrs=(depth.data_ptr(), seg.data_ptr(), intrinsics.data_ptr(),
