@@ -965,6 +965,41 @@ __device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
     a[0] = ins_min(a[0], v);
 }
 
+// ascending sort of 20 values in registers: Batcher's odd-even merge sort of 32 inputs with the
+// comparators that touch inputs 20..31 removed (those would only ever hold +inf), 101 min / max
+// pairs (scripts/gen_sort20.py); the k-NN fills its first 20 candidates this way instead of by
+// 20 sorted inserts (the multiset sorts to the same array by any method)
+__device__ __forceinline__ void bp_ce(double &x, double &y)
+{
+    const double lo = __builtin_fmin(x, y);
+    y = __builtin_fmax(x, y);
+    x = lo;
+}
+__device__ __forceinline__ void sort20(double (&a)[20])
+{
+    bp_ce(a[0], a[1]); bp_ce(a[2], a[3]); bp_ce(a[0], a[2]); bp_ce(a[1], a[3]); bp_ce(a[1], a[2]);
+    bp_ce(a[4], a[5]); bp_ce(a[6], a[7]); bp_ce(a[4], a[6]); bp_ce(a[5], a[7]); bp_ce(a[5], a[6]);
+    bp_ce(a[0], a[4]); bp_ce(a[2], a[6]); bp_ce(a[2], a[4]); bp_ce(a[1], a[5]); bp_ce(a[3], a[7]);
+    bp_ce(a[3], a[5]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]); bp_ce(a[8], a[9]);
+    bp_ce(a[10], a[11]); bp_ce(a[8], a[10]); bp_ce(a[9], a[11]); bp_ce(a[9], a[10]); bp_ce(a[12], a[13]);
+    bp_ce(a[14], a[15]); bp_ce(a[12], a[14]); bp_ce(a[13], a[15]); bp_ce(a[13], a[14]); bp_ce(a[8], a[12]);
+    bp_ce(a[10], a[14]); bp_ce(a[10], a[12]); bp_ce(a[9], a[13]); bp_ce(a[11], a[15]); bp_ce(a[11], a[13]);
+    bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[0], a[8]); bp_ce(a[4], a[12]);
+    bp_ce(a[4], a[8]); bp_ce(a[2], a[10]); bp_ce(a[6], a[14]); bp_ce(a[6], a[10]); bp_ce(a[2], a[4]);
+    bp_ce(a[6], a[8]); bp_ce(a[10], a[12]); bp_ce(a[1], a[9]); bp_ce(a[5], a[13]); bp_ce(a[5], a[9]);
+    bp_ce(a[3], a[11]); bp_ce(a[7], a[15]); bp_ce(a[7], a[11]); bp_ce(a[3], a[5]); bp_ce(a[7], a[9]);
+    bp_ce(a[11], a[13]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]); bp_ce(a[7], a[8]);
+    bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[16], a[17]); bp_ce(a[18], a[19]);
+    bp_ce(a[16], a[18]); bp_ce(a[17], a[19]); bp_ce(a[17], a[18]); bp_ce(a[0], a[16]); bp_ce(a[8], a[16]);
+    bp_ce(a[4], a[8]); bp_ce(a[12], a[16]); bp_ce(a[2], a[18]); bp_ce(a[10], a[18]); bp_ce(a[6], a[10]);
+    bp_ce(a[14], a[18]); bp_ce(a[2], a[4]); bp_ce(a[6], a[8]); bp_ce(a[10], a[12]); bp_ce(a[14], a[16]);
+    bp_ce(a[1], a[17]); bp_ce(a[9], a[17]); bp_ce(a[5], a[9]); bp_ce(a[13], a[17]); bp_ce(a[3], a[19]);
+    bp_ce(a[11], a[19]); bp_ce(a[7], a[11]); bp_ce(a[15], a[19]); bp_ce(a[3], a[5]); bp_ce(a[7], a[9]);
+    bp_ce(a[11], a[13]); bp_ce(a[15], a[17]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]);
+    bp_ce(a[7], a[8]); bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[15], a[16]);
+    bp_ce(a[17], a[18]);
+}
+
 // union-find over a workgroup's LDS parent array (root = smallest index)
 constexpr int kBpLdsUF = 8192;
 // (relaxed workgroup-scope atomic loads / stores: other lanes update the array concurrently, and
@@ -1726,6 +1761,18 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)]); };
                 int k = pm ? __ffsll(static_cast<long long>(pm)) - 1 : 0;
                 double4 nxt = pm ? spt[entry(k)] : make_double4(0.0, 0.0, 0.0, 0.0);
+                if (kk == kBpKnnMax && MC_ABLATE_BP != 3) {
+                    // pm holds >= 20 candidates: the first 20 straight into best, one sort
+#pragma unroll
+                    for (int i = 0; i < kBpKnnMax; i++) {
+                        pm &= pm - 1;
+                        const double4 p = nxt;
+                        if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
+                        const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                        best[i] = ((ex * ex) + (ey * ey)) + (ez * ez);
+                    }
+                    sort20(best);
+                }
                 while (pm) {
                     pm &= pm - 1;
                     const double4 p = nxt;
