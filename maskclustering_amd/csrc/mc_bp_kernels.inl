@@ -1344,6 +1344,39 @@ __device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nbw, 
     for (int k = 0; k < cnt; k++) fn(static_cast<int>((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu));
 }
 
+// nb_list for the DBSCAN union: entry k + 1's neighbour count and union-find parent are loaded
+// before fn(q2, count, parent) runs on entry k's (a parent read early is still a node of q2's
+// component, so it is a valid place to start q2's find)
+template <int N, typename Fn>
+__device__ __forceinline__ void nb_list_uf(const unsigned short *__restrict__ nbw, const int *sflag, int *spar, int q,
+                                           int cnt, Fn &&fn)
+{
+    static_assert(kBpNbCap == 64, "eight uint4 per point");
+    const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
+    unsigned w[32];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
+        w[4 * u] = v.x;
+        w[4 * u + 1] = v.y;
+        w[4 * u + 2] = v.z;
+        w[4 * u + 3] = v.w;
+    }
+    int e = static_cast<int>(w[0] & 0xFFFFu);
+    int nf = cnt > 0 ? sflag[e] : 0, np = cnt > 0 ? ld_wg(spar + e) : 0;
+#pragma unroll 1
+    for (int k = 0; k < cnt; k++) {
+        const int q2 = e, f = nf, p = np;
+        if (k + 1 < cnt) {
+            e = static_cast<int>((w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu);
+            nf = sflag[e];
+            np = ld_wg(spar + e);
+        }
+        fn(q2, f, p);
+    }
+}
+
 // nb_list over the entries' records: the record of entry k + 1 is loaded from LDS before fn runs
 // on entry k's, so the load latency hides behind fn (the k-NN's sorted insert) without a second
 // copy of fn's code
@@ -1418,6 +1451,13 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 // ---------------------------------------------------------------------------------------------
 #ifndef MC_KNN_RING
 #define MC_KNN_RING 1  // 0: points whose eps list holds < k kept points skip the grid rings (whole-cloud scan)
+#endif
+#ifndef MC_UF_PREFETCH
+#define MC_UF_PREFETCH 1  // 0: the union's list walk without the one-ahead count / parent loads
+#endif
+#ifndef MC_SORT20_MIN_N
+#define MC_SORT20_MIN_N 2048  // size classes below this fill the k-NN by sorted inserts only (the
+                               // network's registers spill in the 4- and 2-workgroup-per-CU classes)
 #endif
 #ifndef MC_ABLATE_BP
 #define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union,
@@ -1577,9 +1617,15 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 continue;
             }
             int ra = uf_find_s(spar, q);
+#if MC_UF_PREFETCH
+            nb_list_uf<N>(nbw, sflag, spar, q, cnt, [&](int q2, int f2, int p2) {
+                if (q2 < q && f2 >= pr.minpts && p2 != ra) {  // parent == root: joined already
+                    const int rb = uf_find_s(spar, p2);
+#else
             nb_list<N>(nbw, q, cnt, [&](int q2) {
                 if (q2 < q && sflag[q2] >= pr.minpts) {
                     const int rb = uf_find_s(spar, q2);
+#endif
                     if (rb != ra) {  // most edges of a dense cluster are already joined
                         uf_unite_s(spar, ra, rb);
                         ra = uf_find_s(spar, ra);
@@ -1761,7 +1807,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)]); };
                 int k = pm ? __ffsll(static_cast<long long>(pm)) - 1 : 0;
                 double4 nxt = pm ? spt[entry(k)] : make_double4(0.0, 0.0, 0.0, 0.0);
-                if (kk == kBpKnnMax && MC_ABLATE_BP != 3) {
+                if (kk == kBpKnnMax && MC_ABLATE_BP != 3 && N >= MC_SORT20_MIN_N) {
                     // pm holds >= 20 candidates: the first 20 straight into best, one sort
 #pragma unroll
                     for (int i = 0; i < kBpKnnMax; i++) {
