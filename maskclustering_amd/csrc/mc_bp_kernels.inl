@@ -497,26 +497,33 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
 // A slot whose voxel coordinates span >= 1024 voxels on an axis or that has more than kVxV voxels
 // is listed for the next tier (the larger LDS tables, then k_bp_voxel, the global-hash kernel below).
 // Largest slots first (their per-slot time grows with the pixel count): slots binned by
-// floor(log2(pixels)), bins in descending order.  One workgroup.
+// floor(4 log2(pixels)) (the top three bits of the count), bins in descending order.  One workgroup.
+__device__ __forceinline__ int vox_order_bin(int np)
+{
+    const unsigned x = static_cast<unsigned>(max(np, 1));
+    const int b = 31 - __clz(x);
+    return b < 2 ? b : 4 * b + static_cast<int>((x >> (b - 2)) & 3u) - 6;  // 0 .. 121, monotone in np
+}
 __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ dNS, const int *__restrict__ slot_np,
                                                        int *__restrict__ order)
 {
-    __shared__ int cnt[32];
+    constexpr int NB = 128;
+    __shared__ int cnt[NB];
     const int NS = *dNS, t = threadIdx.x;
-    if (t < 32) cnt[t] = 0;
+    if (t < NB) cnt[t] = 0;
     __syncthreads();
-    for (int s = t; s < NS; s += 1024) atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1);
+    for (int s = t; s < NS; s += 1024) atomicAdd(&cnt[vox_order_bin(slot_np[s])], 1);
     __syncthreads();
     if (t == 0) {
         int o = 0;
-        for (int b = 31; b >= 0; b--) {
+        for (int b = NB - 1; b >= 0; b--) {
             const int c = cnt[b];
             cnt[b] = o;
             o += c;
         }
     }
     __syncthreads();
-    for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[31 - __clz(max(slot_np[s], 1))], 1)] = s;
+    for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[vox_order_bin(slot_np[s])], 1)] = s;
 }
 
 // Workgroup barrier that orders LDS only: this wave's LDS operations complete (lgkmcnt 0), global
@@ -1417,12 +1424,16 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
 // more than kBpLdsN voxels (the global-memory kernel).  min_cls > 0 sends small slots to a larger
 // class (tests: every class gives the same results).  cls_cnt[kBpClasses + 1] must be zero.
 __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
-                                                     int cap, int min_cls, int *__restrict__ cls_cnt,
-                                                     int *__restrict__ cls_list)
+                                                     const int *__restrict__ order, int cap, int min_cls,
+                                                     int *__restrict__ cls_cnt, int *__restrict__ cls_list)
 {
+    // slots taken in k_bp_vox_order's largest-first order, so each class's list (its ticket order)
+    // starts with its largest slots (roughly: the workgroups append concurrently) and the class
+    // ends on small ones instead of a lone large one
     const int NS = *dNS;
-    for (int s = blockIdx.x * 256 + threadIdx.x; s - static_cast<int>(threadIdx.x) < NS; s += gridDim.x * 256) {
-        const bool live = s < NS;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i - static_cast<int>(threadIdx.x) < NS; i += gridDim.x * 256) {
+        const bool live = i < NS;
+        const int s = live ? order[i] : 0;
         const int n = live ? slot_nv[s] : 0;
         const int c = max(min_cls, n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 3072 ? 3 : n <= 4096 ? 4
                                                                                                  : n <= kBpLdsN ? 5 : 6);
