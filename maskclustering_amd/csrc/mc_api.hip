@@ -1962,6 +1962,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             {
                 TimedScope ts(ctx->timer, s, "bp_denoise");
                 const int ncap = static_cast<int>(slots_cap(fb));
+                // largest first again, now by voxel count (the denoise's and the query's cost)
+                hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
+                                   ctx->d_vox_order.as<int>());
                 hipLaunchKernelGGL(mc::k_bp_classify, dim3(64), dim3(256), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
                                    ctx->d_vox_order.as<int>(), ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>());
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
