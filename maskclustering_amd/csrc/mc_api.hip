@@ -1532,7 +1532,10 @@ size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (fram
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
 // Workgroups per resident slot of a denoise class (the classes take slots from tickets): the extra
 // ones start on CUs that other classes free, so no class keeps only its initial share of the chip.
-constexpr int kBpOversub = 2;
+#ifndef MC_BP_OVERSUB
+#define MC_BP_OVERSUB 2
+#endif
+constexpr int kBpOversub = MC_BP_OVERSUB;  // class grids: resident workgroups x this (slots come from tickets)
 // u16 entries of per-workgroup eps-neighbour lists before class cls's region
 inline size_t nbl_offset(const mc_ctx *ctx, int cls)
 {
