@@ -1104,6 +1104,10 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
 {
     return guarded(ctx, [&] {
         MC_REQUIRE(ctx->have_nodes, MC_ERR_STATE, "mc_cluster_run before mc_graph_build / mc_nodes_set");
+        // a sharded level 0 evaluates only this rank's pair rows, so a capture would miss the other
+        // ranks' edges (replay mode is single-process)
+        MC_REQUIRE(!(ctx->cap_edges > 0 && ctx->sh_world > 1), MC_ERR_UNSUPPORTED,
+                   "edge capture (set-order replay) needs an unsharded context (mc_shard_set world 1)");
         hipStream_t s = ctx->stream;
         int *stats = ctx->d_stats.as<int>();
         if (ctx->nodes_from_graph) {
@@ -1907,6 +1911,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         dv.H = H;
         dv.W = W;
         dv.nbands = nbands;
+        // the pixel kernels' uchar4 / float4 loads need aligned frames (a caller's tensor view may start
+        // at any element); every batch starts HW pixels further on, a multiple of 4 when W is
+        dv.vec4 = (W % 4 == 0 && reinterpret_cast<uintptr_t>(dep) % 16 == 0 && reinterpret_cast<uintptr_t>(sg) % 4 == 0)
+                      ? 1 : 0;
 
         int *st = ctx->d_bpstat.as<int>();
         if (!ctx->h_bpstat) MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_bpstat), BS_COUNT * sizeof(int),
@@ -2665,6 +2673,7 @@ int mc_openvoc_query(mc_ctx *ctx, int32_t num_objects, const int64_t *obj_off, c
         MC_REQUIRE(obj_off && out_label && label_features && (num_rows == 0 || features), MC_ERR_INVALID, "null array");
         MC_REQUIRE(obj_off[0] == 0, MC_ERR_INVALID, "obj_off[0] != 0");
         const int64_t nr = obj_off[num_objects];
+        MC_REQUIRE(nr == 0 || obj_rows, MC_ERR_INVALID, "null array");
         for (int k = 0; k < num_objects; k++) MC_REQUIRE(obj_off[k + 1] >= obj_off[k], MC_ERR_INVALID, "obj_off not ascending");
         for (int64_t i = 0; i < nr; i++)
             MC_REQUIRE(obj_rows[i] >= 0 && obj_rows[i] < num_rows, MC_ERR_INVALID, "feature row out of range");

@@ -37,6 +37,7 @@ struct BpDev {
     float r2, scene_inv;
     int minpts, knn, kball, few;
     int H, W, nbands;
+    int vec4;  // W % 4 == 0 with a 16-byte aligned depth and a 4-byte aligned seg pointer: 4 pixels per lane
 };
 
 __device__ __forceinline__ unsigned bp_hash3(int x, int y, int z)
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
     const int sb = band * kBpWaves + wv;  // this wave's sub-band
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int trunc = 0, lastp = -1;
-    if ((W & 3) == 0) {  // four consecutive pixels per lane: one 4-byte seg load and one 16-byte depth load
+    if (pr.vec4) {  // four consecutive pixels per lane: one 4-byte seg load and one 16-byte depth load
       for (int ib0 = i0; ib0 < i1; ib0 += 256 * 2) {
         uchar4 sv[2];
         float4 dq[2];
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
     const int sb = band * kBpWaves + wv;
     const int i0 = min(pr.H, sb * kBpSub) * W, i1 = min(pr.H, (sb + 1) * kBpSub) * W;
     int *mycur = cur[wv];
-    if ((W & 3) == 0) {
+    if (pr.vec4) {
       // four consecutive pixels per lane (lane-major: pixel = 4 * lane + j of the 256-pixel step);
       // per id: each lane counts its matching pixels, a wave exclusive scan of the counts gives
       // the lanes' bases, the leader bumps the cursor by the total

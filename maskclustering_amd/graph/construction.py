@@ -117,8 +117,8 @@ class MaskPointClouds(dict):
     @classmethod
     def from_csr(cls, keys, off, pts):
         m = cls()
-        m._lazy = {k: g for g, k in enumerate(keys)}
-        m._order = list(keys)
+        m._lazy = {k: g for g, k in enumerate(keys)}  # a repeated key maps to its last row
+        m._order = list(dict.fromkeys(keys))          # ... at its first position, as a dict keeps it
         m._off, m._pts = off, pts
         m.csr = (dict(m._lazy), off, pts)
         return m

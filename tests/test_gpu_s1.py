@@ -177,3 +177,28 @@ def test_odd_width_frames_match_oracle(ctx):
     from maskclustering_amd.synthetic_frames import make_frames_shape
     fr = make_frames_shape("tiny", seed=11, H=90, W=122, num_frames=4)
     _check_against_oracle(ctx, fr)
+
+
+def test_misaligned_device_frames_match_aligned(ctx):
+    """Device frames handed over at odd element offsets (a caller's tensor view): the pixel kernels'
+    four-pixel vector loads need 16-byte depth / 4-byte seg alignment, so such frames take the
+    one-pixel-per-lane path and give the same masks."""
+    import torch
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("tiny", seed=5, H=120, W=160, num_frames=3)
+    want = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    dev = torch.device("cuda", 0)
+    n = fr.depth.size
+    dbuf = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+    sbuf = torch.zeros(n + 1, dtype=torch.uint8, device=dev)
+    dbuf[1:] = torch.from_numpy(np.ascontiguousarray(fr.depth).reshape(-1)).to(dev)
+    sbuf[1:] = torch.from_numpy(np.ascontiguousarray(fr.seg).reshape(-1)).to(dev)
+    K = torch.from_numpy(np.ascontiguousarray(fr.intrinsics, np.float64)).to(dev)
+    T = torch.from_numpy(np.ascontiguousarray(fr.poses, np.float64).reshape(-1, 16)).to(dev)
+    d1, s1 = dbuf[1:], sbuf[1:]
+    assert d1.data_ptr() % 16 != 0 and s1.data_ptr() % 4 != 0
+    ctx.backproject(None, None, None, None, shape=fr.depth.shape,
+                    device_ptrs=(d1.data_ptr(), s1.data_ptr(), K.data_ptr(), T.data_ptr()))
+    torch.cuda.synchronize()
+    for x, y in zip(want, ctx.bp_masks()):
+        np.testing.assert_array_equal(x, y)

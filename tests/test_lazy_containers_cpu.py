@@ -33,6 +33,33 @@ def test_reads_match_plain_dict():
         lazy["nope"]
 
 
+def test_repeated_frame_id_keeps_first_position_and_last_set():
+    """a frame id listed twice (construction.py:57 assigns the key twice: first position, last set)"""
+    import pickle
+    rng = np.random.default_rng(4)
+    keys = ["0_1", "0_2", "10_1", "0_1", "20_3", "10_1"]
+    rows = [np.unique(rng.integers(0, 100, 12)).astype(np.int32) for _ in keys]
+    off = np.zeros(len(keys) + 1, np.int64)
+    np.cumsum([len(r) for r in rows], out=off[1:])
+    plain = {}
+    for k, r in zip(keys, rows):
+        plain[k] = set(r.tolist())
+    lazy = MaskPointClouds.from_csr(keys, off, np.concatenate(rows))
+    assert len(lazy) == len(plain) == 4
+    assert lazy["0_1"] == plain["0_1"]
+    assert list(lazy) == list(plain) and list(lazy.items()) == list(plain.items())
+    assert pickle.loads(pickle.dumps(lazy)) == plain
+    lazy2 = MaskPointClouds.from_csr(keys, off, np.concatenate(rows))
+    np.save("/dev/null", np.array([lazy2], dtype=object), allow_pickle=True)
+    lazy2["new"] = {1}
+    plain2 = dict(plain)
+    plain2["new"] = {1}
+    assert list(lazy2) == list(plain2) and lazy2 == plain2
+    del lazy2["10_1"]
+    del plain2["10_1"]
+    assert list(lazy2.values()) == list(plain2.values())
+
+
 def test_mutation_drops_csr_and_keeps_order():
     keys, plain, lazy = _plain_and_lazy(1)
     assert lazy.csr is not None
