@@ -79,7 +79,13 @@ _EDGE_CAP0 = 1 << 22
 
 def _replay(nodes, T, sizes, edges, parts):
     """The reference's container building, level by level (see the module docstring).  Returns
-    [(mask_list, point_ids, son_node_info)] of the final nodes, in component order."""
+    [(mask_list, point_ids, son_node_info)] of the final nodes, in component order.
+
+    The component walk is networkx 3.x's ``_plain_bfs`` (list-valued levels, ``seen`` a set filled
+    in discovery order; networkx 3.4.2 made the pinning golden, tests/golden/e2e_pp_small.meta.json).
+    networkx 2.x fills the component from set-valued levels, so CPython's set iteration order and
+    with it ``Node.mask_list`` / ``point_ids`` order differ: the replay reproduces a reference run
+    on networkx >= 3.0 only (the sets themselves are version-independent)."""
     level = [(n.mask_list, n.point_ids, n.node_info) for n in nodes]
     tt, aa, bb = edges
     bounds = np.searchsorted(tt, np.arange(T + 1))

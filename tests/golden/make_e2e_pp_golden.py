@@ -72,6 +72,12 @@ def main():
         np.savez_compressed(path, **out)
         print(f"{cfg}: nodes={len(objects)} exported objects={len(got['pts'])} "
               f"points={len(oi)} -> {path} {os.path.getsize(path) / 1e3:.1f} kB")
+    import json
+    import networkx
+    with open(os.path.join(HERE, "e2e_pp_small.meta.json"), "w") as f:  # the replay's set orders are networkx 3.x's
+        json.dump({"generated_with": {"networkx": networkx.__version__, "numpy": np.__version__},
+                   "note": "e2e_pp_small_*.npz: the reference main path run by make_e2e_pp_golden.py; the set-order "
+                           "replay reproduces networkx>=3 _plain_bfs orders"}, f, indent=1)
 
 
 if __name__ == "__main__":

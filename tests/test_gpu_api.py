@@ -106,6 +106,10 @@ def test_dropin_frame_backprojection_matches_reference():
 
 
 def _pp_golden(cfg):
+    import json
+    meta = json.load(open(os.path.join(GOLDEN, "e2e_pp_small.meta.json")))
+    # the replay restates networkx 3.x's _plain_bfs set orders (iterative_clustering._replay)
+    assert meta["generated_with"]["networkx"].split(".")[0] == "3", meta
     return np.load(os.path.join(GOLDEN, f"e2e_pp_small_{cfg}.npz"))
 
 
