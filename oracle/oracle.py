@@ -90,16 +90,60 @@ def s1_frame(scene_f32, depth, seg, K, pose, params: BpParams | None = None):
     return labels[:n].copy(), off[:n + 1].copy(), pts[:off[n]].copy(), stats[:ncand.value].copy()
 
 
-def s1_scene(frames, params: BpParams | None = None, timings: dict | None = None):
+def s1_frames(scene_f32, depth, seg, K, poses, params: BpParams | None = None, threads: int | None = None):
+    """s1_frame for many frames at once, OpenMP over frames (orc_s1_batch; frames are independent,
+    utils/mask_backprojection.py:154-156).  depth / seg: sequences of [H,W] arrays (or [F,H,W]).
+    Returns [(labels, off, pts, stats)] per frame, as s1_frame; IndexError for a DEPTH_TRUNC frame."""
+    L = lib()
+    prm = params or BpParams.default()
+    scene = np.ascontiguousarray(scene_f32, np.float32).reshape(-1, 3)
+    dl = [np.ascontiguousarray(d, np.float32) for d in depth]
+    sl = [np.ascontiguousarray(x, np.uint8) for x in seg]
+    F = len(dl)
+    if F == 0:
+        return []
+    H, W = dl[0].shape
+    assert all(d.shape == (H, W) and x.shape == (H, W) for d, x in zip(dl, sl))
+    Kf = np.ascontiguousarray(K, np.float64).reshape(F, 4)
+    Tf = np.ascontiguousarray(poses, np.float64).reshape(F, 16)
+    dp = (ctypes.c_void_p * F)(*[d.ctypes.data for d in dl])
+    sp = (ctypes.c_void_p * F)(*[x.ctypes.data for x in sl])
+    n = np.zeros(F, np.int32)
+    labels = np.zeros((F, 256), np.int32)
+    off = np.zeros((F, 257), np.int64)
+    stats = np.zeros((F, 256, len(S1_STATS)), np.int32)
+    ncand = np.zeros(F, np.int32)
+    total = ctypes.c_int64()
+    h = L.orc_s1_batch(len(scene), scene.reshape(-1), F, H, W, dp, sp, Kf, Tf, ctypes.byref(prm),
+                       int(threads or default_threads()), n, labels, off, stats, ncand, ctypes.byref(total))
+    pts = np.zeros(max(int(total.value), 1), np.int32)
+    L.orc_s1_batch_take(h, pts)
+    out, o = [], 0
+    for f in range(F):
+        if n[f] == -1:
+            raise IndexError(f"frame {f}: depth pixel equal to DEPTH_TRUNC (utils/mask_backprojection.py:100)")
+        k = int(n[f])
+        np_f = int(off[f, k])
+        out.append((labels[f, :k].copy(), off[f, :k + 1].copy(), pts[o:o + np_f].copy(), stats[f, :ncand[f]].copy()))
+        o += np_f
+    return out
+
+
+def default_threads() -> int:
+    """host threads for the oracle: OMP_NUM_THREADS when set (16 per GPU on the box), else all cores"""
+    return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+
+def s1_scene(frames, params: BpParams | None = None, timings: dict | None = None, threads: int | None = None):
     """All frames of a SceneFrames (maskclustering_amd.synthetic_frames) ->
     the flat mask CSR the graph stages consume (mask_col, mask_label, mask_off,
     mask_pts) plus the per-candidate stats with the frame column prepended."""
     scene = np.asarray(frames.scene_points, np.float64).astype(np.float32)  # construction.py:37
     cols, labs, offs, chunks, stats = [], [], [0], [], []
     t0 = time.perf_counter()
+    res = s1_frames(scene, frames.depth, frames.seg, frames.intrinsics, frames.poses, params, threads)
     for f in range(frames.num_frames):
-        lab, off, pts, st = s1_frame(scene, frames.depth[f], frames.seg[f], frames.intrinsics[f], frames.poses[f],
-                                     params)
+        lab, off, pts, st = res[f]
         for k in range(len(lab)):
             cols.append(f)
             labs.append(int(lab[k]))
@@ -153,6 +197,12 @@ def lib():
         L.orcs_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _i64p, _i32p, ctypes.c_int, _f32p,
                                    ctypes.c_double, _i32p, _i32p, _i32p, _i64p, _u64p, _i64p, _i32p]
         _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        L.orc_s1_batch.restype = ctypes.c_void_p
+        L.orc_s1_batch.argtypes = [ctypes.c_int64, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_void_p, _f64p, _f64p, ctypes.POINTER(BpParams), ctypes.c_int, _i32p, _i32p,
+                                   _i64p, _i32p, _i32p, ctypes.POINTER(ctypes.c_int64)]
+        L.orc_s1_batch_take.restype = None
+        L.orc_s1_batch_take.argtypes = [ctypes.c_void_p, _i32p]
         L.orc_s1_frame.restype = ctypes.c_int
         L.orc_s1_frame.argtypes = [ctypes.c_int64, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _u8p, _f64p, _f64p,
                                    ctypes.POINTER(BpParams), _i32p, _i64p, _i32p, ctypes.c_int64,

@@ -72,15 +72,12 @@ static void world_point(const double *K, const double *T, int u, int v, float d,
     for (int k = 0; k < 3; k++) out[k] = r[k] / r[3];
 }
 
-static double d2_f64(const double *a, const double *b)
+/* built with -ffp-contract=off and without -ffast-math on x86-64 (SSE2 doubles), so this is
+ * evaluated exactly as written: three rounded products, two rounded sums, in this order */
+static inline double d2_f64(const double *a, const double *b)
 {
-    volatile double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
-    volatile double s = dx * dx;
-    volatile double t = dy * dy;
-    s = s + t;
-    t = dz * dz;
-    s = s + t;
-    return s;
+    const double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
+    return ((dx * dx) + (dy * dy)) + (dz * dz);
 }
 
 /* ---- (a3) voxel_down_sample (:105), first-occurrence order (u2) ---------- */
@@ -133,16 +130,20 @@ static void dbscan(const double *p, int n, double eps, int minpts, int32_t *labe
 {
     const double e2 = eps * eps;
     int32_t *nbo = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
-    int64_t tot = 0;
+    int64_t tot = 0, ncap = 16 * (int64_t)n + 16;
+    int32_t *nb = (int32_t *)malloc((size_t)ncap * sizeof(int32_t));
     nbo[0] = 0;
-    for (int i = 0; i < n; i++) {
-        for (int j = 0; j < n; j++) tot += d2_f64(p + 3 * i, p + 3 * j) < e2;
+    for (int i = 0; i < n; i++) {  /* every point's eps-neighbours (self included), ascending index */
+        for (int j = 0; j < n; j++)
+            if (d2_f64(p + 3 * i, p + 3 * j) < e2) {
+                if (tot == ncap) {
+                    ncap *= 2;
+                    nb = (int32_t *)realloc(nb, (size_t)ncap * sizeof(int32_t));
+                }
+                nb[tot++] = j;
+            }
         nbo[i + 1] = (int32_t)tot;
     }
-    int32_t *nb = (int32_t *)malloc((size_t)(tot + 1) * sizeof(int32_t));
-    for (int i = 0, k = 0; i < n; i++)
-        for (int j = 0; j < n; j++)
-            if (d2_f64(p + 3 * i, p + 3 * j) < e2) nb[k++] = j;
     uint8_t *queued = (uint8_t *)calloc((size_t)n + 1, 1);
     int32_t *queue = (int32_t *)malloc((size_t)(n + 1) * sizeof(int32_t));
     for (int i = 0; i < n; i++) labels[i] = -2;
@@ -173,12 +174,6 @@ static void dbscan(const double *p, int n, double eps, int minpts, int32_t *labe
     free(nbo); free(nb); free(queued); free(queue);
 }
 
-static int cmp_f64(const void *a, const void *b)
-{
-    const double x = *(const double *)a, y = *(const double *)b;
-    return x < y ? -1 : (x > y ? 1 : 0);
-}
-
 /* remove_statistical_outlier(nb_neighbors, std_ratio) on the points idx[0..m):
  * keep[i] for i < m.  Returns the number kept. */
 static int statistical_outlier(const double *p, const int32_t *idx, int m, int k, double std_ratio, uint8_t *keep)
@@ -186,10 +181,20 @@ static int statistical_outlier(const double *p, const int32_t *idx, int m, int k
     if (m == 0) return 0;
     const int kk = k < m ? k : m;                     /* nanoflann returns min(k, n) */
     double *avg = (double *)malloc((size_t)m * sizeof(double));
-    double *d = (double *)malloc((size_t)m * sizeof(double));
+    double *d = (double *)malloc((size_t)(kk + 1) * sizeof(double));
     for (int i = 0; i < m; i++) {
-        for (int j = 0; j < m; j++) d[j] = d2_f64(p + 3 * idx[i], p + 3 * idx[j]);
-        qsort(d, (size_t)m, sizeof(double), cmp_f64);
+        /* the kk smallest squared distances in ascending order (the head of the sorted list) */
+        int nd = 0;
+        for (int j = 0; j < m; j++) {
+            const double v = d2_f64(p + 3 * idx[i], p + 3 * idx[j]);
+            if (nd == kk && !(v < d[kk - 1])) continue;
+            int q = nd < kk ? nd++ : kk - 1;
+            while (q > 0 && v < d[q - 1]) {
+                d[q] = d[q - 1];
+                q--;
+            }
+            d[q] = v;
+        }
         volatile double s = 0.0;
         for (int j = 0; j < kk; j++) s = s + sqrt(d[j]);  /* std::accumulate of sqrt'ed, ascending */
         avg[i] = s / (double)kk;
@@ -231,9 +236,10 @@ static int cmp_i32(const void *a, const void *b)
  * Returns n >= 0; -1 if a depth pixel equals depth_trunc while the image has a
  * nonzero id (the reference's IndexError at :100); -2 if cap is too
  * small (*need = required). */
-int orc_s1_frame(int64_t P, const float *scene, int H, int W, const float *depth, const uint8_t *seg,
-                 const double *K, const double *T, const orc_bp_params *prm, int32_t *labels, int64_t *off,
-                 int32_t *pts, int64_t cap, int64_t *need, int32_t *stats, int32_t *n_cand)
+/* the frame's work; the neighbour ids go to a growable buffer *pb of *pcap entries */
+static int s1_frame_core(int64_t P, const float *scene, int H, int W, const float *depth, const uint8_t *seg,
+                         const double *K, const double *T, const orc_bp_params *prm, int32_t *labels, int64_t *off,
+                         int32_t **pb, int64_t *pcap, int64_t *need, int32_t *stats, int32_t *n_cand)
 {
     *need = 0;
     *n_cand = 0;
@@ -258,7 +264,7 @@ int orc_s1_frame(int64_t P, const float *scene, int H, int W, const float *depth
     uint8_t *keep = (uint8_t *)malloc((size_t)H * W);
     float *q = (float *)malloc((size_t)H * W * 3 * sizeof(float));
     int32_t *cand = (int32_t *)malloc((size_t)(P + 1) * sizeof(int32_t));
-    int32_t *nbr = NULL;
+    int32_t *nbr = NULL;  /* the ball query's accepted ids (then the frame's unique set) */
     int64_t nbr_cap = 0;
     int32_t *cnt = NULL;
     int ncnt_cap = 0;
@@ -358,7 +364,11 @@ int orc_s1_frame(int64_t P, const float *scene, int H, int W, const float *depth
             if (u == 0 || nbr[i] != nbr[u - 1]) nbr[u++] = nbr[i];
         st[ST_NNBR] = (int32_t)u;
         st[ST_KEPT] = 1;
-        if (np + u <= cap) memcpy(pts + np, nbr, (size_t)u * sizeof(int32_t));
+        if (np + u > *pcap) {
+            while (np + u > *pcap) *pcap = 2 * *pcap + 1024;
+            *pb = (int32_t *)realloc(*pb, (size_t)*pcap * sizeof(int32_t));
+        }
+        memcpy(*pb + np, nbr, (size_t)u * sizeof(int32_t));
         np += u;
         labels[n] = id;
         off[n + 1] = np;
@@ -366,6 +376,70 @@ int orc_s1_frame(int64_t P, const float *scene, int H, int W, const float *depth
     }
     free(mp); free(vp); free(lab); free(sidx); free(keep); free(q); free(cand); free(nbr); free(cnt);
     *need = np;
-    if (np > cap) return -2;
     return n;
+}
+
+int orc_s1_frame(int64_t P, const float *scene, int H, int W, const float *depth, const uint8_t *seg,
+                 const double *K, const double *T, const orc_bp_params *prm, int32_t *labels, int64_t *off,
+                 int32_t *pts, int64_t cap, int64_t *need, int32_t *stats, int32_t *n_cand)
+{
+    int64_t bcap = 1 << 16;
+    int32_t *buf = (int32_t *)malloc((size_t)bcap * sizeof(int32_t));
+    const int n = s1_frame_core(P, scene, H, W, depth, seg, K, T, prm, labels, off, &buf, &bcap, need, stats, n_cand);
+    if (n >= 0 && *need <= cap) memcpy(pts, buf, (size_t)*need * sizeof(int32_t));
+    free(buf);
+    if (n >= 0 && *need > cap) return -2;
+    return n;
+}
+
+/* ---- many frames, OpenMP over frames (frames are independent, mask_backprojection.py:154-156;
+ * the reference runs them one after another, construction.py:44-49) -------------------------
+ * depth[f] / seg[f]: frame f's [H,W] arrays; K [F,4], T [F,16].  Per frame f: n_out[f] kept masks
+ * (-1: the DEPTH_TRUNC error of :100), labels[256 f ..], off[257 f ..] (relative to the frame's
+ * first id), stats[256 ST_NSTAT f ..], n_cand[f].  Returns a handle; *total = the frames' neighbour
+ * ids, which orc_s1_batch_take copies out (frames in order) before freeing the handle. */
+typedef struct {
+    int F;
+    int32_t **pts;
+    int64_t *np;
+} orc_s1_batch_t;
+
+void *orc_s1_batch(int64_t P, const float *scene, int F, int H, int W, const float *const *depth,
+                   const uint8_t *const *seg, const double *K, const double *T, const orc_bp_params *prm,
+                   int nthreads, int32_t *n_out, int32_t *labels, int64_t *off, int32_t *stats, int32_t *n_cand,
+                   int64_t *total)
+{
+    orc_s1_batch_t *h = (orc_s1_batch_t *)calloc(1, sizeof(orc_s1_batch_t));
+    h->F = F;
+    h->pts = (int32_t **)calloc((size_t)F + 1, sizeof(int32_t *));
+    h->np = (int64_t *)calloc((size_t)F + 1, sizeof(int64_t));
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int f = 0; f < F; f++) {
+        int64_t bcap = 1 << 16, need = 0;
+        int32_t *buf = (int32_t *)malloc((size_t)bcap * sizeof(int32_t));
+        const int n = s1_frame_core(P, scene, H, W, depth[f], seg[f], K + 4 * (size_t)f, T + 16 * (size_t)f, prm,
+                                    labels + 256 * (size_t)f, off + 257 * (size_t)f, &buf, &bcap, &need,
+                                    stats + (size_t)256 * ST_NSTAT * f, n_cand + f);
+        n_out[f] = n;
+        h->pts[f] = buf;
+        h->np[f] = n >= 0 ? need : 0;
+    }
+    int64_t t = 0;
+    for (int f = 0; f < F; f++) t += h->np[f];
+    *total = t;
+    return h;
+}
+
+void orc_s1_batch_take(void *hp, int32_t *pts)
+{
+    orc_s1_batch_t *h = (orc_s1_batch_t *)hp;
+    int64_t o = 0;
+    for (int f = 0; f < h->F; f++) {
+        if (pts && h->np[f]) memcpy(pts + o, h->pts[f], (size_t)h->np[f] * sizeof(int32_t));
+        o += h->np[f];
+        free(h->pts[f]);
+    }
+    free(h->pts);
+    free(h->np);
+    free(h);
 }
