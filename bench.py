@@ -1,28 +1,25 @@
 """Benchmark of the view-consensus graph path on MI355X.
 
-A step = one pass of the hot path over one synthetic ScanNet-shaped scene
-(BASELINE.json configs[1]: ~250 frames, ~240k points, ~15k masks).
+A step = one pass of the hot path over one synthetic scene.  Default: the ScanNet++-shaped C3 scene
+(BASELINE.json configs[2]: 1500 frames 1920x1440, ~1M points, ~80k masks), end to end:
 
-  --variant g   (default) graph construction S2-S5 (point lists, boundary,
-                containment, under-segmentation, observer thresholds),
-                iterative clustering S6 (all thresholds) and the final
-                per-object point sets, from per-frame mask sets resident in
-                HBM to final components + merged bitsets in HBM;
-  --variant e2e the same preceded by S1 back-projection of every frame from
-                depth / segmentation / poses resident in HBM (640x480 frames);
-  --variant pp  the post-processing row (utils/post_process.py:173-194): the
-                drop-in post_process over the scene's clustered objects
-                (own JSON line: ms per scene, per-kernel device times).
+  --variant e2e (default) S1 back-projection of every frame from depth / segmentation / poses
+                resident in HBM, then graph construction S2-S5 and iterative clustering S6 to the
+                final per-object point sets;
+  --variant g   S2-S6 only, from per-frame mask sets resident in HBM;
+  --variant pp / api / sweep: the post-processing row, the reference-API call sequence of
+                main.py:17-21, and the 312-scene sweep (BASELINE configs[4]), each its own line.
 
-metric: mask-pair consensus counts/sec = Σ_t N_t² (the ordered node pairs whose
-view consensus the reference evaluates, graph/iterative_clustering.py:20-29)
-summed over the scenes of all ranks ÷ max-over-ranks wall time of the steps.
-ms_per_step is the per-scene graph build + cluster time (BASELINE.json's
-first metric).  Multi-GPU: one process per GPU, each rank its own scene
-(scene-parallel, the reference's run.py:33-50 pattern): weak scaling, no
-data-path collective.
+metric: mask-pair consensus counts/sec = Σ_t N_t² (the ordered node pairs whose view consensus
+the reference evaluates, graph/iterative_clustering.py:20-29) per scene × scenes ÷ max-over-ranks
+wall time; ms_per_step is the per-scene graph build + cluster time (BASELINE.json's first metric).
+Multi-GPU (--shard frames, default): one scene per step, its frames split over the ranks (strong
+scaling); --shard scene: every rank its own scene (weak scaling, run.py:33-50).
+At N=1 the line also carries `secondary`: the ScanNet-sized C2 scene (configs[1]) timed E2E and G
+in the same process, with the host ports beside it (c2_record).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant g|e2e|pp] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--variant e2e|g|pp|api|sweep] [--shape S]
+                    [--no-cpu-baseline] [--no-secondary]
 """
 from __future__ import annotations
 
@@ -145,6 +142,52 @@ def bp_work(ctx, F, H, W):
     }
 
 
+def s1_cpu_rate(scene_f32, frame_at, F, n_all=64, n_one=8):
+    """Seconds per frame of the S1 port (oracle/s1_oracle.c) on the host: all threads (OpenMP over
+    frames) on n_all frames spread evenly over the scene, and one thread on n_one of those frames.
+    frame_at(i) -> (depth [H,W] f32, seg [H,W] u8, K [4], pose [4,4]) host arrays."""
+    from oracle import oracle
+    idx = np.unique(np.linspace(0, F - 1, min(n_all, F)).round().astype(np.int64))
+    fr = [frame_at(int(i)) for i in idx]
+    thr = oracle.default_threads()
+
+    def timed(sel, threads):
+        t0 = time.perf_counter()
+        oracle.s1_frames(scene_f32, [fr[k][0] for k in sel], [fr[k][1] for k in sel],
+                         np.stack([fr[k][2] for k in sel]), np.stack([fr[k][3] for k in sel]), threads=threads)
+        return (time.perf_counter() - t0) / len(sel)
+
+    one = list(range(0, len(idx), max(1, len(idx) // n_one)))[:n_one]
+    return dict(all=timed(range(len(idx)), thr), one=timed(one, 1), threads=thr, n_all=len(idx), n_one=len(one),
+                frames=F)
+
+
+def graph_cpu(P, F, col, lab, off, pts, threads, dense=False):
+    """the S2-S6 port on `threads` host threads: (seconds, timings)"""
+    from oracle import oracle
+    tm = {}
+    with oracle.threads(threads):
+        (oracle.run if dense else oracle.run_sparse)(P, F, col, lab, off, pts, timings=tm, **CFG)
+    return tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"], tm
+
+
+def e2e_cpu_baseline(s1, P, F, col, lab, off, pts):
+    """cpu_baseline of the E2E variants: S1 port (per-frame rates of s1_cpu_rate x F frames) + the
+    S2-S6 port on the full mask set, on all host threads (value) and on one (single_thread)."""
+    g_all, tm = graph_cpu(P, F, col, lab, off, pts, s1["threads"])
+    g_one, _ = graph_cpu(P, F, col, lab, off, pts, 1)
+    all_s, one_s = s1["all"] * F + g_all, s1["one"] * F + g_one
+    pairs = tm["pairs"]
+    return {"value": round(pairs / all_s, 1), "unit": "mask-pairs/s", "cores": s1["threads"], "kind": "port",
+            "sample": f"S1 port (oracle/s1_oracle.c, OpenMP over frames, {s1['threads']} threads) timed on "
+                      f"{s1['n_all']} frames spread over the {F} and scaled to {F} ({s1['all'] * F:.1f} s) + the "
+                      f"S2-S6 port (oracle/graph_sparse.c, {s1['threads']} threads) on the full scene ({g_all:.2f} s)",
+            "scene_ms": round(all_s * 1e3, 1),
+            "single_thread": {"value": round(pairs / one_s, 1), "cores": 1, "scene_ms": round(one_s * 1e3, 1),
+                              "sample": f"S1 port on 1 thread, {s1['n_one']} of those frames ({s1['one'] * F:.1f} s "
+                                        f"scaled) + the S2-S6 port on 1 thread ({g_one:.2f} s)"}}
+
+
 class GraphStep:
     """--variant g: per-frame mask sets resident in HBM -> final objects."""
 
@@ -171,15 +214,17 @@ class GraphStep:
     def cpu_baseline(self):
         from oracle import oracle
         s = self.scene
-        tm = {}
-        run = oracle.run if s.num_masks <= 30000 else oracle.run_sparse  # dense matrices beyond C2 do not fit
-        run(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, timings=tm, **CFG)
-        cpu_s = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
-        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
-                "sample": f"{'oracle/mcgraph_oracle.c' if run is oracle.run else 'oracle/graph_sparse.c'} S2-S6 on "
-                          f"the same scene (1 full scene, {cpu_s:.2f} s: "
+        dense = s.num_masks <= 30000  # dense matrices beyond C2 do not fit
+        thr = oracle.default_threads()
+        cpu_s, tm = graph_cpu(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, thr, dense)
+        one_s, _ = graph_cpu(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, 1, dense)
+        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": thr, "kind": "port",
+                "sample": f"{'oracle/mcgraph_oracle.c' if dense else 'oracle/graph_sparse.c'} S2-S6 on "
+                          f"the same scene (1 full scene, {thr} threads, {cpu_s:.2f} s: "
                           f"S2 {tm['s2']:.2f} S3 {tm['s3']:.2f} S4 {tm['s4']:.2f} S6 {tm['s6']:.2f})",
-                "scene_ms": round(cpu_s * 1e3, 1)}
+                "scene_ms": round(cpu_s * 1e3, 1),
+                "single_thread": {"value": round(tm["pairs"] / one_s, 1), "cores": 1, "scene_ms": round(one_s * 1e3, 1),
+                                  "sample": "the same port and scene on 1 thread"}}
 
 
 class EndToEndStep:
@@ -226,27 +271,15 @@ class EndToEndStep:
         w.update(bp_work(self.ctx, F, H, W))
         return w
 
-    def cpu_baseline(self, budget_s=12.0):
-        """oracle S1 on the first frames (bounded sample, extrapolated per frame) + oracle S2-S6
-        on the full mask set (identical to the device's by the parity tests)."""
-        from oracle import oracle
+    def cpu_baseline(self):
+        """the S1 port on a sample of frames spread over the scene (all threads and one thread,
+        scaled per frame) + the S2-S6 port on the full mask set (identical to the device's by the
+        parity tests, tests/test_gpu_bench_configs.py)."""
         fr = self.fr
-        scene = fr.scene_points.astype(np.float32)
-        t0 = time.perf_counter()
-        k = 0
-        while k < fr.num_frames and time.perf_counter() - t0 < budget_s:
-            oracle.s1_frame(scene, fr.depth[k].cpu().numpy(), fr.seg[k].cpu().numpy(), fr.intrinsics[k], fr.poses[k])
-            k += 1
-        s1 = (time.perf_counter() - t0) / k * fr.num_frames
+        at = lambda i: (fr.depth[i].cpu().numpy(), fr.seg[i].cpu().numpy(), fr.intrinsics[i], fr.poses[i])  # noqa: E731
+        s1 = s1_cpu_rate(fr.scene_points.astype(np.float32), at, fr.num_frames)
         col, lab, off, pts = self.ctx.bp_masks()
-        tm = {}
-        oracle.run_sparse(fr.num_points, fr.num_frames, col, lab, off, pts, timings=tm, **CFG)
-        g = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
-        cpu_s = s1 + g
-        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
-                "sample": f"oracle S1 (oracle/s1_oracle.c, 1 thread) timed on {k} of {fr.num_frames} frames and "
-                          f"extrapolated ({s1:.1f} s) + oracle S2-S6 on the full scene ({g:.2f} s)",
-                "scene_ms": round(cpu_s * 1e3, 1)}
+        return e2e_cpu_baseline(s1, fr.num_points, fr.num_frames, col, lab, off, pts)
 
 
 class ShardedGraphStep(GraphStep):
@@ -337,29 +370,82 @@ class ShardedEndToEndStep(EndToEndStep):
         w.update(bp_work(self.ctx, F, H, W))
         return w
 
-    def cpu_baseline(self, budget_s=12.0):
-        """oracle S1 on the first frames (bounded sample, extrapolated per frame) + the sparse
-        oracle's S2-S6 on the full mask set (identical to the device's by the parity tests)."""
-        from oracle import oracle
+    def cpu_baseline(self):
+        """as EndToEndStep.cpu_baseline (rank 0 at N=1 holds every frame)"""
         fr = self.fr
-        scene = fr.scene_points.astype(np.float32)
-        t0 = time.perf_counter()
-        k = 0
-        while k < len(fr.depth) and time.perf_counter() - t0 < budget_s:
-            oracle.s1_frame(scene, fr.depth[k].cpu().numpy(), fr.seg[k].cpu().numpy(), fr.intrinsics[k], fr.poses[k])
-            k += 1
-        s1 = (time.perf_counter() - t0) / k * self.F_total
+        at = lambda i: (fr.depth[i].cpu().numpy(), fr.seg[i].cpu().numpy(), fr.intrinsics[i], fr.poses[i])  # noqa: E731
+        s1 = s1_cpu_rate(fr.scene_points.astype(np.float32), at, len(fr.depth))
         col, lab, off = self.sh.mask_index
-        pts = self.sh.pts.cpu().numpy()
-        tm = {}
-        oracle.run_sparse(fr.num_points, self.F_total, col, lab, off, pts, timings=tm, **CFG)
-        g = tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"]
-        cpu_s = s1 + g
-        return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": tm["threads"], "kind": "port",
-                "sample": f"oracle S1 (oracle/s1_oracle.c, 1 thread) timed on {k} of {self.F_total} frames and "
-                          f"extrapolated ({s1:.1f} s) + the sparse oracle's S2-S6 (oracle/graph_sparse.c, "
-                          f"{tm['threads']} threads) on the full scene ({g:.2f} s)",
-                "scene_ms": round(cpu_s * 1e3, 1)}
+        return e2e_cpu_baseline(s1, fr.num_points, self.F_total, col, lab, off, self.sh.pts.cpu().numpy())
+
+
+def c2_record(local, steps, warmup):
+    """The ScanNet-sized scene (BASELINE configs[1], the north_star's "ScanNet-sized scene on 1 MI355X")
+    timed in the same process with the same discipline as the main line (warmup steps, then `steps`
+    steps between two device synchronisations): C2 E2E (S1-S6 from RGB-D frames resident in HBM) and
+    C2 G (S2-S6 from per-frame mask sets resident in HBM).  Beside them the ports on the host: S1 on
+    every frame of the scene with all threads (no sampling) + S2-S6, and one thread (S1 on 16 frames
+    spread over the scene, scaled); the S1 port's output is compared with the device's (bit_exact)."""
+    import torch
+    from oracle import oracle
+    rec = {}
+    e2e = EndToEndStep("c2", 0, local)
+    g = GraphStep("c2", 0, local)
+    for name, r in (("c2_e2e", e2e), ("c2_g", g)):
+        for _ in range(max(warmup, 1)):
+            r.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        ctx = r.run.ctx
+        ci = ctx.cluster_info()
+        pairs = int(np.sum(ctx.level_sizes(ci.num_iterations)[:-1].astype(np.int64) ** 2))
+        rec[name] = {"scene_ms": round(dt * 1e3, 4), "value": round(pairs / dt, 1), "unit": "mask-pairs/s",
+                     "workload": r.workload + f" M={ctx.graph_info().num_masks}", "pairs_per_scene": pairs}
+    fr = e2e.fr
+    F, P = fr.num_frames, fr.num_points
+    scene = fr.scene_points.astype(np.float32)
+    depth, seg = fr.depth.cpu().numpy(), fr.seg.cpu().numpy()
+    thr = oracle.default_threads()
+    t0 = time.perf_counter()
+    res = oracle.s1_frames(scene, depth, seg, fr.intrinsics, fr.poses, threads=thr)
+    s1_all = time.perf_counter() - t0
+    one = np.unique(np.linspace(0, F - 1, 16).round().astype(np.int64))
+    t0 = time.perf_counter()
+    oracle.s1_frames(scene, depth[one], seg[one], fr.intrinsics[one], fr.poses[one], threads=1)
+    s1_one = (time.perf_counter() - t0) / len(one) * F
+    col = np.concatenate([np.full(len(r[0]), c, np.int32) for c, r in enumerate(res)])
+    lab = np.concatenate([r[0] for r in res]).astype(np.int32)
+    off = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(r[1]) for r in res]))]).astype(np.int64)
+    pts = np.concatenate([r[2] for r in res]).astype(np.int32)
+    dcol, dlab, doff, dpts = e2e.ctx.bp_masks()
+    exact = bool(np.array_equal(col, dcol) and np.array_equal(lab, dlab) and np.array_equal(off, doff)
+                 and np.array_equal(pts, dpts))
+    g_all, tm = graph_cpu(P, F, col, lab, off, pts, thr, dense=True)
+    g_one, _ = graph_cpu(P, F, col, lab, off, pts, 1, dense=True)
+    cpu_all, cpu_one = s1_all + g_all, s1_one + g_one
+    rec["c2_e2e"]["cpu_baseline"] = {
+        "kind": "port", "cores": thr, "scene_ms": round(cpu_all * 1e3, 1),
+        "sample": f"the whole scene: S1 port on all {F} frames ({s1_all:.2f} s, OpenMP over frames) + the dense "
+                  f"S2-S6 port ({g_all:.2f} s), {thr} threads",
+        "single_thread_scene_ms": round(cpu_one * 1e3, 1),
+        "single_thread_sample": f"S1 port on 16 of the {F} frames scaled ({s1_one:.1f} s) + the S2-S6 port ({g_one:.2f} s)",
+        "s1_bit_exact_vs_device": exact}
+    rec["c2_e2e"]["speedup_vs_cpu_all_cores"] = round(cpu_all * 1e3 / rec["c2_e2e"]["scene_ms"], 1)
+    rec["c2_e2e"]["speedup_vs_cpu_one_thread"] = round(cpu_one * 1e3 / rec["c2_e2e"]["scene_ms"], 1)
+    rec["c2_g"]["cpu_baseline"] = {"kind": "port", "cores": thr, "scene_ms": round(g_all * 1e3, 1),
+                                   "single_thread_scene_ms": round(g_one * 1e3, 1),
+                                   "sample": "the dense S2-S6 port on the same masks (the e2e scene's)"}
+    rec["c2_g"]["speedup_vs_cpu_all_cores"] = round(g_all * 1e3 / rec["c2_g"]["scene_ms"], 1)
+    ratio_path = os.path.join(REPO, "profiles", "cpu_ratio_c2.json")
+    if os.path.exists(ratio_path):  # the reference's own S2-S6, timed in the build container
+        r = json.load(open(ratio_path))
+        rec["c2_g"]["reference_s2_s6_s_container"] = r["reference_s"]
+        rec["c2_g"]["speedup_vs_reference_s2_s6"] = round(r["reference_s"] * 1e3 / rec["c2_g"]["scene_ms"], 1)
+    return rec
 
 
 class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic the path reads
@@ -641,6 +727,7 @@ def main():
     ap.add_argument("--shape", default=None, help="default: c3 (g, e2e), c2 (api, pp, sweep)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 E2E / G record (N=1 only)")
     ap.add_argument("--shard", choices=["scene", "frames"], default="frames",
                     help="frames: one scene, its frames split over the ranks, S2-S6 row-block sharded (strong "
                          "scaling; the north_star's ScanNet++-sized C3 by default); scene: every rank its own "
@@ -760,6 +847,10 @@ def main():
                         f"(profiles/cpu_ratio_c2.json: the reference over the port for S2-S6 on C2); S1 here is the "
                         "port's restatement (oracle/s1_oracle.c) on one thread"}
 
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary and args.variant in ("e2e", "g"):
+        secondary = c2_record(local, max(3, min(args.steps, 10)), args.warmup)
+
     if rank == 0:
         line = {
             "metric": "mask-pair consensus counts/sec (per-scene graph build+cluster)",
@@ -783,6 +874,8 @@ def main():
             "stage_roofline": stages,
             "cpu_baseline": cpu,
         }
+        if secondary:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

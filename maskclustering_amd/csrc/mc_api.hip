@@ -2033,6 +2033,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                                   ": depth pixel equal to depth_trunc (the reference raises "
                                                   "IndexError at utils/mask_backprojection.py:100)"};
             }
+            MC_REQUIRE(!(hs[BS_VOXERR] & 2), MC_ERR_HIP, "voxel hash table not empty at slot start (internal error)");
             MC_REQUIRE(hs[BS_VOXERR] == 0, MC_ERR_UNSUPPORTED, "voxel index beyond 2^21 per axis");
             if (hs[BS_OVF]) {  // neighbour sets overflowed tmp: grow and redo the batch
                 tmp_cap = static_cast<size_t>(hs[BS_TOP]) + (static_cast<size_t>(hs[BS_TOP]) >> 1) + 1024;

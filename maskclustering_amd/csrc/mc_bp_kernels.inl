@@ -829,7 +829,14 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
                 }
                 const unsigned long long key = pack3(static_cast<int>(ix[0]), static_cast<int>(ix[1]), static_cast<int>(ix[2]));
                 e = mod_mul(bp_hash64(key), C);
-                while (true) {
+                // bounded probe: the slot's 2n entries start empty (kept empty by the reset below)
+                // and take <= n keys, so a free or matching entry exists; a table left dirty (a
+                // broken invariant) ends in an error flag instead of a wave that never finishes
+                for (unsigned probe = 0;; probe++) {
+                    if (probe == C) {
+                        atomicOr(errflag, 2);
+                        break;
+                    }
                     unsigned long long cur = hk[e];
                     if (cur == kEmptyKey) {
                         cur = atomicCAS(&hk[e], kEmptyKey, key);
@@ -1525,10 +1532,14 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #ifdef MC_BP_STAMPS
     unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
 #endif
+    // Ticket loop invariant: thread 0 overwrites s_slot only after every thread has read it.  The
+    // barrier after the read gives that directly (the body also ends in a barrier, and every path
+    // through it reaches block barriers, but the loop must not depend on the body's structure).
     while (true) {
         if (t == 0) s_slot = atomicAdd(ticket, 1);
         __syncthreads();
         const int tk = s_slot;
+        __syncthreads();
         if (tk >= cnt_cls) break;
         const int s = cls_list[tk];
         const int base = slot_pix[s], n = slot_nv[s];

@@ -376,3 +376,13 @@ int orc_num_threads(void)
     return 1;
 #endif
 }
+
+/* thread count of the OpenMP loops above (bench.py's single-thread / all-core baselines) */
+void orc_set_num_threads(int n)
+{
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}

@@ -129,6 +129,21 @@ def s1_frames(scene_f32, depth, seg, K, poses, params: BpParams | None = None, t
     return out
 
 
+class threads:
+    """``with oracle.threads(n):`` runs the OpenMP loops of the S2-S6 oracle on n threads"""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+
+    def __enter__(self):
+        self.prev = lib().orc_num_threads()
+        lib().orc_set_num_threads(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_num_threads(self.prev)
+
+
 def default_threads() -> int:
     """host threads for the oracle: OMP_NUM_THREADS when set (16 per GPU on the box), else all cores"""
     return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
@@ -179,6 +194,8 @@ def lib():
         L.orc_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p, ctypes.c_int, _f32p,
                                   ctypes.c_double, _i32p, _i32p, _i32p, _u8p, _u8p]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_set_num_threads.restype = None
+        L.orc_set_num_threads.argtypes = [ctypes.c_int]
         L.orcs_s2.restype = ctypes.c_int
         L.orcs_s2.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _i32p, _i64p, _i32p, _u8p, _u8p, _i64p, _i32p]
         L.orcs_s3.restype = ctypes.c_int

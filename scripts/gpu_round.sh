@@ -26,13 +26,13 @@ cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
 RAW=/tmp/mc_raw_$$   # raw profiler output stays on the box (per-dispatch CSVs are hundreds of MB)
 mkdir -p "$RAW"
 run timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/prof" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" \
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-secondary $BENCH_ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" \
     || { tail -20 "$OUT/prof_bench.err"; exit 1; }
 find "$RAW/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 python3 scripts/kstats.py "$OUT/kernel_stats.csv" | head -25
 for C in FETCH_SIZE WRITE_SIZE; do
   run timeout -s KILL 180 rocprofv3 --pmc "$C" --output-format csv -d "$RAW/pmc_$C" -o run -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err" \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary $BENCH_ARGS > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err" \
       || { tail -20 "$OUT/pmc_$C.err"; exit 1; }
   find "$RAW/pmc_$C" -name "*counter_collection.csv" -exec cp {} "$RAW/pmc_$C.csv" \;
 done
