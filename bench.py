@@ -328,7 +328,8 @@ class ShardedEndToEndStep(EndToEndStep):
         import torch
         import torch.distributed as dist
         from maskclustering_amd import _native
-        from maskclustering_amd.frame_shard import FrameShardedScene, frame_slice
+        from maskclustering_amd.frame_shard import (FrameShardedScene, balanced_frame_slices, frame_costs,
+                                                    frame_slice, gather_frame_costs)
         from maskclustering_amd.pipeline import GraphRun
         from maskclustering_amd.synthetic_frames import FRAME_SHAPES, make_frames_shape
         t0 = time.perf_counter()
@@ -338,13 +339,21 @@ class ShardedEndToEndStep(EndToEndStep):
         lo, hi = frame_slice(F, world, rank)
         dev = torch.device("cuda", local)
         fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}", frames=range(lo, hi), out="torch")
+        costs = None
+        if world > 1:  # cost-balanced slices: every rank costs its equal-count slice, then re-renders
+            costs = gather_frame_costs(frame_costs(fr.depth, fr.seg, fr.intrinsics), F)
+            blo, bhi = balanced_frame_slices(costs, world)[rank]
+            if (blo, bhi) != (lo, hi):
+                del fr
+                lo, hi = blo, bhi
+                fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}", frames=range(lo, hi), out="torch")
         self.fr = fr
         self.run = GraphRun(local)
         self.ctx = self.run.ctx
         self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
         self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
-        self.sh = FrameShardedScene(self.run, fr.num_points, F)
+        self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs)
         assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.t_depth, self.t_seg = fr.depth, fr.seg

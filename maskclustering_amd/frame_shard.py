@@ -1,7 +1,8 @@
 """Frame-sharded scenes over ranks (BASELINE north_star).
 
-One process per GPU.  Rank r owns the contiguous frame slice ``frame_slice(F, world, r)``
-and runs S1 (``utils/mask_backprojection.py:70-151``, per frame and independent across
+One process per GPU.  Rank r owns a contiguous frame slice (``frame_slice``: equal frame
+counts, or ``balanced_frame_slices`` over per-frame S1 cost estimates, ``frame_costs``, so that
+the ranks get equal work rather than equal frames) and runs S1 (``utils/mask_backprojection.py:70-151``, per frame and independent across
 frames) on its own GPU, so every frame's masks are exactly the single-GPU ones.  The
 per-rank mask CSRs are then all-gathered in rank order.  Slices are contiguous and
 ascending, so the concatenation is the reference's global mask order (frames ascending,
@@ -21,13 +22,92 @@ import torch
 import torch.distributed as dist
 
 
-def frame_slice(num_frames: int, world: int, rank: int) -> tuple[int, int]:
-    """[lo, hi) of the frames rank owns: contiguous, sizes differ by at most one."""
+def frame_slice(num_frames: int, world: int, rank: int, costs=None) -> tuple[int, int]:
+    """[lo, hi) of the frames rank owns: contiguous and ascending over the ranks.  Without costs
+    the sizes differ by at most one frame; with a per-frame cost vector (``frame_costs``) the
+    cuts fall where the cost prefix sum crosses r / world of the total, so every rank gets about
+    the same S1 work (frames differ: mask pixels and voxels vary with what a frame sees)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank {rank} of {world}")
+    if costs is not None:
+        return balanced_frame_slices(costs, world)[rank]
     base, extra = divmod(int(num_frames), world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+def balanced_frame_slices(costs, world: int) -> list[tuple[int, int]]:
+    """Contiguous frame slices of about equal total cost: cut r sits at the first frame whose
+    cost prefix sum (exclusive) reaches r / world of the total, nudged to the closer side of that
+    frame.  Costs are non-negative; an all-zero vector falls back to equal frame counts."""
+    c = np.asarray(costs, np.float64).reshape(-1)
+    F = len(c)
+    if world < 1:
+        raise ValueError(f"bad world size {world}")
+    if not np.all(np.isfinite(c)) or np.any(c < 0):
+        raise ValueError("frame costs must be finite and non-negative")
+    tot = float(c.sum())
+    if tot <= 0.0:
+        return [frame_slice(F, world, r) for r in range(world)]
+    incl = np.cumsum(c)
+    excl = incl - c
+    cuts = [0]
+    for r in range(1, world):
+        target = tot * r / world
+        i = int(np.searchsorted(incl, target, side="left"))  # frame i straddles the target
+        if i >= F:
+            cut = F
+        else:  # cut before frame i or after it, whichever lands closer to the target
+            cut = i if target - excl[i] <= incl[i] - target else i + 1
+        cuts.append(min(max(cut, cuts[-1]), F))
+    cuts.append(F)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def frame_costs(depth, seg, intrinsics, voxel_size: float = 0.01, depth_trunc: float = 20.0,
+                pixel_weight: float = 1.0, voxel_weight: float = 37.0, frame_weight: float = 2.4e5):
+    """Per-frame S1 cost estimate (float64 [F], on the frames' device) for ``balanced_frame_slices``.
+
+    S1's groups scale with three things per frame: the frame's pixels (the pixel
+    count, a constant per frame), the mask pixels (voxelisation) and the voxels (denoise and
+    ball query, the bulk).  Mask pixels are those with a mask id and a valid depth
+    (``get_depth_mask``, utils/mask_backprojection.py:42-45); the voxels are estimated from
+    the pixels' footprints: a pixel at depth d covers (d / fx)(d / fy) m², i.e. that over
+    voxel_size² voxels, at most one.  The default weights are the measured C3 per-unit costs
+    relative to a mask pixel (profiles/r02/v54_bench_e2e_c3.json stage times over the scene's
+    pixel, mask-pixel and voxel totals)."""
+    import torch
+    d = depth.to(torch.float32)
+    m = (seg != 0) & (d > 0) & (d <= depth_trunc)
+    K = torch.as_tensor(intrinsics, dtype=torch.float64, device=d.device).reshape(-1, 4)
+    fxy = (K[:, 0] * K[:, 1]).to(torch.float32).view(-1, 1, 1)
+    foot = torch.clamp(d * d / (fxy * float(voxel_size) ** 2), max=1.0)
+    px = m.sum(dim=(1, 2)).to(torch.float64)
+    vox = torch.where(m, foot, torch.zeros_like(foot)).sum(dim=(1, 2)).to(torch.float64)
+    return frame_weight + pixel_weight * px + voxel_weight * vox
+
+
+def gather_frame_costs(local_costs, num_frames: int, group=None) -> np.ndarray:
+    """All-gather the per-frame costs each rank computed over its equal-count slice
+    (``frame_slice`` without costs) into the scene's cost vector (host float64 [F])."""
+    import torch
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    lo, hi = frame_slice(num_frames, world, rank)
+    t = torch.as_tensor(local_costs, dtype=torch.float64).reshape(-1)
+    if len(t) != hi - lo:
+        raise ValueError(f"rank {rank} holds {len(t)} frame costs, its slice is [{lo}, {hi})")
+    if world == 1:
+        return t.cpu().numpy()
+    dev = _comm_device(group, t.device if t.device.type == "cuda" else torch.device("cpu"))
+    width = -(-int(num_frames) // world)  # slices differ by at most one frame
+    buf = torch.zeros(width, dtype=torch.float64, device=dev)
+    buf[:len(t)] = t.to(dev)
+    out = torch.empty(world * width, dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    out = out.cpu().numpy().reshape(world, width)
+    return np.concatenate([out[r, :frame_slice(num_frames, world, r)[1] - frame_slice(num_frames, world, r)[0]]
+                           for r in range(world)])
 
 
 def _comm_device(group, like: torch.device) -> torch.device:
@@ -35,13 +115,22 @@ def _comm_device(group, like: torch.device) -> torch.device:
     return like if dist.get_backend(group) == "nccl" else torch.device("cpu")
 
 
-def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None):
+def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
+                 max_masks: int | None = None):
     """All-gather per-rank mask CSRs into the global one.
 
     mask_col / mask_label / mask_off: this rank's masks (numpy; mask_col relative to
-    frame_lo); mask_pts: int32 tensor of their point ids (any device).
+    frame_lo); mask_pts: int32 tensor of their point ids (any device).  max_masks bounds any
+    rank's mask count (the default: 255 masks per frame of the largest slice, as segmentation
+    ids are uint8), which fixes the size of the first collective; None (masks from any source)
+    takes one max-reduce of the counts first.
     Returns (mask_col, mask_label, mask_off int64) as numpy and the global point ids as an
     int32 tensor on mask_pts' device.
+
+    Two collectives, one host read: (1) one packed int32 block per rank, [M, nnz, col[M],
+    label[M], len[M]] at a fixed stride, whose copy to the host the caller needs anyway (the
+    graph input's mask index is host metadata); (2) the point ids at the largest rank's nnz,
+    gathered on the device into one tensor and compacted there.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     out_dev = mask_pts.device
@@ -54,29 +143,35 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
         raise ValueError("inconsistent mask CSR")
     if world == 1:
         return col, lab, off.copy(), mask_pts[:nnz].clone()
+    if nnz >= 2 ** 31:
+        raise ValueError("a rank's mask point ids exceed the int32 block")
     dev = _comm_device(group, out_dev)
-    sizes = torch.tensor([M, nnz], dtype=torch.int64, device=dev)
-    all_sizes = [torch.empty_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes, group=group)
-    Ms = [int(x[0]) for x in all_sizes]
-    Ns = [int(x[1]) for x in all_sizes]
-    mmax, nmax = max(1, max(Ms)), max(1, max(Ns))
-    meta = np.zeros((3, mmax), np.int32)
-    meta[0, :M], meta[1, :M], meta[2, :M] = col, lab, np.diff(off)
-    meta_t = torch.from_numpy(meta).to(dev)
-    metas = [torch.empty_like(meta_t) for _ in range(world)]
-    dist.all_gather(metas, meta_t, group=group)
-    buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
-    buf[:nnz] = mask_pts[:nnz].to(dev)
-    bufs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf, group=group)
-    metas = [m.cpu().numpy() for m in metas]
-    g_col = np.concatenate([m[0, :k] for m, k in zip(metas, Ms)]).astype(np.int32)
-    g_lab = np.concatenate([m[1, :k] for m, k in zip(metas, Ms)]).astype(np.int32)
-    g_len = np.concatenate([m[2, :k] for m, k in zip(metas, Ms)]).astype(np.int64)
+    if max_masks is None:  # no bound known (masks from any source): one max-reduce of the counts
+        mm = torch.tensor([M], dtype=torch.int64, device=dev)
+        dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
+        max_masks = int(mm.item())
+    if M > max_masks:
+        raise ValueError(f"{M} masks exceed the block bound {max_masks}")
+    stride = 2 + 3 * int(max_masks)
+    blk = np.zeros(stride, np.int32)
+    blk[0], blk[1] = M, nnz
+    blk[2:2 + M], blk[2 + M:2 + 2 * M], blk[2 + 2 * M:2 + 3 * M] = col, lab, np.diff(off)
+    meta = torch.empty(world * stride, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(meta, torch.from_numpy(blk).to(dev), group=group)
+    meta = meta.cpu().numpy().reshape(world, stride)
+    Ms, Ns = meta[:, 0].astype(np.int64), meta[:, 1].astype(np.int64)
+    g_col = np.concatenate([meta[r, 2:2 + Ms[r]] for r in range(world)]).astype(np.int32)
+    g_lab = np.concatenate([meta[r, 2 + Ms[r]:2 + 2 * Ms[r]] for r in range(world)]).astype(np.int32)
+    g_len = np.concatenate([meta[r, 2 + 2 * Ms[r]:2 + 3 * Ms[r]] for r in range(world)]).astype(np.int64)
     g_off = np.zeros(len(g_len) + 1, np.int64)
     np.cumsum(g_len, out=g_off[1:])
-    g_pts = torch.cat([b[:n] for b, n in zip(bufs, Ns)]).to(out_dev)
+    nmax = max(1, int(Ns.max()))
+    buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
+    buf[:nnz] = mask_pts[:nnz].to(dev)
+    allp = torch.empty(world * nmax, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(allp, buf, group=group)
+    allp = allp.view(world, nmax).to(out_dev)
+    g_pts = torch.cat([allp[r, :int(Ns[r])] for r in range(world)])
     return g_col, g_lab, g_off, g_pts
 
 
@@ -88,7 +183,8 @@ class FrameShardedScene:
     frame slice, resident on its GPU.
     """
 
-    def __init__(self, run, num_points: int, num_frames: int, group=None, shard_graph: bool = True):
+    def __init__(self, run, num_points: int, num_frames: int, group=None, shard_graph: bool = True,
+                 costs=None):
         from .graph_shard import ShardedGraph
         self.run = run
         self.ctx = run.ctx
@@ -97,7 +193,14 @@ class FrameShardedScene:
         on = dist.is_initialized()
         self.rank = dist.get_rank(group) if on else 0
         self.world = dist.get_world_size(group) if on else 1
-        self.lo, self.hi = frame_slice(self.F, self.world, self.rank)
+        # costs (per-frame, e.g. gather_frame_costs(frame_costs(...))): cost-balanced slices
+        self.slices = (balanced_frame_slices(costs, self.world) if costs is not None
+                       else [frame_slice(self.F, self.world, r) for r in range(self.world)])
+        if costs is not None and len(costs) != self.F:
+            raise ValueError(f"{len(costs)} frame costs for {self.F} frames")
+        self.lo, self.hi = self.slices[self.rank]
+        # the mask block bound of gather_masks for S1 output: 255 ids per frame of the largest slice
+        self.max_masks = 255 * max(1, max(hi - lo for lo, hi in self.slices))
         self._pts = None  # global point ids (kept alive until the graph input copy is done)
         # the graph stages row-block sharded over the same ranks (shard_graph=False: replicated)
         self.graph = ShardedGraph(run, group) if shard_graph else None
@@ -157,7 +260,7 @@ class FrameShardedScene:
         else:  # more ranks than frames
             col, lab, off = np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64)
             local = torch.zeros(1, dtype=torch.int32, device=depth.device)
-        g_col, g_lab, g_off, self.pts = gather_masks(col, lab, off, local, self.lo, self.group)
+        g_col, g_lab, g_off, self.pts = gather_masks(col, lab, off, local, self.lo, self.group, self.max_masks)
         self.mask_index = (g_col, g_lab, g_off)
         torch.cuda.current_stream(self.pts.device).synchronize()  # the context stream reads them next
         self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, pts_device_ptr=self.pts.data_ptr())

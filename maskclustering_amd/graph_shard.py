@@ -83,11 +83,10 @@ class ShardedGraph:
             self.ctx.shard_import(ph, t, 0)
             self.bytes_moved += n
         else:
-            if ph == S3:  # variable size: the largest block sets the stride
+            if ph == S3:  # variable size: the largest block sets the stride (one max-reduce, one read)
                 sz = torch.tensor([n], dtype=torch.int64, device=self.comm_dev)
-                sizes = [torch.empty_like(sz) for _ in range(self.world)]
-                dist.all_gather(sizes, sz, group=self.group)
-                n_max = max(int(x.item()) for x in sizes)
+                dist.all_reduce(sz, op=dist.ReduceOp.MAX, group=self.group)
+                n_max = int(sz.item())
             else:         # FOREST: 4·(N0 + 2) bytes on every rank
                 n_max = n
             words = max((n_max + 3) // 4, 1)
@@ -96,9 +95,9 @@ class ShardedGraph:
             self.ctx.shard_export(ph, buf)
             self._sync_in()
             src = buf.to(self.comm_dev)
-            parts = [torch.empty_like(src) for _ in range(self.world)]
-            dist.all_gather(parts, src, group=self.group)
-            blocks = torch.cat(parts).to(self.dev)
+            blocks = torch.empty(self.world * words, dtype=torch.int32, device=self.comm_dev)
+            dist.all_gather_into_tensor(blocks, src, group=self.group)
+            blocks = blocks.to(self.dev)
             self._sync_out()
             self.ctx.shard_import(ph, blocks, 4 * words)
             self.bytes_moved += 4 * words * self.world

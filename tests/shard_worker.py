@@ -11,6 +11,11 @@ mode "graph:<shape>:<seed>:<cfg>" (CPU, gloo): every rank holds its frame slice'
 them and runs the sharded S2-S6 through ShardedGraph on the oracle-backed stand-in context
 (tests/oracle_shard_ctx.py); saves the canonical outputs.
 mode "gpugraph:<shape>:<seed>" (GPU, gloo, ranks share cuda:0): the same with the HIP context.
+mode "skew:<shape>:<seed>" (CPU, gloo): a skewed scene (every mask of the first quarter of the
+frames, one in eight elsewhere); each rank costs its equal-count slice's frames by their mask
+points, the costs are all-gathered and the ranks take cost-balanced slices (frame_shard.
+balanced_frame_slices) before the sharded S2-S6 on the oracle-backed context; saves the
+canonical outputs and the slices.
 """
 import os
 import sys
@@ -23,7 +28,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from maskclustering_amd.frame_shard import FrameShardedScene, frame_slice, gather_masks  # noqa: E402
+from maskclustering_amd.frame_shard import (FrameShardedScene, frame_slice, gather_frame_costs,  # noqa: E402
+                                            gather_masks)
 
 
 def local_masks(scene, lo, hi):
@@ -39,6 +45,27 @@ CFGS = {"scannet": dict(mask_visible_threshold=0.3, undersegment_filter_threshol
                        contained_threshold=0.8),
         "scannetpp": dict(mask_visible_threshold=0.4, undersegment_filter_threshold=0.2, view_consensus_threshold=1,
                           contained_threshold=0.9)}
+
+
+def skewed(scene):
+    """every mask of the first quarter of the frames, one in eight of the others"""
+    from maskclustering_amd.synthetic import SceneMasks
+    q = max(1, scene.num_frames // 4)
+    frames = [[] for _ in range(scene.num_frames)]
+    for g in range(scene.num_masks):
+        c = int(scene.mask_col[g])
+        if c < q or g % 8 == 0:
+            frames[c].append((int(scene.mask_label[g]), scene.mask_points(g)))
+    return SceneMasks.from_frame_lists(scene.num_points, frames)
+
+
+class OracleRun:  # the GraphRun surface FrameShardedScene / ShardedGraph use
+    def __init__(self):
+        from oracle_shard_ctx import OracleShardCtx
+        self.ctx = OracleShardCtx()
+
+    def set_masks(self, *a, **kw):
+        self.ctx.set_masks(*a, **kw)
 
 
 def main():
@@ -64,6 +91,21 @@ def main():
             sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
             sh.step(**CFGS[cfg])
             np.savez(out, **{k: np.asarray(v) for k, v in run.ctx.canonical().items()})
+        elif mode.startswith("skew:"):
+            from maskclustering_amd.synthetic import make_shape
+            _, shape, seed = mode.split(":")
+            s = skewed(make_shape(shape, seed=int(seed)))
+            elo, ehi = frame_slice(s.num_frames, world, rank)
+            lens = np.diff(s.mask_off).astype(np.float64)
+            local_costs = np.bincount(s.mask_col, weights=lens, minlength=s.num_frames)[elo:ehi]
+            costs = gather_frame_costs(torch.from_numpy(local_costs), s.num_frames)
+            run = OracleRun()
+            sh = FrameShardedScene(run, s.num_points, s.num_frames, costs=costs)
+            col, lab, off, pts = local_masks(s, sh.lo, sh.hi)
+            sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
+            sh.step(**CFGS["scannet"])
+            res = {k: np.asarray(v) for k, v in run.ctx.canonical().items()}
+            np.savez(out, slices=np.asarray(sh.slices, np.int64), costs=costs, **res)
         elif mode.startswith("gpugraph:"):
             from maskclustering_amd.pipeline import GraphRun
             from maskclustering_amd.synthetic import make_shape
@@ -81,7 +123,7 @@ def main():
             s = make_shape("tiny", seed=4)
             lo, hi = frame_slice(s.num_frames, world, rank)
             col, lab, off, pts = local_masks(s, lo, hi)
-            g = gather_masks(col, lab, off, torch.from_numpy(pts), lo)
+            g = gather_masks(col, lab, off, torch.from_numpy(pts), lo, max_masks=255 * (s.num_frames // world + 1))
             np.savez(out, col=g[0], label=g[1], off=g[2], pts=g[3].numpy())
         else:
             from maskclustering_amd.pipeline import GraphRun

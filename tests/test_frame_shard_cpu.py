@@ -23,6 +23,70 @@ def test_frame_slices_cover_frames_in_order():
         frame_slice(10, 2, 2)
 
 
+def test_balanced_slices_split_cost_evenly():
+    from maskclustering_amd.frame_shard import balanced_frame_slices, frame_slice
+    rng = np.random.default_rng(0)
+    for F in (1, 2, 7, 250, 1500):
+        for world in (1, 2, 3, 8, 16):
+            for kind in ("flat", "skew", "random", "zeros", "spike"):
+                c = {"flat": np.ones(F), "skew": np.where(np.arange(F) < max(1, F // 4), 50.0, 1.0),
+                     "random": rng.gamma(2.0, 1.0, F), "zeros": np.zeros(F),
+                     "spike": np.eye(1, F, F // 2).ravel() * 1e6 + 1.0}[kind]
+                sl = balanced_frame_slices(c, world)
+                assert len(sl) == world and sl[0][0] == 0 and sl[-1][1] == F
+                assert all(a[1] == b[0] and a[0] <= a[1] for a, b in zip(sl, sl[1:]))
+                assert [frame_slice(F, world, r, costs=c) for r in range(world)] == sl
+                if kind == "zeros":
+                    assert sl == [frame_slice(F, world, r) for r in range(world)]
+                    continue
+                # every slice within one frame's cost of the even share
+                share = c.sum() / world
+                for lo, hi in sl:
+                    assert c[lo:hi].sum() <= share + c.max() + 1e-9
+    with pytest.raises(ValueError):
+        balanced_frame_slices([1.0, -1.0], 2)
+
+
+def test_frame_costs_count_mask_pixels_and_footprints():
+    import torch
+    from maskclustering_amd.frame_shard import frame_costs
+    depth = torch.zeros(3, 4, 6)
+    seg = torch.zeros(3, 4, 6, dtype=torch.uint8)
+    depth[0] = 2.0
+    seg[0, :2] = 5                       # 12 mask pixels at 2 m
+    depth[1, :, :3] = 30.0               # beyond DEPTH_TRUNC: no mask pixels
+    seg[1] = 1
+    depth[2] = 1.0
+    seg[2, 0, 0] = 7                     # one pixel
+    K = np.tile([100.0, 100.0, 3.0, 2.0], (3, 1))
+    c = frame_costs(depth, seg, K, pixel_weight=1.0, voxel_weight=10.0, frame_weight=0.0).numpy()
+    foot = lambda d: min(1.0, d * d / (100.0 * 100.0 * 1e-4))  # noqa: E731
+    np.testing.assert_allclose(c, [12 * (1 + 10 * foot(2.0)), 0.0, 1 + 10 * foot(1.0)], rtol=1e-6)
+
+
+def test_skewed_scene_balanced_slices_equal_single_process(tmp_path):
+    """A scene whose masks crowd into the first quarter of the frames: the cost-balanced slices
+    differ from the equal-count ones, and every rank still ends with the single-process result."""
+    from maskclustering_amd.synthetic import make_shape
+    from oracle import oracle
+    from shard_worker import skewed
+    s = skewed(make_shape("c1", seed=1))
+    want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts,
+                             **KW["scannet"])
+    world = 3
+    lens = np.diff(s.mask_off).astype(np.float64)
+    costs = np.bincount(s.mask_col, weights=lens, minlength=s.num_frames)
+    for out in run_ranks("skew:c1:1", world, tmp_path):
+        got = np.load(out)
+        np.testing.assert_array_equal(got["costs"], costs)
+        sl = [tuple(x) for x in got["slices"]]
+        assert sl[0][1] < s.num_frames // world  # the crowded first slice is short
+        share = [costs[lo:hi].sum() for lo, hi in sl]
+        assert max(share) <= costs.sum() / world + costs.max()
+        for k in want:
+            np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_equals_global_mask_list(tmp_path, world):
     from maskclustering_amd.synthetic import make_shape
