@@ -516,7 +516,8 @@ def run_api(a):
         t = time.perf_counter()
         nodes, thr, mpc, pfm = construction.mask_graph_construction(args, fr.scene_points, fids, ds)
         t1 = time.perf_counter()
-        objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+        objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False,
+                                                            replay=a.replay)
         t2 = time.perf_counter()
         out = pp.post_process_objects(objects, mpc, fr.scene_points, pfm, fids, args.point_filter_threshold) \
             if a.with_pp else None
@@ -551,6 +552,7 @@ def run_api(a):
            "config": {"workload": f"{a.shape}: synthetic RGB-D scene, {fr.num_frames} frames "
                                   f"{fr.depth.shape[2]}x{fr.depth.shape[1]}, P={fr.num_points}, "
                                   f"{len(nodes)} nodes -> {len(objects)} objects", "variant": "api",
+                      "replay": bool(a.replay),
                       "with_post_process": bool(a.with_pp),
                       "part_ms": {k: round(1e3 * float(np.mean(v)), 3) for k, v in parts.items() if v}}}
     print(json.dumps(res), flush=True)
@@ -733,6 +735,8 @@ def main():
     ap.add_argument("--pool", type=int, default=4, help="sweep: distinct rendered scenes per rank")
     ap.add_argument("--with-pp", action="store_true", help="api: include post_process's compute")
     ap.add_argument("--profile", action="store_true", help="api: cProfile one extra step to stderr")
+    ap.add_argument("--replay", action="store_true", help="api: iterative_clustering(replay=True), the "
+                                                          "reference-exact set orders (INTEGRATION.md §4)")
     ap.add_argument("--shape", default=None, help="default: c3 (g, e2e), c2 (api, pp, sweep)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -854,7 +858,7 @@ def main():
                 "note": "the reference's own S1 (utils/mask_backprojection.py) calls Open3D and pytorch3d, which are not "
                         "installed in the build container or on the box, so only its S2-S6 was timed against the C port "
                         f"(profiles/cpu_ratio_c2.json: the reference over the port for S2-S6 on C2); S1 here is the "
-                        "port's restatement (oracle/s1_oracle.c) on one thread"}
+                        "port's restatement (oracle/s1_oracle.c), timed on all host threads (value) and on one (single_thread)"}
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary and args.variant in ("e2e", "g"):

@@ -112,6 +112,7 @@ struct mc_ctx {
     DevBuf d_scene, d_gcnt, d_gstart, d_gbkt, d_gcellk, d_gpts, d_gidx, d_gcell, d_gscan_tmp;
     DevBuf d_in_depth, d_in_seg, d_in_intr, d_in_pose;
     DevBuf d_band, d_present, d_fflags, d_cand, d_npix, d_csidx, d_poff, d_slot_of, d_bpstat;
+    DevBuf d_bpvid;  // per-batch valid-id map (k_bp_count -> k_bp_compact), 1 byte per pixel
     DevBuf d_slot_frame, d_slot_id, d_slot_np, d_slot_pix, d_slot_nv, d_slot_m, d_slot_ns, d_slot_box, d_slot_nn,
         d_slot_toff, d_slot_cov;
     DevBuf d_pix_list, d_hkey, d_hvid, d_hfirst, d_vox_entry, d_acc, d_vpts, d_pcell, d_pbkt, d_bcnt, d_bstart,
@@ -342,7 +343,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     for (DevBuf *b : bufs) b->release();
     DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
                          &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg,
-                         &ctx->d_in_intr, &ctx->d_in_pose, &ctx->d_band, &ctx->d_present, &ctx->d_fflags,
+                         &ctx->d_in_intr, &ctx->d_in_pose, &ctx->d_band, &ctx->d_bpvid, &ctx->d_present, &ctx->d_fflags,
                          &ctx->d_cand, &ctx->d_npix, &ctx->d_csidx, &ctx->d_poff, &ctx->d_slot_of, &ctx->d_bpstat,
                          &ctx->d_slot_frame, &ctx->d_slot_id, &ctx->d_slot_np, &ctx->d_slot_pix, &ctx->d_slot_nv,
                          &ctx->d_slot_m, &ctx->d_slot_ns, &ctx->d_slot_box, &ctx->d_slot_nn, &ctx->d_slot_toff,
@@ -1572,6 +1573,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     const size_t px = static_cast<size_t>(fb) * H * W + 1;
     const size_t slots = slots_cap(fb);
     ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * mc::kBpWaves * 256 * 4);
+    ctx->d_bpvid.reserve(static_cast<size_t>(fb) * H * W + 16);
     ctx->d_present.reserve(static_cast<size_t>(fb) * 8 * 4);
     ctx->d_fflags.reserve(static_cast<size_t>(fb) * 4);
     ctx->d_cand.reserve(slots * 4);
@@ -1932,7 +1934,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 MC_HIP(hipMemsetAsync(ctx->d_present.ptr, 0, fb * 8 * 4, s));
                 MC_HIP(hipMemsetAsync(ctx->d_fflags.ptr, 0, fb * 4, s));
                 hipLaunchKernelGGL(mc::k_bp_count, dim3(nbands, fb), dim3(256), 0, s, dB, sB, TB, dv,
-                                   ctx->d_band.as<int>(), ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>());
+                                   ctx->d_band.as<int>(), ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(),
+                                   ctx->d_bpvid.as<unsigned char>());
                 hipLaunchKernelGGL(mc::k_bp_frames, dim3(fb), dim3(256), 0, s, ctx->d_band.as<int>(),
                                    ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(), dv, ctx->d_cand.as<int>(),
                                    ctx->d_npix.as<int>(), st + BS_ERRF);
@@ -1942,7 +1945,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_csidx.as<int>(), ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), nslot,
                                    ctx->d_slot_of.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(),
                                    ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>());
-                hipLaunchKernelGGL(mc::k_bp_compact, dim3(nbands, fb), dim3(256), 0, s, dB, sB, ctx->d_band.as<int>(),
+                hipLaunchKernelGGL(mc::k_bp_compact, dim3(nbands, fb), dim3(256), 0, s, ctx->d_bpvid.as<unsigned char>(),
+                                   ctx->d_band.as<int>(),
                                    ctx->d_slot_of.as<int>(), ctx->d_slot_pix.as<int>(), dv,
                                    ctx->d_pix_list.as<unsigned>());
                 bp_debug_sync(s, "bp_pixels");

@@ -80,9 +80,11 @@ __device__ __forceinline__ void bp_world(const double *__restrict__ K, const dou
     double r[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) r[k] = (((T[4 * k] * x) + (T[4 * k + 1] * y)) + (T[4 * k + 2] * z)) + T[4 * k + 3];
-    ox = r[0] / r[3];
-    oy = r[1] / r[3];
-    oz = r[2] / r[3];
+    // the homogeneous divide is the identity when w == 1 (a rigid pose): skipped, bit for bit the same
+    const bool unit = r[3] == 1.0;
+    ox = unit ? r[0] : r[0] / r[3];
+    oy = unit ? r[1] : r[1] / r[3];
+    oz = unit ? r[2] : r[2] / r[3];
 }
 
 // (u3): nanoflann L2 for 3-D, ((dx*dx + dy*dy) + dz*dz)
@@ -199,7 +201,8 @@ constexpr int kBpSub = kBpBand / kBpWaves;    // rows per sub-band
 constexpr int kBpPix = 4;                     // 64-pixel steps whose loads a wave issues together
 __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
                                                   const double *__restrict__ pose, BpDev pr, int *__restrict__ band_cnt,
-                                                  unsigned *__restrict__ present, int *__restrict__ fflags)
+                                                  unsigned *__restrict__ present, int *__restrict__ fflags,
+                                                  unsigned char *__restrict__ vid)
 {
     __shared__ int cnt[kBpWaves][256];
     __shared__ unsigned pres[8];
@@ -233,6 +236,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
           const int i = ib0 + 256 * u + 4 * lane;
           const int sids[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
           const float ds[4] = {dq[u].x, dq[u].y, dq[u].z, dq[u].w};
+          unsigned vw = 0u;  // the four pixels' valid ids (k_bp_compact reads these instead of seg + depth)
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             int id = -1;
@@ -246,6 +250,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
                 if (static_cast<double>(d) == pr.trunc) trunc = 1;
                 if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id = sid;
             }
+            vw |= static_cast<unsigned>(id > 0 ? id : 0) << (8 * j);
             unsigned long long act = __ballot(id >= 0);
             while (act) {
                 const int leader = __ffsll(static_cast<long long>(act)) - 1;
@@ -255,6 +260,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
                 act &= ~m;
             }
           }
+          if (i < i1) *reinterpret_cast<unsigned *>(vid + fb + i) = vw;
         }
       }
     } else
@@ -281,6 +287,7 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
             }
             if (static_cast<double>(d) == pr.trunc) trunc = 1;
             if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id = sid;
+            vid[fb + i] = static_cast<unsigned char>(id > 0 ? id : 0);
         }
         unsigned long long act = __ballot(id >= 0);
         while (act) {  // one LDS add per distinct id per wave
@@ -350,8 +357,10 @@ __global__ __launch_bounds__(256) void k_bp_slots(const int *__restrict__ cand, 
 
 // Stable compaction: every slot's pixels in row-major order (the order of view_points[valid_mask],
 // :96-100).  Each wave walks its own sub-band with its own per-id cursors (the sub-band offsets of
-// k_bp_frames), ranks within a 64-pixel step by ballot groups: no barrier after the set-up.
-__global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ depth, const unsigned char *__restrict__ seg,
+// k_bp_frames), ranks within a 64-pixel step by ballot groups: no barrier after the set-up.  The
+// pixels come from k_bp_count's valid-id map (1 byte per pixel: the id where the depth is valid, else
+// 0), not from the frames' seg + depth (5 bytes).
+__global__ __launch_bounds__(256) void k_bp_compact(const unsigned char *__restrict__ vid,
                                                     const int *__restrict__ band_off, const int *__restrict__ slot_of,
                                                     const int *__restrict__ slot_pix, BpDev pr,
                                                     unsigned *__restrict__ pix_list)
@@ -376,29 +385,25 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
       // four consecutive pixels per lane (lane-major: pixel = 4 * lane + j of the 256-pixel step);
       // per id: each lane counts its matching pixels, a wave exclusive scan of the counts gives
       // the lanes' bases, the leader bumps the cursor by the total
-      for (int ib0 = i0; ib0 < i1; ib0 += 256 * 2) {
-        uchar4 sv[2];
-        float4 dq[2];
+      for (int ib0 = i0; ib0 < i1; ib0 += 256 * 4) {
+        uchar4 sv[4];
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < 4; u++) {
           const int i = ib0 + 256 * u + 4 * lane;
-          sv[u] = i < i1 ? *reinterpret_cast<const uchar4 *>(seg + fb + i) : make_uchar4(0, 0, 0, 0);
-          dq[u] = i < i1 ? *reinterpret_cast<const float4 *>(depth + fb + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+          sv[u] = i < i1 ? *reinterpret_cast<const uchar4 *>(vid + fb + i) : make_uchar4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < 4; u++) {
           const int i = ib0 + 256 * u + 4 * lane;
           const int sids[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
-          const float ds[4] = {dq[u].x, dq[u].y, dq[u].z, dq[u].w};
           int id[4];
           unsigned pend = 0u;
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             id[j] = -1;
             if (i < i1) {
-                const int sid = sids[j];
-                const float d = ds[j];
-                if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && mycur[sid] >= 0) id[j] = sid;
+                const int sid = sids[j];  // valid-id map of k_bp_count: 0 = no id or no valid depth
+                if (sid != 0 && mycur[sid] >= 0) id[j] = sid;
             }
             if (id[j] >= 0) pend |= 1u << j;
           }
@@ -444,12 +449,10 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
     }
     for (int ib0 = i0; ib0 < i1; ib0 += 64 * kBpPix) {
       int sidv[kBpPix];
-      float dv[kBpPix];
 #pragma unroll
       for (int u = 0; u < kBpPix; u++) {
         const int i = ib0 + 64 * u + lane;
-        sidv[u] = i < i1 ? seg[fb + i] : 0;
-        dv[u] = i < i1 ? depth[fb + i] : 0.f;
+        sidv[u] = i < i1 ? vid[fb + i] : 0;
       }
 #pragma unroll
       for (int u = 0; u < kBpPix; u++) {
@@ -457,8 +460,7 @@ __global__ __launch_bounds__(256) void k_bp_compact(const float *__restrict__ de
         int id = -1;
         if (i < i1) {
             const int sid = sidv[u];
-            const float d = dv[u];
-            if (sid != 0 && d > 0.0f && static_cast<double>(d) < pr.trunc && mycur[sid] >= 0) id = sid;
+            if (sid != 0 && mycur[sid] >= 0) id = sid;
         }
         unsigned long long act = __ballot(id >= 0);
         int pos = 0;
@@ -545,6 +547,7 @@ constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_l
 constexpr int kVxH = 6144, kVxV = 4096;      // first tier: LDS hash entries (load <= 2/3), voxels
 constexpr int kVxH2 = 12288, kVxV2 = 8192;   // second tier
 constexpr unsigned kVxEmpty = ~0u;
+
 
 __device__ __forceinline__ void vx_point(const unsigned *__restrict__ pl, const float *__restrict__ dep,
                                          const double *__restrict__ K, const double *__restrict__ T, int W, int k,
@@ -1164,22 +1167,6 @@ __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks
 #define BP_STAMP(k) do { } while (0)
 #endif
 
-// acc + v(lane 0) + v(lane 1) + ... + v(lane 63), in lane order, skipping lanes with v <= 0 (a
-// std::accumulate step over 64 values); the lane values are read as scalars
-__device__ __forceinline__ double seq_add64_pos(double acc, double v)
-{
-    const long long bits = __double_as_longlong(v);
-    const int lo = static_cast<int>(bits), hi = static_cast<int>(bits >> 32);
-#pragma unroll
-    for (int j = 0; j < 64; j++) {
-        const unsigned long long b = (static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readlane(hi, j))) << 32) |
-                                     static_cast<unsigned>(__builtin_amdgcn_readlane(lo, j));
-        const double a = __longlong_as_double(static_cast<long long>(b));
-        if (a > 0) acc = acc + a;
-    }
-    return acc;
-}
-
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
 constexpr int kBpLdsN = 16384;  // largest class of the LDS-kernel template
@@ -1325,99 +1312,128 @@ __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, in
     }
 }
 
-// Per-workgroup eps-neighbour lists: entry k of sorted position q is the u16 at
-// uint4 index (k / 8) * N + q, half-word k % 8: a wave's stores of one k fall on 16-byte strided
-// words (few cache lines), and a point's whole list (<= 64 entries) is 8 uint4 loads that are all
-// issued before the first is used.
+// Per-workgroup eps-neighbour lists: slot k of sorted position q is the u16 at uint4 index
+// (k / 8) * N + q, half-word k % 8: a wave's stores of one k fall on 16-byte strided words (few cache
+// lines), and a point's whole list (<= 64 slots) is 8 uint4 loads issued before the first is used.
+// An entry is the neighbour's sorted position (14 bits: N <= 16384) and, in the top two bits, its
+// k-NN radius class: 0 / 1 / 2 = inside knn_r2[0 / 1 / 2] (0.6 / 0.75 / 0.9 eps), 3 = the rest of
+// the eps ball.  Two regions: the near entries (class <= 1) fill slots 0, 1, .. upward, the far ones
+// slots 63, 62, .. downward, so that the near set is a prefix: when it holds >= k points (the common
+// case) the k-NN takes its candidates from it with static register indices, no selection pass.
+// sflag[q] = count (bits 0-14, self included) | near count (bits 15-21) | kept (bit 30).
+constexpr unsigned kNbPos = 0x3FFFu;
+constexpr int kNbCnt = 0x7FFF;
+static_assert(kBpLdsN <= 16384, "sorted positions fit 14 bits, counts 15 bits");
+__device__ __forceinline__ int nb_cnt(int f) { return f & kNbCnt; }
+__device__ __forceinline__ int nb_near(int f) { return (f >> 15) & 0x7F; }
 template <int N>
-__device__ __forceinline__ void nb_put(unsigned short *__restrict__ nbw, int q, int k, int q2)
+__device__ __forceinline__ void nb_put(unsigned short *__restrict__ nbw, int q, int k, unsigned e)
 {
-    nbw[(static_cast<size_t>(k >> 3) * N + q) * 8 + (k & 7)] = static_cast<unsigned short>(q2);
+    nbw[(static_cast<size_t>(k >> 3) * N + q) * 8 + (k & 7)] = static_cast<unsigned short>(e);
+}
+__device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
+{
+    return 3u - (d2 < pr.knn_r2[0] ? 1u : 0u) - (d2 < pr.knn_r2[1] ? 1u : 0u) - (d2 < pr.knn_r2[2] ? 1u : 0u);
 }
 
-// fn(q2) for the first cnt (<= kBpNbCap) entries of sorted position q's list: the two halves of
-// 32 entries are loaded before either is processed; the entries are then visited by one rolled
-// loop with a wave-uniform index (register-relative moves), so fn's code appears once: unrolled
-// copies of a 20-step insertion overflow the instruction cache.
-template <int N, typename Fn>
-__device__ __forceinline__ void nb_list(const unsigned short *__restrict__ nbw, int q, int cnt, Fn &&fn)
+// The eps-neighbour list of sorted position q (point a, cell (x, y, z)): every point of the 27 cells
+// with d2 < eps2 (self included), in cell-walk order within each region.  One predicate per
+// candidate (cell key and distance together, the record loaded whole) and one store; once the two
+// regions meet the entries are counted only (more than kBpNbCap: the point walks its cells).
+// Returns (count, near count).
+template <int N>
+__device__ __forceinline__ int2 lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
+                                             const BpDev &pr, unsigned short *__restrict__ nbw, int q)
 {
-    static_assert(kBpNbCap == 64, "eight uint4 per point");
-    const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
-    unsigned w[32];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
-        w[4 * u] = v.x;
-        w[4 * u + 1] = v.y;
-        w[4 * u + 2] = v.z;
-        w[4 * u + 3] = v.w;
-    }
-    // k is the same in every active lane (lanes only leave), so w[k >> 1] is a uniform index
-#pragma unroll 1
-    for (int k = 0; k < cnt; k++) fn(static_cast<int>((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu));
-}
-
-// nb_list for the DBSCAN union: entry k + 1's neighbour count and union-find parent are loaded
-// before fn(q2, count, parent) runs on entry k's (a parent read early is still a node of q2's
-// component, so it is a valid place to start q2's find)
-template <int N, typename Fn>
-__device__ __forceinline__ void nb_list_uf(const unsigned short *__restrict__ nbw, const int *sflag, int *spar, int q,
-                                           int cnt, Fn &&fn)
-{
-    static_assert(kBpNbCap == 64, "eight uint4 per point");
-    const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
-    unsigned w[32];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
-        w[4 * u] = v.x;
-        w[4 * u + 1] = v.y;
-        w[4 * u + 2] = v.z;
-        w[4 * u + 3] = v.w;
-    }
-    int e = static_cast<int>(w[0] & 0xFFFFu);
-    int nf = cnt > 0 ? sflag[e] : 0, np = cnt > 0 ? ld_wg(spar + e) : 0;
-#pragma unroll 1
-    for (int k = 0; k < cnt; k++) {
-        const int q2 = e, f = nf, p = np;
-        if (k + 1 < cnt) {
-            e = static_cast<int>((w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu);
-            nf = sflag[e];
-            np = ld_wg(spar + e);
+    auto range = [&](int d, unsigned long long &key) {
+        const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
+        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        key = pack3(cx, cy, cz);
+        const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
+        return make_int2(g.bs[b], g.bs[b + 1]);
+    };
+    const double eps2 = pr.eps2;
+    int ca = 0, cb = 0;
+    auto visit = [&](const double4 &p, int q2, unsigned long long key) {
+        const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
+        const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
+        if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
+            const unsigned c = nb_class(d2, pr);
+            const bool nearc = c <= 1u;
+            if (ca + cb < kBpNbCap) nb_put<N>(nbw, q, nearc ? ca : kBpNbCap - 1 - cb, static_cast<unsigned>(q2) | (c << 14));
+            ca += nearc ? 1 : 0;
+            cb += nearc ? 0 : 1;
         }
-        fn(q2, f, p);
+    };
+    unsigned long long nkey = 0;
+    int2 nr = range(0, nkey);
+#pragma unroll 1
+    for (int d = 0; d < 27; d++) {
+        const unsigned long long key = nkey;
+        const int2 r = nr;
+        if (d + 1 < 27) nr = range(d + 1, nkey);
+        int q2 = r.x;
+        const int e = r.y;
+        for (; q2 + 2 <= e; q2 += 2) {
+            const double4 p0 = g.pt[q2], p1 = g.pt[q2 + 1];
+            visit(p0, q2, key);
+            visit(p1, q2 + 1, key);
+        }
+        if (q2 < e) visit(g.pt[q2], q2, key);
     }
+    return make_int2(ca + cb, ca);
 }
 
-// nb_list over the entries' records: the record of entry k + 1 is loaded from LDS before fn runs
-// on entry k's, so the load latency hides behind fn (the k-NN's sorted insert) without a second
-// copy of fn's code
-template <int N, typename Fn>
-__device__ __forceinline__ void nb_list_pts(const unsigned short *__restrict__ nbw, const double4 *spt, int q, int cnt,
-                                            Fn &&fn)
+// the uint4 words of sorted position q's list that hold its two regions (slots [0, ca) and
+// [64 - cb, 64)), all issued together; the other words are zero
+template <int N>
+__device__ __forceinline__ void nb_load(const unsigned short *__restrict__ nbw, int q, int ca, int cb, unsigned (&w)[32])
 {
     static_assert(kBpNbCap == 64, "eight uint4 per point");
     const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
-    unsigned w[32];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
+        if (8 * u < ca || 8 * u + 8 > kBpNbCap - cb) v = row[static_cast<size_t>(u) * N];
         w[4 * u] = v.x;
         w[4 * u + 1] = v.y;
         w[4 * u + 2] = v.z;
         w[4 * u + 3] = v.w;
     }
-    double4 nxt = cnt > 0 ? spt[w[0] & 0xFFFFu] : make_double4(0.0, 0.0, 0.0, 0.0);
+}
+// slot k of the loaded words (k must be wave-uniform: register-relative moves, no scratch)
+__device__ __forceinline__ unsigned nb_ent(const unsigned (&w)[32], int k)
+{
+    return (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+}
+
+// fn(k, entry, pre(entry)) for the slots of both regions, near region upward then far region
+// downward; pre(entry of the next slot) is issued before fn runs on this one (its loads overlap fn).
+// The slot index is the same in every active lane (lanes only leave), so each region's loop keeps
+// one copy of fn's code and reads the words with uniform register indices.
+template <typename Pre, typename Fn>
+__device__ __forceinline__ void nb_walk(const unsigned (&w)[32], int ca, int cb, Pre &&pre, Fn &&fn)
+{
+    if (ca > 0) {
+        auto nx = pre(nb_ent(w, 0));
 #pragma unroll 1
-    for (int k = 0; k < cnt; k++) {
-        const double4 cur = nxt;
-        const int k1 = k + 1;
-        if (k1 < cnt) nxt = spt[(w[k1 >> 1] >> (16 * (k1 & 1))) & 0xFFFFu];
-        fn(cur);
+        for (int k = 0; k < ca; k++) {
+            const auto cur = nx;
+            const unsigned e = nb_ent(w, k);
+            if (k + 1 < ca) nx = pre(nb_ent(w, k + 1));
+            fn(k, e, cur);
+        }
+    }
+    if (cb > 0) {
+        auto nx = pre(nb_ent(w, kBpNbCap - 1));
+#pragma unroll 1
+        for (int j = 0; j < cb; j++) {
+            const int k = kBpNbCap - 1 - j;
+            const auto cur = nx;
+            const unsigned e = nb_ent(w, k);
+            if (j + 1 < cb) nx = pre(nb_ent(w, k - 1));
+            fn(k, e, cur);
+        }
     }
 }
 
@@ -1471,16 +1487,12 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 #ifndef MC_KNN_RING
 #define MC_KNN_RING 1  // 0: points whose eps list holds < k kept points skip the grid rings (whole-cloud scan)
 #endif
-#ifndef MC_UF_PREFETCH
-#define MC_UF_PREFETCH 1  // 0: the union's list walk without the one-ahead count / parent loads
-#endif
 #ifndef MC_SORT20_MIN_N
 #define MC_SORT20_MIN_N 2048  // size classes below this fill the k-NN by sorted inserts only (the
                                // network's registers spill in the 4- and 2-workgroup-per-CU classes)
 #endif
 #ifndef MC_ABLATE_BP
-#define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union,
-                        // 3 = k-NN list pass without the sorted inserts, 4 = k-NN list pass on self only
+#define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union
 #endif
 
 template <int N>
@@ -1529,6 +1541,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     const int cnt_cls = *cls_cnt;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     unsigned short *nbw = nbl + static_cast<size_t>(blockIdx.x) * N * kBpNbCap;
+    // one array for the list words of every walk (union, labels, k-NN): the compiler keeps a
+    // dynamically indexed array in registers only within a per-function budget, so separate arrays
+    // per walk would land in scratch
+    unsigned w[32];
 #ifdef MC_BP_STAMPS
     unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1616,14 +1632,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             int x, y, z;
             unpack3(keyof(q), x, y, z);
             const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-            int cnt = 0;
-            lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                if (d2 < pr.eps2) {
-                    if (cnt < kBpNbCap) nb_put<N>(nbw, q, cnt, q2);
-                    cnt++;
-                }
-            });
-            sflag[q] = cnt;
+            const int2 c2 = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
+            sflag[q] = c2.x | (min(c2.y, kBpNbCap) << 15);
             spar[q] = q;
         }
         __syncthreads();
@@ -1633,28 +1643,29 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         if (t == 0) s_ndef = 0;
         __syncthreads();
         for (int q = t; q < n; q += T) {
-            const int cnt = sflag[q];
+            const int fl = sflag[q], cnt = nb_cnt(fl);
             if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
             if (cnt > kBpNbCap) {
                 sX[atomicAdd(&s_ndef, 1)] = q;
                 continue;
             }
             int ra = uf_find_s(spar, q);
-#if MC_UF_PREFETCH
-            nb_list_uf<N>(nbw, sflag, spar, q, cnt, [&](int q2, int f2, int p2) {
-                if (q2 < q && f2 >= pr.minpts && p2 != ra) {  // parent == root: joined already
-                    const int rb = uf_find_s(spar, p2);
-#else
-            nb_list<N>(nbw, q, cnt, [&](int q2) {
-                if (q2 < q && sflag[q2] >= pr.minpts) {
-                    const int rb = uf_find_s(spar, q2);
-#endif
-                    if (rb != ra) {  // most edges of a dense cluster are already joined
-                        uf_unite_s(spar, ra, rb);
-                        ra = uf_find_s(spar, ra);
-                    }
-                }
-            });
+            const int ca = nb_near(fl);
+            nb_load<N>(nbw, q, ca, cnt - ca, w);
+            // the next entry's count and union-find parent are loaded before this one's find (a parent
+            // read early is still a node of q2's component, so it is a valid place to start the find)
+            nb_walk(w, ca, cnt - ca,
+                    [&](unsigned e) { return make_int2(sflag[e & kNbPos], ld_wg(spar + (e & kNbPos))); },
+                    [&](int, unsigned e, int2 fp) {
+                        const int q2 = static_cast<int>(e & kNbPos);
+                        if (q2 < q && nb_cnt(fp.x) >= pr.minpts && fp.y != ra) {  // parent == root: joined already
+                            const int rb = uf_find_s(spar, fp.y);
+                            if (rb != ra) {  // most edges of a dense cluster are already joined
+                                uf_unite_s(spar, ra, rb);
+                                ra = uf_find_s(spar, ra);
+                            }
+                        }
+                    });
         }
         __syncthreads();
         for (int f = t; f < s_ndef; f += T) {
@@ -1664,7 +1675,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
             int ra = uf_find_s(spar, q);
             lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                if (d2 < pr.eps2 && q2 < q && sflag[q2] >= pr.minpts) {
+                if (d2 < pr.eps2 && q2 < q && nb_cnt(sflag[q2]) >= pr.minpts) {
                     const int rb = uf_find_s(spar, q2);
                     if (rb != ra) {
                         uf_unite_s(spar, ra, rb);
@@ -1681,7 +1692,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #pragma unroll
             for (int k = 0; k < (N + T - 1) / T; k++) {
                 const int q = t + k * T;
-                rq[k] = (q < n && sflag[q] >= pr.minpts) ? uf_find_s(spar, q) : -1;
+                rq[k] = (q < n && nb_cnt(sflag[q]) >= pr.minpts) ? uf_find_s(spar, q) : -1;
             }
             __syncthreads();
             for (int q = t; q < n; q += T) sB[q] = INT_MAX;
@@ -1717,7 +1728,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             if (spar[q] >= 0) {
                 l = sX[spar[q]];
             } else {
-                const int cnt = sflag[q];
+                const int fl = sflag[q], cnt = nb_cnt(fl);
                 int best = INT_MAX, broot = -1;
                 auto near = [&](int q2) {
                     const int r2 = spar[q2];
@@ -1727,7 +1738,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     }
                 };
                 if (cnt <= kBpNbCap) {
-                    nb_list<N>(nbw, q, cnt, near);
+                    const int ca = nb_near(fl);
+                    nb_load<N>(nbw, q, ca, cnt - ca, w);
+                    nb_walk(w, ca, cnt - ca, [](unsigned e) { return e; },
+                            [&](int, unsigned e, unsigned) { near(static_cast<int>(e & kNbPos)); });
                 } else {
                     int x, y, z;
                     unpack3(keyof(q), x, y, z);
@@ -1765,6 +1779,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         __syncthreads();
         BP_STAMP(25);
+        const bool all_kept = m == n;
         // 10. k nearest kept points: the eps list when it holds >= k kept points; else (deferred to a
         //     compacted pass, so that few waves walk cells) grid rings up to R = 2; else (sparse
         //     point, or m < k) all of S, by a whole wave or one lane per point
@@ -1789,7 +1804,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             savg[r] = 1.0;
             continue;
 #endif
-            const int cnt = fl & ((1 << 30) - 1);
+            const int cnt = nb_cnt(fl);
             if (kk != kBpKnnMax) {
                 sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
                 continue;
@@ -1799,61 +1814,75 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 continue;
             }
             const double4 a = spt[q];
+            auto d2of = [&](const double4 &p) {
+                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                return ((ex * ex) + (ey * ey)) + (ez * ez);
+            };
             double best[kBpKnnMax];
+            const int ca = nb_near(fl), cb = cnt - ca;
+            nb_load<N>(nbw, q, ca, cb, w);
+            int found;
+            if (all_kept && ca >= kBpKnnMax) {
+                // the near region (d < 0.75 eps) holds >= k points, so the k nearest are among them
+                // (every far entry is farther than >= k near ones): slots 0..19 straight into best with
+                // static register indices (records loaded four at a time), one sort, then the rest of
+                // the region by sorted inserts
+                if (N >= MC_SORT20_MIN_N) {
 #pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-            int found = 0;
-            // count pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = list entry k);
-            // if >= k of them lie inside radius i, the k nearest are among those (every other kept
-            // candidate is farther than >= k others), so only they are inserted: each lane walks its
-            // own mask, and the wave's insert loop runs max-over-lanes of ~k + a few instead of the
-            // largest list
-            unsigned long long m1 = 0, m2 = 0, m3 = 0, mall = 0;
-            {
-                int k = 0;
-                nb_list_pts<N>(nbw, spt, q, MC_ABLATE_BP == 4 ? 0 : cnt, [&](const double4 &p) {
-                    const unsigned long long bit = 1ull << k;
-                    k++;
-                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) return;
-                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                    const double d2 = ((ex * ex) + (ey * ey)) + (ez * ez);
-                    mall |= bit;
-                    if (d2 < pr.knn_r2[0]) m1 |= bit;
-                    if (d2 < pr.knn_r2[1]) m2 |= bit;
-                    if (d2 < pr.knn_r2[2]) m3 |= bit;
-                });
-            }
-            found = __popcll(mall);
-            unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
-            if (found >= kk) {
-                const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // entry k: lst[(k / 8) * 8 * N + k % 8]
-                auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)]); };
-                int k = pm ? __ffsll(static_cast<long long>(pm)) - 1 : 0;
-                double4 nxt = pm ? spt[entry(k)] : make_double4(0.0, 0.0, 0.0, 0.0);
-                if (kk == kBpKnnMax && MC_ABLATE_BP != 3 && N >= MC_SORT20_MIN_N) {
-                    // pm holds >= 20 candidates: the first 20 straight into best, one sort
+                    for (int i0 = 0; i0 < kBpKnnMax; i0 += 4) {
+                        double4 p[4];
 #pragma unroll
-                    for (int i = 0; i < kBpKnnMax; i++) {
-                        pm &= pm - 1;
-                        const double4 p = nxt;
-                        if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
-                        const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                        best[i] = ((ex * ex) + (ey * ey)) + (ez * ez);
+                        for (int u = 0; u < 4; u++) p[u] = spt[nb_ent(w, i0 + u) & kNbPos];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) best[i0 + u] = d2of(p[u]);
                     }
                     sort20(best);
+                } else {  // (the network's registers spill in the 4- and 2-workgroup-per-CU classes)
+#pragma unroll
+                    for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+#pragma unroll
+                    for (int i0 = 0; i0 < kBpKnnMax; i0 += 2) {
+                        const double4 p0 = spt[nb_ent(w, i0) & kNbPos], p1 = spt[nb_ent(w, i0 + 1) & kNbPos];
+                        sorted_insert(best, d2of(p0));
+                        sorted_insert(best, d2of(p1));
+                    }
                 }
-                while (pm) {
-                    pm &= pm - 1;
-                    const double4 p = nxt;
-                    if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
-                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                    if (MC_ABLATE_BP == 3) best[0] += ((ex * ex) + (ey * ey)) + (ez * ez);
-                    else sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+                if (ca > kBpKnnMax) {
+                    double4 nx = spt[nb_ent(w, kBpKnnMax) & kNbPos];
+#pragma unroll 1
+                    for (int k = kBpKnnMax; k < ca; k++) {
+                        const double4 p = nx;
+                        if (k + 1 < ca) nx = spt[nb_ent(w, k + 1) & kNbPos];
+                        sorted_insert(best, d2of(p));
+                    }
                 }
+                found = ca;
+            } else {
+                // selection pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = slot k),
+                // from the entries' radius classes; if >= k of them lie inside radius i, the k nearest
+                // are among those, so only they are inserted (kept flags: bit 30 of sflag, the next
+                // one loaded ahead; none needed when the class filter kept every point)
+                unsigned long long m1 = 0, m2 = 0, m3 = 0, mall = 0;
+                nb_walk(w, ca, cb, [&](unsigned e) { return all_kept ? 1 << 30 : sflag[e & kNbPos]; },
+                        [&](int k, unsigned e, int f) {
+                            const unsigned long long bit = (f & (1 << 30)) ? 1ull << k : 0ull;
+                            const unsigned c = e >> 14;
+                            mall |= bit;
+                            m1 |= c == 0u ? bit : 0ull;
+                            m2 |= c <= 1u ? bit : 0ull;
+                            m3 |= c <= 2u ? bit : 0ull;
+                        });
+                found = __popcll(mall);
+                const unsigned long long pm =
+                    __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
+#pragma unroll
+                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+                if (found >= kk)
+                    nb_walk(w, ca, cb, [&](unsigned e) { return spt[e & kNbPos]; },
+                            [&](int k, unsigned, const double4 &p) {
+                                if ((pm >> k) & 1ull) sorted_insert(best, d2of(p));
+                            });
             }
-#if MC_ABLATE_BP == 3 || MC_ABLATE_BP == 4
-            found = kk;
-#endif
 #ifdef MC_BP_STAMPS
             atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
             atomicAdd(&g_bp_stamps[13], 1ull);
@@ -1941,21 +1970,33 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         __syncthreads();
         BP_STAMP(26);
-        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate), by wave 0:
-        //     64 values per step are read at once, then added in order (lane reads are scalar)
-        if (wv == 0) {
-            double mean = 0.0, sq = 0.0;
-            for (int r0 = 0; r0 < m; r0 += 64) {
-                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;  // 0 adds nothing below
-                mean = seq_add64_pos(mean, v);
-            }
-            mean = mean / static_cast<double>(m);
-            for (int r0 = 0; r0 < m; r0 += 64) {
-                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;
-                sq = seq_add64_pos(sq, v > 0 ? (v - mean) * (v - mean) : 0.0);
-            }
+        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate, positive values
+        //     only), by one lane: eight values are loaded ahead of their eight dependent adds (a
+        //     wave-wide form reads every value through v_readlane, about 3x the time per add)
+        if (t == 0) {
+            auto seq = [&](auto term) {
+                double acc = 0.0;
+                int r = 0;
+                for (; r + 8 <= m; r += 8) {
+                    double v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) v[u] = savg[r + u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const double x = term(v[u]);
+                        if (x > 0) acc = acc + x;
+                    }
+                }
+                for (; r < m; r++) {
+                    const double x = term(savg[r]);
+                    if (x > 0) acc = acc + x;
+                }
+                return acc;
+            };
+            const double mean = seq([](double v) { return v; }) / static_cast<double>(m);
+            const double sq = seq([&](double v) { return v > 0 ? (v - mean) * (v - mean) : 0.0; });
             const double sd = sqrt(sq / static_cast<double>(m - 1));
-            if (lane == 0) s_thr = mean + pr.std_ratio * sd;
+            s_thr = mean + pr.std_ratio * sd;
         }
         __syncthreads();
         const double thr = s_thr;
