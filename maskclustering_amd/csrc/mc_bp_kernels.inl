@@ -621,6 +621,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the points are read by any wave in 4.
         block_minmax3_nw<NW>(mn, mx, red);
         double vmin[3];
 #pragma unroll
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             }
             if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
         }
-        __syncthreads();
+        sync_global();  // 4. reads the lists other waves wrote
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
         for (int v = t; v < (MC_ABLATE_VX ? 0 : nv); v += kVxT) {
             const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
                 }
                 if (ld_agent(&hv[e]) < 0) atomicMin(&hf[e], k);
             }
-            __syncthreads();
+            sync_global();
             const bool first = valid && ld_agent(&hv[e]) < 0 && ld_agent(&hf[e]) == k;
             int tot;
             const int pos = block_excl_scan<256>(first ? 1 : 0, ws, tot);
@@ -863,12 +864,12 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
                 ac[4 * v + 2] = 0.0;
                 ac[4 * v + 3] = 0.0;
             }
-            __syncthreads();
+            sync_global();
             const int vid = valid ? ld_agent(&hv[e]) : -1;
             sp[3 * t] = p[0];
             sp[3 * t + 1] = p[1];
             sp[3 * t + 2] = p[2];
-            __syncthreads();
+            sync_global();
             // group lanes by voxel (ballots only), then every group leader of the wave adds its
             // group's points in lane order to the running sum at once (one round trip per wave)
             unsigned long long gm = 0;
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
                     ac[4 * vid + 2] = az;
                     ac[4 * vid + 3] = an;
                 }
-                __syncthreads();
+                sync_global();
             }
             nv += tot;
         }
@@ -917,7 +918,7 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
             st_agent(&hf[e], INT_MAX);
         }
         if (t == 0) slot_nv[s] = nv;
-        __syncthreads();
+        sync_global();
     }
 }
 
@@ -981,41 +982,6 @@ __device__ __forceinline__ void sorted_insert(V (&a)[N], V v)
 #pragma unroll
     for (int q = N - 1; q > 0; q--) a[q] = ins_min(a[q], ins_max(a[q - 1], v));
     a[0] = ins_min(a[0], v);
-}
-
-// ascending sort of 20 values in registers: Batcher's odd-even merge sort of 32 inputs with the
-// comparators that touch inputs 20..31 removed (those would only ever hold +inf), 101 min / max
-// pairs (scripts/gen_sort20.py); the k-NN fills its first 20 candidates this way instead of by
-// 20 sorted inserts (the multiset sorts to the same array by any method)
-__device__ __forceinline__ void bp_ce(double &x, double &y)
-{
-    const double lo = __builtin_fmin(x, y);
-    y = __builtin_fmax(x, y);
-    x = lo;
-}
-__device__ __forceinline__ void sort20(double (&a)[20])
-{
-    bp_ce(a[0], a[1]); bp_ce(a[2], a[3]); bp_ce(a[0], a[2]); bp_ce(a[1], a[3]); bp_ce(a[1], a[2]);
-    bp_ce(a[4], a[5]); bp_ce(a[6], a[7]); bp_ce(a[4], a[6]); bp_ce(a[5], a[7]); bp_ce(a[5], a[6]);
-    bp_ce(a[0], a[4]); bp_ce(a[2], a[6]); bp_ce(a[2], a[4]); bp_ce(a[1], a[5]); bp_ce(a[3], a[7]);
-    bp_ce(a[3], a[5]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]); bp_ce(a[8], a[9]);
-    bp_ce(a[10], a[11]); bp_ce(a[8], a[10]); bp_ce(a[9], a[11]); bp_ce(a[9], a[10]); bp_ce(a[12], a[13]);
-    bp_ce(a[14], a[15]); bp_ce(a[12], a[14]); bp_ce(a[13], a[15]); bp_ce(a[13], a[14]); bp_ce(a[8], a[12]);
-    bp_ce(a[10], a[14]); bp_ce(a[10], a[12]); bp_ce(a[9], a[13]); bp_ce(a[11], a[15]); bp_ce(a[11], a[13]);
-    bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[0], a[8]); bp_ce(a[4], a[12]);
-    bp_ce(a[4], a[8]); bp_ce(a[2], a[10]); bp_ce(a[6], a[14]); bp_ce(a[6], a[10]); bp_ce(a[2], a[4]);
-    bp_ce(a[6], a[8]); bp_ce(a[10], a[12]); bp_ce(a[1], a[9]); bp_ce(a[5], a[13]); bp_ce(a[5], a[9]);
-    bp_ce(a[3], a[11]); bp_ce(a[7], a[15]); bp_ce(a[7], a[11]); bp_ce(a[3], a[5]); bp_ce(a[7], a[9]);
-    bp_ce(a[11], a[13]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]); bp_ce(a[7], a[8]);
-    bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[16], a[17]); bp_ce(a[18], a[19]);
-    bp_ce(a[16], a[18]); bp_ce(a[17], a[19]); bp_ce(a[17], a[18]); bp_ce(a[0], a[16]); bp_ce(a[8], a[16]);
-    bp_ce(a[4], a[8]); bp_ce(a[12], a[16]); bp_ce(a[2], a[18]); bp_ce(a[10], a[18]); bp_ce(a[6], a[10]);
-    bp_ce(a[14], a[18]); bp_ce(a[2], a[4]); bp_ce(a[6], a[8]); bp_ce(a[10], a[12]); bp_ce(a[14], a[16]);
-    bp_ce(a[1], a[17]); bp_ce(a[9], a[17]); bp_ce(a[5], a[9]); bp_ce(a[13], a[17]); bp_ce(a[3], a[19]);
-    bp_ce(a[11], a[19]); bp_ce(a[7], a[11]); bp_ce(a[15], a[19]); bp_ce(a[3], a[5]); bp_ce(a[7], a[9]);
-    bp_ce(a[11], a[13]); bp_ce(a[15], a[17]); bp_ce(a[1], a[2]); bp_ce(a[3], a[4]); bp_ce(a[5], a[6]);
-    bp_ce(a[7], a[8]); bp_ce(a[9], a[10]); bp_ce(a[11], a[12]); bp_ce(a[13], a[14]); bp_ce(a[15], a[16]);
-    bp_ce(a[17], a[18]);
 }
 
 // union-find over a workgroup's LDS parent array (root = smallest index)
@@ -1167,6 +1133,25 @@ __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks
 #define BP_STAMP(k) do { } while (0)
 #endif
 
+// acc + v(lane 0) + v(lane 1) + ... + v(lane 63), in lane order, skipping lanes with v <= 0 (a
+// std::accumulate step over 64 values); the lane values are read as scalars
+__device__ __forceinline__ double seq_add64_pos(double acc, double v)
+{
+    const long long bits = __double_as_longlong(v);
+    const int lo = static_cast<int>(bits), hi = static_cast<int>(bits >> 32);
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const unsigned long long b = (static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readlane(hi, j))) << 32) |
+                                     static_cast<unsigned>(__builtin_amdgcn_readlane(lo, j));
+        const double a = __longlong_as_double(static_cast<long long>(b));
+        if (a > 0) acc = acc + a;
+    }
+    return acc;
+}
+
+#ifndef MC_DBG_CHECK
+#define MC_DBG_CHECK 0
+#endif
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
 constexpr int kBpLdsN = 16384;  // largest class of the LDS-kernel template
@@ -1317,15 +1302,14 @@ __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, in
 // lines), and a point's whole list (<= 64 slots) is 8 uint4 loads issued before the first is used.
 // An entry is the neighbour's sorted position (14 bits: N <= 16384) and, in the top two bits, its
 // k-NN radius class: 0 / 1 / 2 = inside knn_r2[0 / 1 / 2] (0.6 / 0.75 / 0.9 eps), 3 = the rest of
-// the eps ball.  Two regions: the near entries (class <= 1) fill slots 0, 1, .. upward, the far ones
-// slots 63, 62, .. downward, so that the near set is a prefix: when it holds >= k points (the common
-// case) the k-NN takes its candidates from it with static register indices, no selection pass.
-// sflag[q] = count (bits 0-14, self included) | near count (bits 15-21) | kept (bit 30).
+// the eps ball; the k-NN's candidate selection reads the classes instead of recomputing distances.
+// sflag[q] = count (bits 0-14, self included) | kept (bit 30).
+// (Measured and not kept: the near entries in a prefix region of their own, so that the k-NN of a
+// point with >= k near entries reads them with static register indices: C3 denoise +4 %, C2 +5 %.)
 constexpr unsigned kNbPos = 0x3FFFu;
 constexpr int kNbCnt = 0x7FFF;
 static_assert(kBpLdsN <= 16384, "sorted positions fit 14 bits, counts 15 bits");
 __device__ __forceinline__ int nb_cnt(int f) { return f & kNbCnt; }
-__device__ __forceinline__ int nb_near(int f) { return (f >> 15) & 0x7F; }
 template <int N>
 __device__ __forceinline__ void nb_put(unsigned short *__restrict__ nbw, int q, int k, unsigned e)
 {
@@ -1337,13 +1321,12 @@ __device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
 }
 
 // The eps-neighbour list of sorted position q (point a, cell (x, y, z)): every point of the 27 cells
-// with d2 < eps2 (self included), in cell-walk order within each region.  One predicate per
-// candidate (cell key and distance together, the record loaded whole) and one store; once the two
-// regions meet the entries are counted only (more than kBpNbCap: the point walks its cells).
-// Returns (count, near count).
+// with d2 < eps2 (self included), in cell-walk order.  One predicate per candidate (cell key and
+// distance together, the record loaded whole) and one store; entries past kBpNbCap overwrite the
+// last slot (the list is unused then: the point walks its cells).  Returns the count.
 template <int N>
-__device__ __forceinline__ int2 lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                             const BpDev &pr, unsigned short *__restrict__ nbw, int q)
+__device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
+                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
@@ -1353,16 +1336,13 @@ __device__ __forceinline__ int2 lds_eps_list(const BpLdsGrid &g, int x, int y, i
         return make_int2(g.bs[b], g.bs[b + 1]);
     };
     const double eps2 = pr.eps2;
-    int ca = 0, cb = 0;
+    int cnt = 0;
     auto visit = [&](const double4 &p, int q2, unsigned long long key) {
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
         if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
-            const unsigned c = nb_class(d2, pr);
-            const bool nearc = c <= 1u;
-            if (ca + cb < kBpNbCap) nb_put<N>(nbw, q, nearc ? ca : kBpNbCap - 1 - cb, static_cast<unsigned>(q2) | (c << 14));
-            ca += nearc ? 1 : 0;
-            cb += nearc ? 0 : 1;
+            nb_put<N>(nbw, q, min(cnt, kBpNbCap - 1), static_cast<unsigned>(q2) | (nb_class(d2, pr) << 14));
+            cnt++;
         }
     };
     unsigned long long nkey = 0;
@@ -1381,20 +1361,65 @@ __device__ __forceinline__ int2 lds_eps_list(const BpLdsGrid &g, int x, int y, i
         }
         if (q2 < e) visit(g.pt[q2], q2, key);
     }
-    return make_int2(ca + cb, ca);
+    return cnt;
 }
 
-// the uint4 words of sorted position q's list that hold its two regions (slots [0, ca) and
-// [64 - cb, 64)), all issued together; the other words are zero
+// The same lists built from each unordered pair once (classes whose counts live in LDS): sorted
+// position q visits the points of its own cell at later positions and the 13 cells after its own in
+// (z, y, x) order; a pair within eps is appended to both lists, each at the slot an LDS atomic on its
+// counter returns (sflag[] holds the counts, self entries already in slot 0).  Half the candidate
+// records of lds_eps_list; the slot order within a list is arbitrary, which no consumer depends on
+// (the union and the border labels are order-free, the k-NN sorts).
 template <int N>
-__device__ __forceinline__ void nb_load(const unsigned short *__restrict__ nbw, int q, int ca, int cb, unsigned (&w)[32])
+__device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
+                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag)
+{
+    auto range = [&](int d, unsigned long long &key) {
+        const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
+        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        key = pack3(cx, cy, cz);
+        const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
+        return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
+    };
+    const double eps2 = pr.eps2;
+    auto visit = [&](const double4 &p, int q2, unsigned long long key) {
+        const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
+        const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
+        if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
+            const unsigned c = nb_class(d2, pr) << 14;
+            const int o1 = atomicAdd(&sflag[q], 1), o2 = atomicAdd(&sflag[q2], 1);
+            if (o1 < kBpNbCap) nb_put<N>(nbw, q, o1, static_cast<unsigned>(q2) | c);
+            if (o2 < kBpNbCap) nb_put<N>(nbw, q2, o2, static_cast<unsigned>(q) | c);
+        }
+    };
+    unsigned long long nkey = 0;
+    int2 nr = range(13, nkey);
+#pragma unroll 1
+    for (int d = 13; d < 27; d++) {
+        const unsigned long long key = nkey;
+        const int2 r = nr;
+        if (d + 1 < 27) nr = range(d + 1, nkey);
+        int q2 = r.x;
+        const int e = r.y;
+        for (; q2 + 2 <= e; q2 += 2) {
+            const double4 p0 = g.pt[q2], p1 = g.pt[q2 + 1];
+            visit(p0, q2, key);
+            visit(p1, q2 + 1, key);
+        }
+        if (q2 < e) visit(g.pt[q2], q2, key);
+    }
+}
+
+// the uint4 words of sorted position q's first cnt slots, all issued together; the others zero
+template <int N>
+__device__ __forceinline__ void nb_load(const unsigned short *__restrict__ nbw, int q, int cnt, unsigned (&w)[32])
 {
     static_assert(kBpNbCap == 64, "eight uint4 per point");
     const uint4 *row = reinterpret_cast<const uint4 *>(nbw) + q;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (8 * u < ca || 8 * u + 8 > kBpNbCap - cb) v = row[static_cast<size_t>(u) * N];
+        if (8 * u < cnt) v = row[static_cast<size_t>(u) * N];
         w[4 * u] = v.x;
         w[4 * u + 1] = v.y;
         w[4 * u + 2] = v.z;
@@ -1407,33 +1432,21 @@ __device__ __forceinline__ unsigned nb_ent(const unsigned (&w)[32], int k)
     return (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
 }
 
-// fn(k, entry, pre(entry)) for the slots of both regions, near region upward then far region
-// downward; pre(entry of the next slot) is issued before fn runs on this one (its loads overlap fn).
-// The slot index is the same in every active lane (lanes only leave), so each region's loop keeps
-// one copy of fn's code and reads the words with uniform register indices.
+// fn(k, entry, pre(entry)) for slots 0 .. cnt - 1; pre(entry of the next slot) is issued before fn
+// runs on this one (its loads overlap fn).  The slot index is the same in every active lane (lanes
+// only leave), so the loop keeps one copy of fn's code and reads the words with uniform register
+// indices (unrolled copies of a 20-step insertion overflow the instruction cache).
 template <typename Pre, typename Fn>
-__device__ __forceinline__ void nb_walk(const unsigned (&w)[32], int ca, int cb, Pre &&pre, Fn &&fn)
+__device__ __forceinline__ void nb_walk(const unsigned (&w)[32], int cnt, Pre &&pre, Fn &&fn)
 {
-    if (ca > 0) {
-        auto nx = pre(nb_ent(w, 0));
+    if (cnt <= 0) return;
+    auto nx = pre(nb_ent(w, 0));
 #pragma unroll 1
-        for (int k = 0; k < ca; k++) {
-            const auto cur = nx;
-            const unsigned e = nb_ent(w, k);
-            if (k + 1 < ca) nx = pre(nb_ent(w, k + 1));
-            fn(k, e, cur);
-        }
-    }
-    if (cb > 0) {
-        auto nx = pre(nb_ent(w, kBpNbCap - 1));
-#pragma unroll 1
-        for (int j = 0; j < cb; j++) {
-            const int k = kBpNbCap - 1 - j;
-            const auto cur = nx;
-            const unsigned e = nb_ent(w, k);
-            if (j + 1 < cb) nx = pre(nb_ent(w, k - 1));
-            fn(k, e, cur);
-        }
+    for (int k = 0; k < cnt; k++) {
+        const auto cur = nx;
+        const unsigned e = nb_ent(w, k);
+        if (k + 1 < cnt) nx = pre(nb_ent(w, k + 1));
+        fn(k, e, cur);
     }
 }
 
@@ -1487,10 +1500,6 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 #ifndef MC_KNN_RING
 #define MC_KNN_RING 1  // 0: points whose eps list holds < k kept points skip the grid rings (whole-cloud scan)
 #endif
-#ifndef MC_SORT20_MIN_N
-#define MC_SORT20_MIN_N 2048  // size classes below this fill the k-NN by sorted inserts only (the
-                               // network's registers spill in the 4- and 2-workgroup-per-CU classes)
-#endif
 #ifndef MC_ABLATE_BP
 #define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union
 #endif
@@ -1509,6 +1518,11 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     constexpr int kFbCount = 2 * N + 1;  // index of the fallback counter in sB
     constexpr int NL = kLean ? 1 : N;    // extent of the arrays a lean class keeps in global scratch
     constexpr bool kLean3 = kBpLean3<N>;
+    // a lean class hands its global-scratch arrays between waves at every barrier (sync_global)
+    auto bar = []() {
+        if constexpr (kLean) sync_global();
+        else __syncthreads();
+    };
     __shared__ double4 spt_l[kLean3 ? 1 : N];  // cell-sorted points + cell keys
     __shared__ int sA_l[kLean3 ? 1 : NBK * N + 1];  // bucket starts
     __shared__ int sB_l[2 * NL + 2];     // bucket counts; then min original index per root [0, n) +
@@ -1553,9 +1567,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     // through it reaches block barriers, but the loop must not depend on the body's structure).
     while (true) {
         if (t == 0) s_slot = atomicAdd(ticket, 1);
-        __syncthreads();
+        bar();
         const int tk = s_slot;
-        __syncthreads();
+        bar();
         if (tk >= cnt_cls) break;
         const int s = cls_list[tk];
         const int base = slot_pix[s], n = slot_nv[s];
@@ -1586,7 +1600,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         BP_STAMP(17);
         // 2. bucket counts
         for (int b = t; b < NBK * n; b += T) sB[b] = 0;
-        __syncthreads();
+        bar();
         for (int i = t; i < n; i += T) {
             int c3[3];
 #pragma unroll
@@ -1595,7 +1609,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             sX[i] = static_cast<int>(b);
             atomicAdd(&sB[b], 1);
         }
-        __syncthreads();
+        bar();
         BP_STAMP(18);
         // 3. bucket starts
         {
@@ -1610,7 +1624,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             }
             if (t == 0) sA[NBK * n] = carry;
         }
-        __syncthreads();
+        bar();
         BP_STAMP(19);
         // 4. counting-sort scatter into LDS (bucket counters return to zero)
         for (int i = t; i < n; i += T) {
@@ -1624,24 +1638,39 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             sorig[q] = static_cast<short>(i);
             spos[i] = static_cast<short>(q);
         }
-        __syncthreads();
+        bar();
         auto keyof = [&](int q) { return static_cast<unsigned long long>(__double_as_longlong(spt[q].w)); };
         BP_STAMP(20);
-        // 5. eps-neighbour counts (self included) and lists
-        for (int q = t; q < n; q += T) {
-            int x, y, z;
-            unpack3(keyof(q), x, y, z);
-            const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-            const int2 c2 = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
-            sflag[q] = c2.x | (min(c2.y, kBpNbCap) << 15);
-            spar[q] = q;
+        // 5. eps-neighbour counts (self included) and lists: from each pair once where the counts
+        //    live in LDS, by a full 27-cell walk per point where they are global scratch
+        if constexpr (!kBpLean2<N>) {
+            for (int q = t; q < n; q += T) {
+                sflag[q] = 1;
+                nb_put<N>(nbw, q, 0, static_cast<unsigned>(q));  // self, class 0
+                spar[q] = q;
+            }
+            bar();
+            for (int q = t; q < n; q += T) {
+                int x, y, z;
+                unpack3(keyof(q), x, y, z);
+                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag);
+            }
+            sync_global();  // the lists hold other waves' stores
+        } else {
+            for (int q = t; q < n; q += T) {
+                int x, y, z;
+                unpack3(keyof(q), x, y, z);
+                const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
+                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
+                spar[q] = q;
+            }
         }
-        __syncthreads();
+        bar();
         BP_STAMP(21);
         // 6. connected core points: list points first; points with more than kBpNbCap neighbours
         //    are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
         if (t == 0) s_ndef = 0;
-        __syncthreads();
+        bar();
         for (int q = t; q < n; q += T) {
             const int fl = sflag[q], cnt = nb_cnt(fl);
             if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
@@ -1650,11 +1679,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 continue;
             }
             int ra = uf_find_s(spar, q);
-            const int ca = nb_near(fl);
-            nb_load<N>(nbw, q, ca, cnt - ca, w);
+            nb_load<N>(nbw, q, cnt, w);
             // the next entry's count and union-find parent are loaded before this one's find (a parent
             // read early is still a node of q2's component, so it is a valid place to start the find)
-            nb_walk(w, ca, cnt - ca,
+            nb_walk(w, cnt,
                     [&](unsigned e) { return make_int2(sflag[e & kNbPos], ld_wg(spar + (e & kNbPos))); },
                     [&](int, unsigned e, int2 fp) {
                         const int q2 = static_cast<int>(e & kNbPos);
@@ -1667,7 +1695,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         }
                     });
         }
-        __syncthreads();
+        bar();
         for (int f = t; f < s_ndef; f += T) {
             const int q = sX[f];
             int x, y, z;
@@ -1684,7 +1712,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 }
             });
         }
-        __syncthreads();
+        bar();
         BP_STAMP(22);
         // 7. roots; every component keyed by its smallest original index; clusters ranked by it
         {
@@ -1694,7 +1722,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 const int q = t + k * T;
                 rq[k] = (q < n && nb_cnt(sflag[q]) >= pr.minpts) ? uf_find_s(spar, q) : -1;
             }
-            __syncthreads();
+            bar();
             for (int q = t; q < n; q += T) sB[q] = INT_MAX;
             for (int x = t; x <= n; x += T) ccnt[x] = 0;
 #pragma unroll
@@ -1702,10 +1730,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 const int q = t + k * T;
                 if (q < n) spar[q] = rq[k];
             }
-            __syncthreads();
+            bar();
             for (int q = t; q < n; q += T)
                 if (spar[q] >= 0) atomicMin(&sB[spar[q]], static_cast<int>(sorig[q]));
-            __syncthreads();
+            bar();
             int carry = 0;
             for (int i0 = 0; i0 < n; i0 += T) {
                 const int i = i0 + t;
@@ -1720,7 +1748,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 carry += tot;
             }
         }
-        __syncthreads();
+        bar();
         BP_STAMP(23);
         // 8. labels and class counts (a border point joins the adjacent cluster of smallest key)
         for (int q = t; q < n; q += T) {
@@ -1728,7 +1756,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             if (spar[q] >= 0) {
                 l = sX[spar[q]];
             } else {
-                const int fl = sflag[q], cnt = nb_cnt(fl);
+                const int cnt = nb_cnt(sflag[q]);
                 int best = INT_MAX, broot = -1;
                 auto near = [&](int q2) {
                     const int r2 = spar[q2];
@@ -1738,9 +1766,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     }
                 };
                 if (cnt <= kBpNbCap) {
-                    const int ca = nb_near(fl);
-                    nb_load<N>(nbw, q, ca, cnt - ca, w);
-                    nb_walk(w, ca, cnt - ca, [](unsigned e) { return e; },
+                    nb_load<N>(nbw, q, cnt, w);
+                    nb_walk(w, cnt, [](unsigned e) { return e; },
                             [&](int, unsigned e, unsigned) { near(static_cast<int>(e & kNbPos)); });
                 } else {
                     int x, y, z;
@@ -1755,7 +1782,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             slab[q] = l;
             atomicAdd(&ccnt[l + 1], 1);
         }
-        __syncthreads();
+        bar();
         BP_STAMP(24);
         // 9. class filter; S in original index order; kept rank per sorted position
         const double lim = pr.frac * static_cast<double>(n);
@@ -1764,7 +1791,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 sflag[q] |= 1 << 30;
                 spt[q].w = __longlong_as_double(static_cast<long long>(keyof(q) | kKeptBit));
             }
-        __syncthreads();
+        bar();
         int m = 0;
         for (int i0 = 0; i0 < n; i0 += T) {
             const int i = i0 + t;
@@ -1777,9 +1804,16 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             }
             m += tot;
         }
-        __syncthreads();
+        bar();
         BP_STAMP(25);
         const bool all_kept = m == n;
+#if MC_DBG_CHECK
+        __shared__ int s_dbg_m;
+        if (t == 0) s_dbg_m = m;
+        for (int r = t; r < m; r += T) savg[r] = -7.0;
+        bar();
+        if (s_dbg_m != m) printf("DBG m mismatch N=%d s=%d t=%d m=%d m0=%d\n", N, s, t, m, s_dbg_m);
+#endif
         // 10. k nearest kept points: the eps list when it holds >= k kept points; else (deferred to a
         //     compacted pass, so that few waves walk cells) grid rings up to R = 2; else (sparse
         //     point, or m < k) all of S, by a whole wave or one lane per point
@@ -1789,7 +1823,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             sfb[kFbCount] = 0;
             s_ndef = 0;
         }
-        __syncthreads();
+        bar();
         auto put_mean = [&](int r, const double(&best)[kBpKnnMax]) {
             double sum = 0.0;
 #pragma unroll
@@ -1819,69 +1853,41 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 return ((ex * ex) + (ey * ey)) + (ez * ez);
             };
             double best[kBpKnnMax];
-            const int ca = nb_near(fl), cb = cnt - ca;
-            nb_load<N>(nbw, q, ca, cb, w);
-            int found;
-            if (all_kept && ca >= kBpKnnMax) {
-                // the near region (d < 0.75 eps) holds >= k points, so the k nearest are among them
-                // (every far entry is farther than >= k near ones): slots 0..19 straight into best with
-                // static register indices (records loaded four at a time), one sort, then the rest of
-                // the region by sorted inserts
-                if (N >= MC_SORT20_MIN_N) {
 #pragma unroll
-                    for (int i0 = 0; i0 < kBpKnnMax; i0 += 4) {
-                        double4 p[4];
-#pragma unroll
-                        for (int u = 0; u < 4; u++) p[u] = spt[nb_ent(w, i0 + u) & kNbPos];
-#pragma unroll
-                        for (int u = 0; u < 4; u++) best[i0 + u] = d2of(p[u]);
-                    }
-                    sort20(best);
-                } else {  // (the network's registers spill in the 4- and 2-workgroup-per-CU classes)
-#pragma unroll
-                    for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-#pragma unroll
-                    for (int i0 = 0; i0 < kBpKnnMax; i0 += 2) {
-                        const double4 p0 = spt[nb_ent(w, i0) & kNbPos], p1 = spt[nb_ent(w, i0 + 1) & kNbPos];
-                        sorted_insert(best, d2of(p0));
-                        sorted_insert(best, d2of(p1));
-                    }
+            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+            // selection pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = slot k),
+            // from the entries' radius classes; if >= k of them lie inside radius i, the k nearest are
+            // among those (every other kept candidate is farther than >= k others), so only they are
+            // inserted: each lane walks its own mask, and the wave's insert loop runs max-over-lanes
+            // of ~k + a few instead of the largest list.  Kept flags (bit 30 of sflag, the next one
+            // loaded ahead) are read only when the class filter dropped points.
+            unsigned long long m1 = 0, m2 = 0, m3 = 0, mall = 0;
+            nb_load<N>(nbw, q, cnt, w);
+            nb_walk(w, cnt, [&](unsigned e) { return all_kept ? 1 << 30 : sflag[e & kNbPos]; },
+                    [&](int k, unsigned e, int f) {
+                        const unsigned long long bit = (f & (1 << 30)) ? 1ull << k : 0ull;
+                        const unsigned c = e >> 14;
+                        mall |= bit;
+                        m1 |= c == 0u ? bit : 0ull;
+                        m2 |= c <= 1u ? bit : 0ull;
+                        m3 |= c <= 2u ? bit : 0ull;
+                    });
+            const int found = __popcll(mall);
+            unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
+            if (found >= kk) {
+                const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
+                auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)] & kNbPos); };
+                // (Not kept: the first 20 candidates straight into best and one 101-comparator sorting
+                // network.  With the pair-built lists its results in the 1024-thread class varied from
+                // run to run although the network sorts every input (0-1 principle, all 2^20 cases);
+                // the sorted inserts alone are exact and as fast with these lists.)
+                double4 nxt = pm ? spt[entry(__ffsll(static_cast<long long>(pm)) - 1)] : make_double4(0.0, 0.0, 0.0, 0.0);
+                while (pm) {
+                    pm &= pm - 1;
+                    const double4 p = nxt;
+                    if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
+                    sorted_insert(best, d2of(p));
                 }
-                if (ca > kBpKnnMax) {
-                    double4 nx = spt[nb_ent(w, kBpKnnMax) & kNbPos];
-#pragma unroll 1
-                    for (int k = kBpKnnMax; k < ca; k++) {
-                        const double4 p = nx;
-                        if (k + 1 < ca) nx = spt[nb_ent(w, k + 1) & kNbPos];
-                        sorted_insert(best, d2of(p));
-                    }
-                }
-                found = ca;
-            } else {
-                // selection pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = slot k),
-                // from the entries' radius classes; if >= k of them lie inside radius i, the k nearest
-                // are among those, so only they are inserted (kept flags: bit 30 of sflag, the next
-                // one loaded ahead; none needed when the class filter kept every point)
-                unsigned long long m1 = 0, m2 = 0, m3 = 0, mall = 0;
-                nb_walk(w, ca, cb, [&](unsigned e) { return all_kept ? 1 << 30 : sflag[e & kNbPos]; },
-                        [&](int k, unsigned e, int f) {
-                            const unsigned long long bit = (f & (1 << 30)) ? 1ull << k : 0ull;
-                            const unsigned c = e >> 14;
-                            mall |= bit;
-                            m1 |= c == 0u ? bit : 0ull;
-                            m2 |= c <= 1u ? bit : 0ull;
-                            m3 |= c <= 2u ? bit : 0ull;
-                        });
-                found = __popcll(mall);
-                const unsigned long long pm =
-                    __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
-#pragma unroll
-                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-                if (found >= kk)
-                    nb_walk(w, ca, cb, [&](unsigned e) { return spt[e & kNbPos]; },
-                            [&](int k, unsigned, const double4 &p) {
-                                if ((pm >> k) & 1ull) sorted_insert(best, d2of(p));
-                            });
             }
 #ifdef MC_BP_STAMPS
             atomicAdd(&g_bp_stamps[29], static_cast<unsigned long long>(found));
@@ -1893,7 +1899,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             }
             put_mean(r, best);
         }
-        __syncthreads();
+        bar();
 #ifdef MC_BP_STAMPS
         if (t == 0) atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(s_ndef));
 #endif
@@ -1933,7 +1939,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             }
             put_mean(r, best);
         }
-        __syncthreads();
+        bar();
         const int nfb = sfb[kFbCount];
         if (nfb > 2 * NW && kk == kBpKnnMax) {
             // many sparse points: one per lane, every kept point scanned in sorted order (the same
@@ -1968,37 +1974,32 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 if (lane == 0) savg[r] = mean;
             }
         }
-        __syncthreads();
+        bar();
         BP_STAMP(26);
-        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate, positive values
-        //     only), by one lane: eight values are loaded ahead of their eight dependent adds (a
-        //     wave-wide form reads every value through v_readlane, about 3x the time per add)
-        if (t == 0) {
-            auto seq = [&](auto term) {
-                double acc = 0.0;
-                int r = 0;
-                for (; r + 8 <= m; r += 8) {
-                    double v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) v[u] = savg[r + u];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        const double x = term(v[u]);
-                        if (x > 0) acc = acc + x;
-                    }
-                }
-                for (; r < m; r++) {
-                    const double x = term(savg[r]);
-                    if (x > 0) acc = acc + x;
-                }
-                return acc;
-            };
-            const double mean = seq([](double v) { return v; }) / static_cast<double>(m);
-            const double sq = seq([&](double v) { return v > 0 ? (v - mean) * (v - mean) : 0.0; });
+#if MC_DBG_CHECK
+        for (int r = t; r < m; r += T)
+            if (!(savg[r] > 0.0) || savg[r] > 1.0) printf("DBG savg N=%d s=%d n=%d m=%d r=%d v=%g nfb=%d\n", N, s, n, m, r, savg[r], nfb);
+        bar();
+#endif
+        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate), by wave 0:
+        //     64 values per step are read at once, then added in order (lane reads are scalar).
+        //     (Measured and not kept: one lane loading eight values ahead of its eight dependent adds,
+        //     30 us per slot against 19.)
+        if (wv == 0) {
+            double mean = 0.0, sq = 0.0;
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;  // 0 adds nothing below
+                mean = seq_add64_pos(mean, v);
+            }
+            mean = mean / static_cast<double>(m);
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;
+                sq = seq_add64_pos(sq, v > 0 ? (v - mean) * (v - mean) : 0.0);
+            }
             const double sd = sqrt(sq / static_cast<double>(m - 1));
-            s_thr = mean + pr.std_ratio * sd;
+            if (lane == 0) s_thr = mean + pr.std_ratio * sd;
         }
-        __syncthreads();
+        bar();
         const double thr = s_thr;
         BP_STAMP(27);
         // 12. survivors -> float32 mask points and their AABB
@@ -2034,8 +2035,12 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 fred[3 * NW + c * NW + wv] = b;
             }
         }
-        __syncthreads();
+        bar();
         BP_STAMP(28);
+#if MC_DBG_CHECK
+        if (ns > m || ns < 0) printf("DBG ns N=%d s=%d t=%d n=%d m=%d ns=%d thr=%g\n", N, s, t, n, m, ns, thr);
+        if (t == 0 && N == 2048) printf("DBG slot N=%d s=%d n=%d m=%d ns=%d thr=%.17g nfb=%d\n", N, s, n, m, ns, thr, nfb);
+#endif
 #ifdef MC_BP_STAMPS
         if (t == 0 && s < (1 << 16)) g_bp_slot_time[s] = static_cast<unsigned>(__builtin_amdgcn_s_memrealtime() - slot_t0);
 #endif
@@ -2053,7 +2058,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 slot_box[6 * s + 3 + c] = b;
             }
         }
-        __syncthreads();
+        bar();
     }
 }
 
@@ -2116,7 +2121,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             atomicAdd(&bc[b], 1);
         }
         for (int i = t; i <= n; i += 256) cc[i] = 0;
-        __syncthreads();
+        sync_global();
         BP_STAMP(2);
         // 3. bucket starts
         {
@@ -2131,14 +2136,14 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             }
             if (t == 0) bs[nb] = carry;
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(3);
         // 4. counting-sort scatter (bucket counters return to zero)
         for (int i = t; i < n; i += 256) {
             const int b = pb[i];
             bl[bs[b] + atomicSub(&bc[b], 1) - 1] = i;
         }
-        __syncthreads();
+        sync_global();
         auto cell_of = [&](int i, int &x, int &y, int &z) {
             const unsigned long long k = pc[i];
             x = static_cast<int>(k >> 42);
@@ -2158,7 +2163,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             if (n <= kBpLdsUF) s_par[i] = i;
             else pa[i] = i;
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(5);
         // 6. connected core points (union-find, root = smallest index)
         for (int i = t; i < n; i += 256) {
@@ -2174,7 +2179,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                     }
                 });
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(6);
         // 7. clusters numbered in order of their smallest point
         {
@@ -2193,7 +2198,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                 carry += tot;
             }
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(7);
         // 8. labels (+1 = the reference's shifted labels, geometry.py:10) and class counts
         for (int i = t; i < n; i += 256) {
@@ -2214,7 +2219,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             lb[i] = l;
             atomicAdd(&cc[l + 1], 1);
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(8);
         // 9. class filter (geometry.py:15-20): the kept set S in index order
         const double lim = pr.frac * static_cast<double>(n);
@@ -2228,12 +2233,12 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
             if (i < n) nc[i] = keep ? (nc[i] | (1 << 30)) : (nc[i] & ~(1 << 30));
             m += tot;
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(9);
         // 10. k nearest kept points: grid rings up to R = 2, then (rare: sparse points) all of S
         const int kk = min(pr.knn, m);
         bp_knn<kBpKnnMax>(g, P, nc, si, m, kk, pr.ce, av, t, s_par, kBpLdsUF, &s_nfb);
-        __syncthreads();
+        sync_global();
         BP_STAMP(10);
         // 11. cloud mean and Bessel std: sequential sums in index order (std::accumulate)
         {
@@ -2242,7 +2247,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                 for (int c0 = 0; c0 < m; c0 += kBpStage) {
                     const int cn = min(kBpStage, m - c0);
                     for (int x = t; x < cn; x += 256) s_avg[x] = av[c0 + x];
-                    __syncthreads();
+                    sync_global();
                     if (t == 0) {
                         for (int x = 0; x < cn; x++) {
                             const double a = s_avg[x];
@@ -2253,7 +2258,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                             }
                         }
                     }
-                    __syncthreads();
+                    sync_global();
                 }
                 if (pass == 0 && t == 0) mean = mean / static_cast<double>(m);
             }
@@ -2262,7 +2267,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                 s_thr = mean + pr.std_ratio * sd;
             }
         }
-        __syncthreads();
+        sync_global();
         const double thr = s_thr;
         BP_STAMP(11);
         // 12. survivors -> float32 mask points (:112) and their float32 AABB (:59-61)
@@ -2298,7 +2303,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                 fred[12 + c * 4 + wv] = b;
             }
         }
-        __syncthreads();
+        sync_global();
         BP_STAMP(12);
         if (t == 0) {
             slot_m[s] = m;
@@ -2310,7 +2315,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
                     fmaxf(fmaxf(fred[12 + c * 4], fred[12 + c * 4 + 1]), fmaxf(fred[12 + c * 4 + 2], fred[12 + c * 4 + 3]));
             }
         }
-        __syncthreads();
+        sync_global();
     }
 }
 

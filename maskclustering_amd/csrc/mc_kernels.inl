@@ -61,6 +61,16 @@ __device__ __forceinline__ int wave_max_i(int v)
 }
 
 // Block-wide exclusive scan for blockDim.x == NT (multiple of 64). `ws` holds NT/64 ints.
+// Workgroup barrier for data handed between waves through GLOBAL memory.  On gfx950 __syncthreads()
+// is s_waitcnt lgkmcnt(0) + s_barrier: a plain global store (or a no-return atomic) of one wave can
+// still be in flight when another wave loads the address after the barrier.  Every wave first waits
+// for its own vector-memory operations (MI355X_MICROARCH.md: intra-workgroup hand-off through memory).
+__device__ __forceinline__ void sync_global()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int *ws, int &total)
 {
@@ -1354,7 +1364,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
         keys[s] = -1;
         cnts[s] = 0;
     }
-    __syncthreads();
+    sync_global();
     for (int a = (blockIdx.x * kPairWaves + wv) * shard_world + shard_rank; a < N;
          a += gridDim.x * kPairWaves * shard_world) {
         if (lane == 0) {
@@ -1487,7 +1497,7 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
     ne = wave_sum(ne);
     if (MC_ABLATE_PAIRS < 4 && lane == 0 && ne)
         spread_add(edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, static_cast<unsigned long long>(ne));
-    __syncthreads();
+    sync_global();
     if (s_novf > 0)  // uniform
         pairs_overflow_local(ow, s_ovf, s_novf, n_off, n_len, pool, coloff, collen, colnodes, nvf, FW, er, parent,
                              edges + static_cast<size_t>(t) * kSpread * kSpreadStrideL, ec, t);
@@ -1684,7 +1694,7 @@ __global__ __launch_bounds__(1024) void k6_components(
     int rk = block_excl_scan<1024>(nr, ws, K);
     for (int i = i0; i < i1; i++)
         if (root[i] == i) rank[i] = rk++;
-    __syncthreads();
+    sync_global();  // root / rank / counters / offsets are read by other waves
     // labels, member counts, row-length upper bounds
     for (int i = t; i < N; i += 1024) {
         const int k = rank[root[i]];
@@ -1693,7 +1703,7 @@ __global__ __launch_bounds__(1024) void k6_components(
         atomicAdd(&memcnt[k], 1);
         atomicAdd(&ublen[k], n_len[i]);
     }
-    __syncthreads();
+    sync_global();  // root / rank / counters / offsets are read by other waves
     // member offsets and next-level row offsets (K + 1 entries each)
     const int pk = (K + 1023) / 1024;
     const int k0 = min(K, t * pk), k1 = min(K, k0 + pk);
@@ -1716,7 +1726,7 @@ __global__ __launch_bounds__(1024) void k6_components(
         *dcap_next = T1;
         *dNn = K;
     }
-    __syncthreads();
+    sync_global();  // root / rank / counters / offsets are read by other waves
     // members of every new node (memcnt returns to zero)
     for (int i = t; i < N; i += 1024) {
         const int k = label[i];

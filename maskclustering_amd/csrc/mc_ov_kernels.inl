@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void k_ov_query(int num_objects, const long lo
         for (long long r = r0 + 1; r < r1; r++) acc = __fadd_rn(acc, feats[static_cast<size_t>(obj_rows[r]) * dim + d]);
         smean[d] = __fdiv_rn(acc, cnt);
     }
-    __syncthreads();
+    sync_global();
     float *sim = sim_scratch + static_cast<size_t>(k) * num_labels;
     // dot products: the BLAS sgemm's summation order is its own; here every product is summed in
     // float64 and rounded once (a few ULP from any float32 order)
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void k_ov_query(int num_objects, const long lo
         for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
         if (lane == 0) sim[l] = static_cast<float>(s);
     }
-    __syncthreads();
+    sync_global();
     // exp(sim * T) in float32, the sum, prob = e / sum, first argmax (NaN counts as the maximum,
     // like np.argmax)
     if (wv == 0) {

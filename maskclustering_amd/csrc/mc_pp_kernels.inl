@@ -57,7 +57,7 @@ __device__ __forceinline__ void pp_block_minmax3(double mn[3], double mx[3], dou
             red[(3 + c) * NW + wv] = hi;
         }
     }
-    __syncthreads();
+    sync_global();
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         mn[c] = red[c * NW];
@@ -67,7 +67,7 @@ __device__ __forceinline__ void pp_block_minmax3(double mn[3], double mx[3], dou
             mx[c] = fmax(mx[c], red[(3 + c) * NW + w]);
         }
     }
-    __syncthreads();
+    sync_global();
 }
 
 // DBSCAN of every node (utils/post_process.py:109): labels -> object index within the node
@@ -108,9 +108,9 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
     const int t = threadIdx.x;
     while (true) {
         if (t == 0) s_k = atomicAdd(ticket, 1);
-        __syncthreads();
+        sync_global();
         const int kk = s_k;
-        __syncthreads();
+        sync_global();
         if (kk >= N) break;
         const int k = order[kk];
         const int64_t e0 = pt_off[k];
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             atomicAdd(&bc[b], 1);
         }
         for (int i = t; i <= n; i += NT) cc[i] = 0;
-        __syncthreads();
+        sync_global();
         // 3. bucket starts
         {
             int carry = 0;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             }
             if (t == 0) bs[nb] = carry;
         }
-        __syncthreads();
+        sync_global();
         // 4. counting-sort scatter (bucket counters return to zero)
         unsigned long long *sk = skey + e0;
         double *sx = sxyz + 3 * e0;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
 #pragma unroll
             for (int c = 0; c < 3; c++) sx[3 * q + c] = P[3 * i + c];
         }
-        __syncthreads();
+        sync_global();
         auto cell_of = [&](int i, int &x, int &y, int &z) { unpack3(pc[i], x, y, z); };
         // 5. eps-neighbour counts, self included (nanoflann radius search: d2 < eps^2)
         for (int i = t; i < n; i += NT) {
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             if (n <= kPPLdsUF) s_par[i] = i;
             else pa[i] = i;
         }
-        __syncthreads();
+        sync_global();
         // 6. core points connected within eps: union-find, root = smallest index
         for (int i = t; i < n; i += NT) {
             if (nc[i] < pr.minpts) continue;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
                 }
             });
         }
-        __syncthreads();
+        sync_global();
         // 7. clusters numbered by their smallest core point (Open3D seeds in index order)
         int ncl;
         {
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             }
             ncl = carry;
         }
-        __syncthreads();
+        sync_global();
         // 8. labels: a border point joins the first cluster that reaches it = the adjacent cluster
         //    of smallest number; class = label + 1 (post_process.py:109)
         for (int i = t; i < n; i += NT) {
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             lb[i] = l + 1;
             atomicAdd(&cc[l + 1], 1);
         }
-        __syncthreads();
+        sync_global();
         // 9. objects = non-empty classes (:115-118): the noise class only when it is non-empty;
         //    object = class - shift
         if (t == 0) {
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(NT) void k_pp_dbscan(
             nob[k] = ncl + noise;
             nsh[k] = 1 - noise;
         }
-        __syncthreads();
+        sync_global();
     }
 }
 
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(NT) void k_pp_big_grid(int nbig, const int *__restr
             pa[i] = i;
         }
         for (int i = t; i <= n; i += NT) cc[i] = 0;
-        __syncthreads();
+        sync_global();
         int carry = 0;
         for (int b0 = 0; b0 < static_cast<int>(nb); b0 += NT) {
             const int h = b0 + t;
@@ -327,12 +327,12 @@ __global__ __launch_bounds__(NT) void k_pp_big_grid(int nbig, const int *__restr
             carry += tot;
         }
         if (t == 0) bs[nb] = carry;
-        __syncthreads();
+        sync_global();
         for (int i = t; i < n; i += NT) {
             const int h = pb[i];
             bl[bs[h] + atomicSub(&bc[h], 1) - 1] = i;
         }
-        __syncthreads();
+        sync_global();
     }
 }
 
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(NT) void k_pp_big_label(int nbig, const int *__rest
             carry += tot;
         }
         const int ncl = carry;
-        __syncthreads();
+        sync_global();
         for (int i = t; i < n; i += NT) {
             int l;
             if (nc[i] >= pr.minpts) {
@@ -416,13 +416,13 @@ __global__ __launch_bounds__(NT) void k_pp_big_label(int nbig, const int *__rest
             lb[i] = l + 1;
             atomicAdd(&cc[l + 1], 1);
         }
-        __syncthreads();
+        sync_global();
         if (t == 0) {
             const int noise = ld_agent(&cc[0]) > 0 ? 1 : 0;
             nob[k] = ncl + noise;
             nsh[k] = 1 - noise;
         }
-        __syncthreads();
+        sync_global();
     }
 }
 
@@ -461,9 +461,9 @@ __global__ __launch_bounds__(256) void k_pp_filter(
     int *pm = posmap + static_cast<int64_t>(blockIdx.x) * P;
     while (true) {
         if (t == 0) s_k = atomicAdd(ticket, 1);
-        __syncthreads();
+        sync_global();
         const int kk = s_k;
-        __syncthreads();
+        sync_global();
         if (kk >= N) break;
         const int k = order[kk];
         const int64_t e0 = pt_off[k];
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k_pp_filter(
             for (int w = 0; w < FW; w++) c += __popcll(pfm[static_cast<int64_t>(p) * FW + w] & vf[w]);
             cvid[e0 + i] = c;
         }
-        __syncthreads();
+        sync_global();
         // 2. masks of the node, a wave each (:68-81): frame bits of the points they hold, and the
         //    object of largest intersection
         const int64_t q0 = qoff[k], q1 = qoff[k + 1];
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void k_pp_filter(
                 if (best >= 0) atomicAdd(&obj_nmask[ob + best], 1);
             }
         }
-        __syncthreads();
+        sync_global();
         // 3. detection ratio (:93-95), kept-point counts and bboxes of all object points (:99)
         for (int c0 = 0; c0 < no; c0 += kPPBoxChunk) {
             const int cn = min(kPPBoxChunk, no - c0);
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(256) void k_pp_filter(
                     s_box[6 * c + 3 + d] = 0ull;
                 }
             }
-            __syncthreads();
+            sync_global();
             for (int i = t; i < n; i += 256) {
                 const int o = lb[i] - sh;
                 int cnode = 0;
@@ -553,17 +553,17 @@ __global__ __launch_bounds__(256) void k_pp_filter(
                     atomicMax(&s_box[6 * oc + 3 + d], u);
                 }
             }
-            __syncthreads();
+            sync_global();
             for (int c = t; c < cn; c += 256) {
                 obj_nvalid[ob + c0 + c] = s_nv[c];
 #pragma unroll
                 for (int d = 0; d < 6; d++) obj_box[6 * static_cast<int64_t>(ob + c0 + c) + d] = pp_unord(s_box[6 * c + d]);
             }
-            __syncthreads();
+            sync_global();
         }
         // 4. the position map returns to -1
         for (int i = t; i < n; i += 256) pm[pts[e0 + i]] = -1;
-        __syncthreads();
+        sync_global();
     }
 }
 
@@ -638,10 +638,10 @@ __global__ __launch_bounds__(1024) void k_pp_greedy(int K, const unsigned char *
     __shared__ int s_flag;
     const int t = threadIdx.x;
     for (int i = t; i < K; i += 1024) inv[i] = 0;
-    __syncthreads();
+    sync_global();
     for (int i = 0; i < K; i++) {
         if (t == 0) s_flag = 0;
-        __syncthreads();
+        sync_global();
         if (inv[i]) continue;  // uniform: written before the last barrier
         const unsigned char *d = dec + static_cast<int64_t>(i) * K;
         int f = 0;
@@ -652,9 +652,9 @@ __global__ __launch_bounds__(1024) void k_pp_greedy(int K, const unsigned char *
             else if (r == 2) inv[j] = 1;
         }
         if (f) s_flag = 1;
-        __syncthreads();
+        sync_global();
         if (t == 0 && s_flag) inv[i] = 1;
-        __syncthreads();
+        sync_global();
     }
 }
 
