@@ -1896,10 +1896,15 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         dv.trunc = prm.depth_trunc;
         dv.vs = prm.voxel_size;
         dv.eps2 = prm.dbscan_eps * prm.dbscan_eps;
-        for (int i = 0; i < 3; i++) {
-            const double f = 0.6 + 0.15 * i;
-            dv.knn_r2[i] = (f * prm.dbscan_eps) * (f * prm.dbscan_eps);
+        // k-NN pre-selection radii (fractions of eps, ascending, < 1): any choice gives the same
+        // results (the smallest radius holding >= k kept points is used); MC_KNN_RADII="a,b,c" tunes
+        double kfr[3] = {0.6, 0.75, 0.9};
+        if (const char *e = getenv("MC_KNN_RADII")) {
+            double a[3];
+            if (sscanf(e, "%lf,%lf,%lf", &a[0], &a[1], &a[2]) == 3 && 0 < a[0] && a[0] < a[1] && a[1] < a[2] && a[2] < 1)
+                for (int i = 0; i < 3; i++) kfr[i] = a[i];
         }
+        for (int i = 0; i < 3; i++) dv.knn_r2[i] = (kfr[i] * prm.dbscan_eps) * (kfr[i] * prm.dbscan_eps);
         dv.ce = prm.dbscan_eps * 1.01;
         dv.frac = prm.component_min_fraction;
         dv.std_ratio = prm.sor_std_ratio;
