@@ -1941,7 +1941,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_count, dim3(nbands, fb), dim3(256), 0, s, dB, sB, TB, dv,
                                    ctx->d_band.as<int>(), ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(),
                                    ctx->d_bpvid.as<unsigned char>());
-                hipLaunchKernelGGL(mc::k_bp_frames, dim3(fb), dim3(256), 0, s, ctx->d_band.as<int>(),
+                hipLaunchKernelGGL(mc::k_bp_frames, dim3(fb), dim3(1024), 0, s, ctx->d_band.as<int>(),
                                    ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(), dv, ctx->d_cand.as<int>(),
                                    ctx->d_npix.as<int>(), st + BS_ERRF);
                 mc::scan_device_n(s, ctx->d_cand.as<int>(), ctx->d_csidx.as<int>(), nullptr, nslot, st + BS_NS,

@@ -308,31 +308,55 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
     if (t == 0 && sflag) atomicOr(&fflags[f], sflag);
 }
 
-// One block per frame, thread = id: sub-band counts -> sub-band offsets within the id's pixel
-// list; candidate = id != 0 with >= few_points valid pixels (:101) in a frame that neither returns
-// early (inf pose) nor raises (d == trunc with ids present; *err_frame = first such frame).
-__global__ __launch_bounds__(256) void k_bp_frames(int *__restrict__ band_cnt, const unsigned *__restrict__ present,
-                                                   const int *__restrict__ fflags, BpDev pr, int *__restrict__ cand,
-                                                   int *__restrict__ npix, int *__restrict__ err_frame)
+// One block per frame, 1024 threads = id x quarter: sub-band counts -> sub-band offsets within the id's
+// pixel list (each quarter of the sub-bands summed with eight loads in flight, the quarters' totals
+// scanned through LDS); candidate = id != 0 with >= few_points valid pixels (:101) in a frame that
+// neither returns early (inf pose) nor raises (d == trunc with ids present; *err_frame = first such
+// frame).
+__global__ __launch_bounds__(1024) void k_bp_frames(int *__restrict__ band_cnt, const unsigned *__restrict__ present,
+                                                    const int *__restrict__ fflags, BpDev pr, int *__restrict__ cand,
+                                                    int *__restrict__ npix, int *__restrict__ err_frame)
 {
-    const int f = blockIdx.x, id = threadIdx.x;
+    __shared__ int qsum[4][256];
+    const int f = blockIdx.x, id = threadIdx.x & 255, qt = threadIdx.x >> 8;
     const int fl = fflags[f];
     bool any_id = false;
     for (int w = 0; w < 8; w++) any_id |= (present[f * 8 + w] & (w == 0 ? ~1u : ~0u)) != 0u;
     const bool inf_pose = (fl & 2) != 0;
     const bool err = !inf_pose && any_id && (fl & 1);
-    if (err && id == 0) atomicMin(err_frame, f);
-    int tot = 0;
+    if (err && threadIdx.x == 0) atomicMin(err_frame, f);
     const int nsb = pr.nbands * kBpWaves;
+    const int per = (nsb + 3) / 4, b0 = min(nsb, qt * per), b1 = min(nsb, b0 + per);
     int *bc = band_cnt + static_cast<size_t>(f) * nsb * 256 + id;
-    for (int b = 0; b < nsb; b++) {
-        const int c = bc[static_cast<size_t>(b) * 256];
-        bc[static_cast<size_t>(b) * 256] = tot;
-        tot += c;
+    // this quarter's total, eight sub-bands' loads issued together
+    int tot = 0;
+    for (int b = b0; b < b1; b += 8) {
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) c[u] = b + u < b1 ? bc[static_cast<size_t>(b + u) * 256] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) tot += c[u];
     }
-    const bool ok = id != 0 && !inf_pose && !err && tot >= pr.few;
-    cand[f * 256 + id] = ok ? 1 : 0;
-    npix[f * 256 + id] = ok ? tot : 0;
+    qsum[qt][id] = tot;
+    __syncthreads();
+    int run = 0;
+    for (int k = 0; k < qt; k++) run += qsum[k][id];
+    // exclusive offsets of this quarter's sub-bands
+    for (int b = b0; b < b1; b += 8) {
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) c[u] = b + u < b1 ? bc[static_cast<size_t>(b + u) * 256] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (b + u < b1) bc[static_cast<size_t>(b + u) * 256] = run;
+            run += c[u];
+        }
+    }
+    if (qt == 3) {  // run = the id's total in the frame
+        const bool ok = id != 0 && !inf_pose && !err && run >= pr.few;
+        cand[f * 256 + id] = ok ? 1 : 0;
+        npix[f * 256 + id] = ok ? run : 0;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_bp_slots(const int *__restrict__ cand, const int *__restrict__ sidx,
