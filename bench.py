@@ -761,9 +761,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob for the multi-rank path on a one-GPU box (never for a measured run): every rank on
+    # device MC_BENCH_DEVICE, collectives over gloo (host tensors) instead of RCCL
+    if os.environ.get("MC_BENCH_DEVICE") is not None:
+        local = int(os.environ["MC_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("MC_BENCH_BACKEND", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     frames = args.shard == "frames"
     if frames:  # one scene, frame slices per rank (strong scaling)
@@ -811,7 +818,8 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     dom_ms, dom_n = ctx.kernel_time(dominant)
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
