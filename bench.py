@@ -126,6 +126,34 @@ def roofline_entry(w, avg_s, pmc_group=None):
     return e
 
 
+SQ_DENOISE = os.path.join(REPO, "profiles", "r03", "denoise_sq_counters_c3_v13.json")
+SQ_DENOISE_FRAMES = 100     # the counter pass: C3 frames 600-699 (scripts/pmc_kernel.py over scripts/bp_profile.py)
+CLOCK_GHZ = 2.4             # MI355X engine clock (MI355X_MICROARCH.md)
+
+
+def denoise_valu(frames, launches, avg_s):
+    """The denoise's second bound: VALU issue.  The committed SQ pass gives the size classes' VALU
+    instructions per frame; times the frames of one launch (a batch), x 4 cycles per wave64
+    instruction (a SIMD is 16 lanes wide), over the SIMDs' cycles in the live launch time."""
+    if not os.path.exists(SQ_DENOISE):
+        return None
+    sq = json.load(open(SQ_DENOISE))
+    insts = sum(v.get("SQ_INSTS_VALU", 0.0) for k, v in sq.items() if "denoise" in k)
+    simds = 4 * _torch_cu_count()
+    per_launch = insts / SQ_DENOISE_FRAMES * frames / max(launches, 1)
+    frac = per_launch * 4 / (simds * CLOCK_GHZ * 1e9 * avg_s)
+    return {"bound": "valu-issue", "insts_per_launch": round(per_launch, 0), "frac": round(frac, 4),
+            "simds": simds, "clock_ghz": CLOCK_GHZ, "source": os.path.relpath(SQ_DENOISE, REPO),
+            "note": "VALU instructions of the size classes per frame from the committed SQ counter pass, x the "
+                    "launch's frames, 4 cycles per wave64 instruction; the rest of the cycles the waves wait on "
+                    "memory or barriers (SQ_WAIT_ANY 67-73 %, DESIGN.md)"}
+
+
+def _torch_cu_count():
+    import torch
+    return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+
+
 def bp_work(ctx, F, H, W):
     """Per-launch algorithmic bytes of the S1 groups: each frame's depth + seg
     read once and every mask pixel listed once (pixels); every mask pixel's list entry and
@@ -837,6 +865,8 @@ def main():
     roof = roofline_entry(work[dominant], (dom_ms / max(dom_n, 1)) / 1e3, pmc.get(dominant))
     roof["kernel"] = dominant
     roof["launches_timed"] = int(dom_n)
+    if dominant == "bp_denoise":
+        roof["valu"] = denoise_valu(runner.shape[0], calib[dominant][1], dom_ms / max(dom_n, 1) / 1e3)
     if pmc.get(dominant):
         roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
     stages = {}

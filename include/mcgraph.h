@@ -240,6 +240,22 @@ int mc_shard_pending(mc_ctx *ctx, int32_t *phase);
 int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes);
 int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes);
 
+/* ---- native collectives ---------------------------------------------------
+ * With an RCCL communicator attached, rank and world come from it and the sharded mc_graph_build /
+ * mc_cluster_run run their exchanges themselves, stream-ordered on the context stream (S3 rows and
+ * union-find forests: ncclAllGather; the observer histogram: ncclAllReduce sum int64; one max
+ * all-reduce + host read for the S3 block stride): nothing is left pending for the host.  This is
+ * what the Python collectives in maskclustering_amd/graph_shard.py do through torch.distributed.
+ * RCCL is loaded (dlopen librccl.so.1) on first use; MC_ERR_UNSUPPORTED if it is absent.
+ *   mc_comm_unique_id   ncclGetUniqueId, on one rank; the caller broadcasts the 128 bytes
+ *   mc_ctx_comm_init    ncclCommInitRank on the context's device; the context owns the communicator
+ *   mc_ctx_attach_comm  a caller-owned ncclComm_t (NULL detaches: back to the single-process path)
+ * A communicator of one rank runs the same exchange flow (each collective an identity). */
+#define MC_COMM_ID_BYTES 128
+int mc_comm_unique_id(uint8_t id[MC_COMM_ID_BYTES]);
+int mc_ctx_comm_init(mc_ctx *ctx, const uint8_t id[MC_COMM_ID_BYTES], int32_t rank, int32_t world);
+int mc_ctx_attach_comm(mc_ctx *ctx, void *nccl_comm);
+
 /* ---- post-processing of the clustered objects ----------------------
  * Replaces the compute of utils/post_process.py:173-194 (post_process up to export):
  * dbscan_process (:104-123), filter_point (:40-101), merge_overlapping_objects (:7-37).

@@ -38,7 +38,9 @@ EXPORTED = [
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
     "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query", "mc_bits_unpack",
+    "mc_comm_unique_id", "mc_ctx_comm_init", "mc_ctx_attach_comm",
 ]
+MC_COMM_ID_BYTES = 128
 
 MC_SHARD_S3 = 1
 MC_SHARD_HIST = 2
@@ -175,6 +177,9 @@ def load():
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
         "mc_shard_import": (ctypes.c_int, [vp, i32, vp, i64]),
+        "mc_comm_unique_id": (ctypes.c_int, [vp]),
+        "mc_ctx_comm_init": (ctypes.c_int, [vp, vp, i32, i32]),
+        "mc_ctx_attach_comm": (ctypes.c_int, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -182,6 +187,15 @@ def load():
         fn.argtypes = args
     _lib = L
     return L
+
+
+def comm_unique_id() -> bytes:
+    """mc_comm_unique_id (ncclGetUniqueId): made on one rank, broadcast to the others."""
+    buf = ctypes.create_string_buffer(MC_COMM_ID_BYTES)
+    rc = load().mc_comm_unique_id(buf)
+    if rc != MC_OK:
+        raise McError(rc, "mc_comm_unique_id failed (RCCL not loadable?)")
+    return buf.raw
 
 
 def _ptr(a):
@@ -247,6 +261,17 @@ class Context:
 
     def shard_set(self, rank, world):
         self._check(self.L.mc_shard_set(self.h, int(rank), int(world)))
+
+    def comm_init(self, unique_id: bytes, rank: int, world: int):
+        """mc_ctx_comm_init: an RCCL communicator owned by the context (rank / world of the sharded
+        graph stages come from it; the exchanges then run inside mc_graph_build / mc_cluster_run)."""
+        assert len(unique_id) == MC_COMM_ID_BYTES
+        buf = ctypes.create_string_buffer(bytes(unique_id), MC_COMM_ID_BYTES)
+        self._check(self.L.mc_ctx_comm_init(self.h, buf, int(rank), int(world)))
+
+    def attach_comm(self, nccl_comm):
+        """mc_ctx_attach_comm: a caller-owned ncclComm_t (an int address); None detaches."""
+        self._check(self.L.mc_ctx_attach_comm(self.h, None if nccl_comm is None else ctypes.c_void_p(int(nccl_comm))))
 
     def shard_pending(self) -> int:
         ph = ctypes.c_int32()

@@ -1,5 +1,8 @@
 // mc_api.hip — C-ABI of libmcgraph: context, scene upload, S2–S6 orchestration, getters.
 // Single translation unit: the kernels live in mc_kernels.inl.
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: the library loads RCCL at mc_ctx_attach_comm / mc_ctx_comm_init (dlopen)
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -64,6 +67,10 @@ struct mc_ctx {
     size_t stage_bytes = 0;
     hipEvent_t ev_stage[2] = {};
     bool stage_used[2] = {false, false};
+    // host frames staged batch by batch on their own stream while the previous batch computes
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_up = nullptr;
+    struct BpUpload *bp_up = nullptr;  // set for the duration of mc_backproject_frames' S1 call
 
     // ---- scene ----
     bool have_scene = false, have_graph = false, have_nodes = false, have_cluster = false;
@@ -137,6 +144,11 @@ struct mc_ctx {
     int64_t sh_s3_words = -1;    // size of this rank's S3 block (valid while sh_pending == MC_SHARD_S3)
     mc_graph_params sh_params{};
     DevBuf d_sh_eoff;
+    // native collectives (mc_ctx_attach_comm / mc_ctx_comm_init): with a communicator attached the
+    // sharded mc_graph_build / mc_cluster_run run their exchanges themselves, on the context stream
+    void *comm = nullptr;        // ncclComm_t
+    bool own_comm = false;
+    DevBuf d_sh_send, d_sh_recv, d_sh_size;
     // S6 state kept across the FOREST exchange
     int s6_nthr = 0;
     bool s6_dense_obs = false;
@@ -287,6 +299,12 @@ std::vector<int32_t> frame_starts(const mc_ctx *ctx)
 
 }  // namespace
 
+static void shard_drain_native(mc_ctx *ctx);
+static void comm_detach(mc_ctx *ctx);
+namespace {
+bool sharded(const mc_ctx *ctx);
+}
+
 extern "C" {
 
 int mc_ctx_create(int device, mc_ctx **out)
@@ -324,6 +342,12 @@ void mc_ctx_destroy(mc_ctx *ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) {
+        try {
+            comm_detach(ctx);
+        } catch (const McError &) {
+        }
+    }
     DevBuf *bufs[] = {&ctx->d_mask_off, &ctx->d_mask_pts, &ctx->d_mask_col, &ctx->d_mask_label, &ctx->d_frame_start,
                       &ctx->d_valid, &ctx->d_deg, &ctx->d_pt_off, &ctx->d_pt_list, &ctx->d_boundary,
                       &ctx->d_pfm, &ctx->d_scan_tmp, &ctx->d_ctmp, &ctx->d_crow_len, &ctx->d_useg, &ctx->d_keep_cnt,
@@ -338,7 +362,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_vfA, &ctx->d_vfB, &ctx->d_pmin, &ctx->d_pmax, &ctx->d_nwords, &ctx->d_woff,
                       &ctx->d_bm, &ctx->d_ptcnt, &ctx->d_ptoff_out, &ctx->d_pts_out, &ctx->d_owner0,
                       &ctx->d_node_of_mask, &ctx->d_ownA, &ctx->d_ownB, &ctx->d_cap, &ctx->d_obj_of_mask,
-                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen, &ctx->d_sh_eoff,
+                      &ctx->d_s3_small, &ctx->d_s3_big, &ctx->d_collen, &ctx->d_sh_eoff, &ctx->d_sh_send, &ctx->d_sh_recv, &ctx->d_sh_size,
                       &ctx->d_cap_buf, &ctx->d_cap_cnt};
     for (DevBuf *b : bufs) b->release();
     DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
@@ -356,6 +380,8 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
                          &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid};
     for (DevBuf *b : bp_bufs) b->release();
+    if (ctx->copy) (void)hipStreamSynchronize(ctx->copy), (void)hipStreamDestroy(ctx->copy);
+    if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->h_bppack) (void)hipHostFree(ctx->h_bppack);
     if (ctx->h_bpstat) (void)hipHostFree(ctx->h_bpstat);
@@ -693,9 +719,10 @@ int mc_graph_build(mc_ctx *ctx, const mc_graph_params *params)
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
             }
         }
-        if (ctx->sh_world > 1) {  // this rank's S3 rows go to the others first (mc_shard_export/import)
+        if (sharded(ctx)) {  // this rank's S3 rows go to the others first (mc_shard_export/import)
             ctx->sh_pending = MC_SHARD_S3;
             ctx->sh_s3_words = -1;
+            if (ctx->comm) shard_drain_native(ctx);  // S3 rows, then the histogram, over RCCL
             return;
         }
         graph_build_tail(ctx);
@@ -1107,7 +1134,7 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         MC_REQUIRE(ctx->have_nodes, MC_ERR_STATE, "mc_cluster_run before mc_graph_build / mc_nodes_set");
         // a sharded level 0 evaluates only this rank's pair rows, so a capture would miss the other
         // ranks' edges (replay mode is single-process)
-        MC_REQUIRE(!(ctx->cap_edges > 0 && ctx->sh_world > 1), MC_ERR_UNSUPPORTED,
+        MC_REQUIRE(!(ctx->cap_edges > 0 && sharded(ctx)), MC_ERR_UNSUPPORTED,
                    "edge capture (set-order replay) needs an unsharded context (mc_shard_set world 1)");
         hipStream_t s = ctx->stream;
         int *stats = ctx->d_stats.as<int>();
@@ -1217,7 +1244,7 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
         ctx->s6_ctf = ctf;
         ctx->have_cluster = false;
         ctx->sh_pending = 0;
-        if (nthr > 0 && N0 > 0 && ctx->sh_world > 1 && !dense_obs) {
+        if (nthr > 0 && N0 > 0 && sharded(ctx) && !dense_obs) {
             // iteration 0 (the N0 x N0 pairs) on this rank's rows; the union-find forests of all
             // ranks are united by mc_shard_import(MC_SHARD_FOREST), which runs the rest
             TimedScope ts(ctx->timer, s, "s6_pairs");
@@ -1230,6 +1257,7 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
                                mc::EdgeCap{nullptr, nullptr, 0});
             MC_HIP(hipGetLastError());
             ctx->sh_pending = MC_SHARD_FOREST;
+            if (ctx->comm) shard_drain_native(ctx);  // the forests over RCCL, then the rest of S6
             return;
         }
         s6_iterations(ctx, 0, false);
@@ -1243,6 +1271,7 @@ int mc_shard_set(mc_ctx *ctx, int32_t rank, int32_t world)
 {
     return guarded(ctx, [&] {
         MC_REQUIRE(world >= 1 && world <= 1024 && rank >= 0 && rank < world, MC_ERR_INVALID, "bad rank / world");
+        MC_REQUIRE(!ctx->comm, MC_ERR_STATE, "a communicator is attached (rank / world come from it; detach first)");
         ctx->sh_rank = rank;
         ctx->sh_world = world;
         ctx->sh_pending = 0;
@@ -1258,9 +1287,9 @@ int mc_shard_pending(mc_ctx *ctx, int32_t *phase)
     });
 }
 
-int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes)
+static void shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes)
 {
-    return guarded(ctx, [&] {
+    {
         MC_REQUIRE(bytes, MC_ERR_INVALID, "null bytes");
         MC_REQUIRE(phase == ctx->sh_pending && phase != 0, MC_ERR_STATE, "no such exchange pending");
         hipStream_t s = ctx->stream;
@@ -1296,12 +1325,12 @@ int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes)
             throw McError{MC_ERR_INVALID, "unknown exchange phase"};
         }
         MC_HIP(hipGetLastError());
-    });
+    }
 }
 
-int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes)
+static void shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes)
 {
-    return guarded(ctx, [&] {
+    {
         MC_REQUIRE(phase == ctx->sh_pending && phase != 0, MC_ERR_STATE, "no such exchange pending");
         MC_REQUIRE(src_dev, MC_ERR_INVALID, "null source");
         hipStream_t s = ctx->stream;
@@ -1335,6 +1364,171 @@ int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t str
         } else {
             throw McError{MC_ERR_INVALID, "unknown exchange phase"};
         }
+    }
+}
+
+int mc_shard_export(mc_ctx *ctx, int32_t phase, void *dst_dev, int64_t *bytes)
+{
+    return guarded(ctx, [&] { shard_export(ctx, phase, dst_dev, bytes); });
+}
+
+int mc_shard_import(mc_ctx *ctx, int32_t phase, const void *src_dev, int64_t stride_bytes)
+{
+    return guarded(ctx, [&] { shard_import(ctx, phase, src_dev, stride_bytes); });
+}
+
+// ---- native collectives: RCCL, loaded on first use ------------------------------------------
+namespace {
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl *rccl_lib()
+{
+    static const Rccl r = [] {
+        Rccl x;
+        void *h = nullptr;
+        for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) return x;
+        x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        x.comm_count = reinterpret_cast<decltype(x.comm_count)>(dlsym(h, "ncclCommCount"));
+        x.comm_user_rank = reinterpret_cast<decltype(x.comm_user_rank)>(dlsym(h, "ncclCommUserRank"));
+        x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(h, "ncclAllGather"));
+        x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+        return x;
+    }();
+    MC_REQUIRE(r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.comm_count && r.comm_user_rank &&
+                   r.all_reduce && r.all_gather && r.error_string,
+               MC_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not loadable");
+    return &r;
+}
+
+void rccl_check(ncclResult_t e, const char *what)
+{
+    if (e != ncclSuccess) throw McError{MC_ERR_HIP, std::string(what) + ": " + rccl_lib()->error_string(e)};
+}
+
+bool sharded(const mc_ctx *ctx) { return ctx->sh_world > 1 || ctx->comm; }
+}  // namespace
+
+// every pending exchange over the attached communicator, stream-ordered on the context stream:
+// the S3 and FOREST blocks all-gathered into [world][stride] (S3's stride from a max all-reduce of
+// the block sizes, one host read), the HIST block all-reduced (sum, int64)
+static void shard_drain_native(mc_ctx *ctx)
+{
+    const Rccl &r = *rccl_lib();
+    hipStream_t s = ctx->stream;
+    auto comm = static_cast<ncclComm_t>(ctx->comm);
+    const size_t W = static_cast<size_t>(ctx->sh_world);
+    while (ctx->sh_pending) {
+        const int ph = ctx->sh_pending;
+        int64_t bytes = 0;
+        shard_export(ctx, ph, nullptr, &bytes);
+        if (ph == MC_SHARD_HIST) {
+            const size_t n = static_cast<size_t>(bytes) / 8;
+            ctx->d_sh_send.reserve(n * 8);
+            ctx->d_sh_recv.reserve(n * 8);
+            shard_export(ctx, ph, ctx->d_sh_send.ptr, &bytes);
+            rccl_check(r.all_reduce(ctx->d_sh_send.ptr, ctx->d_sh_recv.ptr, n, ncclInt64, ncclSum, comm, s),
+                       "ncclAllReduce (observer histogram)");
+            shard_import(ctx, ph, ctx->d_sh_recv.ptr, 0);
+            continue;
+        }
+        int64_t n_max = bytes;
+        if (ph == MC_SHARD_S3) {
+            ctx->d_sh_size.reserve(8);
+            MC_HIP(hipMemcpy(ctx->d_sh_size.ptr, &bytes, 8, hipMemcpyHostToDevice));  // done at return
+            rccl_check(r.all_reduce(ctx->d_sh_size.ptr, ctx->d_sh_size.ptr, 1, ncclInt64, ncclMax, comm, s),
+                       "ncclAllReduce (S3 block size)");
+            MC_HIP(hipMemcpyAsync(&n_max, ctx->d_sh_size.ptr, 8, hipMemcpyDeviceToHost, s));
+            MC_HIP(hipStreamSynchronize(s));
+        }
+        const size_t words = static_cast<size_t>(std::max<int64_t>((n_max + 3) / 4, 1));
+        ctx->d_sh_send.reserve(words * 4);
+        ctx->d_sh_recv.reserve(W * words * 4);
+        MC_HIP(hipMemsetAsync(ctx->d_sh_send.ptr, 0, words * 4, s));
+        shard_export(ctx, ph, ctx->d_sh_send.ptr, &bytes);
+        rccl_check(r.all_gather(ctx->d_sh_send.ptr, ctx->d_sh_recv.ptr, words, ncclInt32, comm, s),
+                   ph == MC_SHARD_S3 ? "ncclAllGather (S3 rows)" : "ncclAllGather (union-find forests)");
+        shard_import(ctx, ph, ctx->d_sh_recv.ptr, static_cast<int64_t>(4 * words));
+    }
+}
+
+static void comm_detach(mc_ctx *ctx)
+{
+    if (ctx->comm && ctx->own_comm) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)rccl_lib()->comm_destroy(static_cast<ncclComm_t>(ctx->comm));
+    }
+    ctx->comm = nullptr;
+    ctx->own_comm = false;
+}
+
+static void comm_attach(mc_ctx *ctx, void *comm, bool own)
+{
+    int rank = 0, world = 1;
+    rccl_check(rccl_lib()->comm_user_rank(static_cast<ncclComm_t>(comm), &rank), "ncclCommUserRank");
+    rccl_check(rccl_lib()->comm_count(static_cast<ncclComm_t>(comm), &world), "ncclCommCount");
+    comm_detach(ctx);
+    ctx->comm = comm;
+    ctx->own_comm = own;
+    ctx->sh_rank = rank;
+    ctx->sh_world = world;
+    ctx->sh_pending = 0;
+    if (ctx->have_scene) build_s3_lists(ctx, frame_starts(ctx));
+}
+
+int mc_comm_unique_id(uint8_t id[MC_COMM_ID_BYTES])
+{
+    static_assert(MC_COMM_ID_BYTES == sizeof(ncclUniqueId), "unique id size");
+    if (!id) return MC_ERR_INVALID;
+    try {
+        ncclUniqueId u;
+        rccl_check(rccl_lib()->get_unique_id(&u), "ncclGetUniqueId");
+        memcpy(id, &u, sizeof(u));
+        return MC_OK;
+    } catch (const McError &e) {
+        return e.code;
+    }
+}
+
+int mc_ctx_comm_init(mc_ctx *ctx, const uint8_t id[MC_COMM_ID_BYTES], int32_t rank, int32_t world)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(id, MC_ERR_INVALID, "null unique id");
+        MC_REQUIRE(world >= 1 && world <= 1024 && rank >= 0 && rank < world, MC_ERR_INVALID, "bad rank / world");
+        MC_HIP(hipSetDevice(ctx->device));
+        ncclUniqueId u;
+        memcpy(&u, id, sizeof(u));
+        ncclComm_t c = nullptr;
+        rccl_check(rccl_lib()->comm_init_rank(&c, world, u, rank), "ncclCommInitRank");
+        comm_attach(ctx, c, true);
+    });
+}
+
+int mc_ctx_attach_comm(mc_ctx *ctx, void *nccl_comm)
+{
+    return guarded(ctx, [&] {
+        if (!nccl_comm) {
+            comm_detach(ctx);
+            ctx->sh_rank = 0;
+            ctx->sh_world = 1;
+            ctx->sh_pending = 0;
+            if (ctx->have_scene) build_s3_lists(ctx, frame_starts(ctx));
+            return;
+        }
+        comm_attach(ctx, nccl_comm, false);
     });
 }
 
@@ -1726,10 +1920,20 @@ int mc_scene_set_points(mc_ctx *ctx, int64_t num_points, const float *xyz, int o
 // Per-frame host arrays -> one device array [F, frame_bytes]: the frames are copied by host
 // threads into a pinned chunk while the previous chunk's DMA runs (pageable hipMemcpy would stage
 // through the runtime's own buffers on one thread, and np.stack would add a full host copy).
-static void stage_frames(mc_ctx *ctx, const void *const *frames, size_t frame_bytes, int F, char *dst)
+// host frames of one mc_backproject_frames call; frames [0, staged) are on the device (or queued
+// on ctx->copy before ctx->ev_up)
+struct BpUpload {
+    const void *const *depth;
+    const void *const *seg;
+    int staged;
+};
+
+// frames [f_lo, f_hi) (frames[f] = host pointer of frame f) -> dst + f * frame_bytes, through the
+// pinned ping-pong chunks: host threads fill one chunk while the DMA of the other runs on stream s
+static void stage_frames(mc_ctx *ctx, const void *const *frames, size_t frame_bytes, int f_lo, int f_hi, char *dst,
+                         hipStream_t s)
 {
-    if (!F || !frame_bytes) return;
-    hipStream_t s = ctx->stream;
+    if (f_hi <= f_lo || !frame_bytes) return;
     const size_t want = std::max<size_t>(frame_bytes, static_cast<size_t>(32) << 20);
     if (ctx->stage_bytes < want) {
         for (int b = 0; b < 2; b++) {
@@ -1749,8 +1953,8 @@ static void stage_frames(mc_ctx *ctx, const void *const *frames, size_t frame_by
     if (const char *e = getenv("MC_STAGE_THREADS")) nthreads = std::max(1, std::min(64, atoi(e)));
     const int per = static_cast<int>(std::max<size_t>(1, ctx->stage_bytes / frame_bytes));
     int b = 0;
-    for (int f0 = 0; f0 < F; f0 += per, b ^= 1) {
-        const int n = std::min(per, F - f0);
+    for (int f0 = f_lo; f0 < f_hi; f0 += per, b ^= 1) {
+        const int n = std::min(per, f_hi - f0);
         if (ctx->stage_used[b]) MC_HIP(hipEventSynchronize(ctx->ev_stage[b]));  // its last DMA is done
         char *buf = ctx->h_stage[b];
         const size_t total = static_cast<size_t>(n) * frame_bytes;
@@ -1798,10 +2002,10 @@ int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32
         ctx->d_in_pose.reserve(F * 16 * 8ull);
         MC_HIP(hipMemcpyAsync(ctx->d_in_intr.ptr, intrinsics, F * 4 * 8ull, hipMemcpyHostToDevice, s));
         MC_HIP(hipMemcpyAsync(ctx->d_in_pose.ptr, poses, F * 16 * 8ull, hipMemcpyHostToDevice, s));
-        stage_frames(ctx, reinterpret_cast<const void *const *>(depth_frames), HW * 4, F,
-                     static_cast<char *>(ctx->d_in_depth.ptr));
-        stage_frames(ctx, reinterpret_cast<const void *const *>(seg_frames), HW, F,
-                     static_cast<char *>(ctx->d_in_seg.ptr));
+        if (!ctx->copy) {
+            MC_HIP(hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking));
+            MC_HIP(hipEventCreateWithFlags(&ctx->ev_up, hipEventDisableTiming));
+        }
     });
     if (rc != MC_OK) return rc;
     if (!num_frames) {
@@ -1810,8 +2014,15 @@ int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32
         static const double zd[16] = {};
         return mc_backproject(ctx, 0, height, width, &zf, &zs, zd, zd, 0, params);
     }
-    return mc_backproject(ctx, num_frames, height, width, ctx->d_in_depth.as<float>(), ctx->d_in_seg.as<uint8_t>(),
-                          ctx->d_in_intr.as<double>(), ctx->d_in_pose.as<double>(), 1, params);
+    // the frames are staged by the S1 batch loop itself: batch b + 1's while batch b computes
+    BpUpload up{reinterpret_cast<const void *const *>(depth_frames), reinterpret_cast<const void *const *>(seg_frames), 0};
+    ctx->bp_up = &up;
+    const int rc2 = mc_backproject(ctx, num_frames, height, width, ctx->d_in_depth.as<float>(),
+                                   ctx->d_in_seg.as<uint8_t>(), ctx->d_in_intr.as<double>(),
+                                   ctx->d_in_pose.as<double>(), 1, params);
+    ctx->bp_up = nullptr;
+    (void)hipStreamSynchronize(ctx->copy);  // no DMA into d_in_* outlives the call (error paths)
+    return rc2;
 }
 
 int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
@@ -1881,7 +2092,23 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                           std::min(budget, (free_b + ctx->bp_px_cap * 200) / 100 * 45 / 200));
         }
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
-        const int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
+        BpUpload *const up = on_device ? ctx->bp_up : nullptr;
+        int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
+        // frames arriving from the host: at least 8 batches, so all but the first batch's upload
+        // runs under the previous batch's compute (MC_BP_UPLOAD_BATCHES tunes; 1 = one upload first)
+        if (up) {
+            int nb = 8;
+            if (const char *e = getenv("MC_BP_UPLOAD_BATCHES")) nb = std::max(1, atoi(e));
+            FB = std::max(1, std::min(FB, (F + nb - 1) / nb));
+        }
+        // stage the host frames [up->staged, f_hi) on the copy stream
+        auto upload_to = [&](int f_hi) {
+            if (!up || f_hi <= up->staged) return;
+            stage_frames(ctx, up->depth, HW * 4, up->staged, f_hi, static_cast<char *>(ctx->d_in_depth.ptr), ctx->copy);
+            stage_frames(ctx, up->seg, HW, up->staged, f_hi, static_cast<char *>(ctx->d_in_seg.ptr), ctx->copy);
+            MC_HIP(hipEventRecord(ctx->ev_up, ctx->copy));
+            up->staged = f_hi;
+        };
         bp_reserve(ctx, FB, H, W, nbands, s);
         const int PW = static_cast<int>((ctx->P_scene + 63) / 64) + 1;
         if (ctx->d_bpbm.bytes < static_cast<size_t>(kBpGrid) * PW * 8) {
@@ -1929,6 +2156,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         int *const hs = ctx->h_bpstat;  // pinned
         for (int b0 = 0; b0 < F;) {
             const int fb = std::min(FB, F - b0);
+            if (up) {
+                upload_to(b0 + fb);
+                MC_HIP(hipStreamWaitEvent(s, ctx->ev_up, 0));
+            }
             const float *dB = dep + b0 * HW;
             const uint8_t *sB = sg + b0 * HW;
             const double *KB = Kp + 4 * static_cast<size_t>(b0), *TB = Tp + 16 * static_cast<size_t>(b0);
@@ -2034,6 +2265,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 bp_debug_sync(s, "bp_query");
             }
             MC_HIP(hipMemcpyAsync(hs, st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));
+            upload_to(std::min(F, b0 + fb + FB));  // the host copies the next batch while this one computes
             MC_HIP(hipStreamSynchronize(s));
             ctx->timer.collect();
             if (hs[BS_ERRF] != INT_MAX) {

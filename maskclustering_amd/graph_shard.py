@@ -19,7 +19,10 @@ exchanges here are ~13 MB (S3 rows), 12 KB (histogram) and 4·N0 bytes per rank 
 The collectives are torch.distributed's (RCCL over xGMI under "nccl"; gloo for the tests, where
 blocks go through host memory).  The library (``mc_shard_*`` in include/mcgraph.h) only packs and
 unpacks the blocks, on its stream; a context whose stream is not torch's current stream is
-synchronised around each exchange.
+synchronised around each exchange.  With ``native_comm=True`` the library owns an RCCL
+communicator instead (``mc_ctx_comm_init``; the unique id is broadcast over ``group``) and runs
+the same exchanges itself inside mc_graph_build / mc_cluster_run, stream-ordered, with nothing
+left pending for the host.
 """
 from __future__ import annotations
 
@@ -33,7 +36,7 @@ class ShardedGraph:
     """Drives one rank's context through the sharded S2-S6 (``run``: a pipeline.GraphRun, or any
     object with a ``ctx`` exposing the mc_shard_* methods; ``group``: the process group)."""
 
-    def __init__(self, run, group=None):
+    def __init__(self, run, group=None, native_comm=False):
         self.run = run
         self.ctx = run.ctx
         self.group = group
@@ -42,8 +45,23 @@ class ShardedGraph:
         self.world = dist.get_world_size(group) if on else 1
         self.dev = self.ctx.torch_device
         self.comm_dev = self.dev if on and dist.get_backend(group) == "nccl" else torch.device("cpu")
-        self.ctx.shard_set(self.rank, self.world)
+        self.native = bool(native_comm)
+        if self.native:
+            self._comm_init()
+        else:
+            self.ctx.shard_set(self.rank, self.world)
         self.bytes_moved = 0
+
+    def _comm_init(self):
+        from ._native import MC_COMM_ID_BYTES, comm_unique_id
+        uid = torch.zeros(MC_COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            uid = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
+        if self.world > 1:
+            t = uid.to(self.comm_dev)
+            dist.broadcast(t, 0, group=self.group)
+            uid = t.cpu()
+        self.ctx.comm_init(bytes(uid.tolist()), self.rank, self.world)
 
     def _same_stream(self):
         if self.dev.type != "cuda":

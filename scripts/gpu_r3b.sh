@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# One box, in order of importance; each step has its own time limit and a failure ends the script:
+# the S1 GPU tests (incl. the per-batch host staging), the reference-API path at C2 with per-batch
+# staging, a C3 kernel trace (per-batch group / class spans), the frame-sharded bench with 2 ranks on
+# the one GPU (gloo), the API path at C3.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${OUT:-gpurun_out/r3b}
+mkdir -p "$OUT"
+step() { local name=$1; shift; echo "== $name $(date +%T)"; timeout -k 10 "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" \
+    || { echo "$name failed"; tail -20 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }; tail -3 "$OUT/$name.out"; }
+step pytest_s1 300 python -u -m pytest tests/test_gpu_s1.py tests/test_gpu_frame_shard.py -x -v --timeout 120 --timeout-method thread -m gpu
+step api_c2 300 python bench.py --variant api --shape c2 --steps 5 --warmup 2
+echo "== ktrace $(date +%T)"
+OUT=$OUT/kt timeout -k 10 700 bash scripts/gpu_ktrace_c3.sh || { echo "ktrace failed"; exit 1; }
+step n2_e2e_c2 420 env MC_BENCH_BACKEND=gloo MC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --shape c2 --steps 3 --warmup 1
+step api_c3 600 python bench.py --variant api --shape c3 --steps 3 --warmup 1

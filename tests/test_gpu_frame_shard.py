@@ -45,3 +45,31 @@ def test_sharded_graph_stages_equal_single(tmp_path, world, shape, seed):
         assert sorted(got.files) == sorted(want)
         for k in want:
             np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)
+
+
+def test_native_rccl_exchanges_equal_single():
+    """mc_ctx_comm_init (the library's own RCCL communicator): with a one-rank
+    communicator the sharded flow runs every exchange through RCCL inside mc_graph_build /
+    mc_cluster_run (all-gather / all-reduce of one block: identities), and every stage equals the
+    single-process run; detaching restores the plain path."""
+    from maskclustering_amd.graph_shard import ShardedGraph
+    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.synthetic import make_shape
+    s = make_shape("c1", seed=1)
+    run = GraphRun(0)
+    run.set_scene(s)
+    run.step(0.3, 0.3, 0.9, 0.8)
+    want = run.canonical(dense=False)
+    run2 = GraphRun(0)
+    run2.set_scene(s)
+    sh = ShardedGraph(run2, native_comm=True)
+    sh.step(0.3, 0.3, 0.9, 0.8)
+    assert run2.ctx.shard_pending() == 0
+    got = run2.canonical(dense=False)
+    for k in want:
+        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=k)
+    run2.ctx.attach_comm(None)
+    run2.step(0.3, 0.3, 0.9, 0.8)
+    got = run2.canonical(dense=False)
+    for k in want:
+        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=k)

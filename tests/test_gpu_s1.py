@@ -109,6 +109,22 @@ def test_backproject_batched_equals_single(ctx, monkeypatch):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("nb", ["1", "3", "16"])
+def test_backproject_frames_staged_per_batch(ctx, monkeypatch, nb):
+    """mc_backproject_frames (per-frame host arrays, batch b + 1 staged on the copy stream while
+    batch b computes) == mc_backproject over the contiguous [F, H, W] arrays."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=4)
+    a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    sa = ctx.bp_candidates()
+    monkeypatch.setenv("MC_BP_UPLOAD_BATCHES", nb)
+    ctx.backproject_frames([np.ascontiguousarray(d) for d in fr.depth], [np.ascontiguousarray(s) for s in fr.seg],
+                           fr.intrinsics, fr.poses)
+    for x, y in zip(a, ctx.bp_masks()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(sa, ctx.bp_candidates())
+
+
 def test_end_to_end_matches_oracle(ctx):
     """S1 on the device feeding S2-S6 on the device == the oracle's S1 feeding its S2-S6."""
     from maskclustering_amd.pipeline import GraphRun
