@@ -61,6 +61,7 @@ struct mc_ctx {
     int *h_stats = nullptr;  // pinned
     int *h_bppack = nullptr;   // pinned per-batch S1 readback (k_bp_pack), h_bppack_n ints
     int *h_bpstat = nullptr;   // pinned per-batch statistics block
+    hipEvent_t ev_pack = nullptr;  // the last batch's h_bppack copy (unpacked under the next batch)
     size_t h_bppack_n = 0;
     // pinned staging ring of mc_backproject_frames (two chunks, ping-pong)
     char *h_stage[2] = {nullptr, nullptr};
@@ -385,6 +386,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->h_bppack) (void)hipHostFree(ctx->h_bppack);
     if (ctx->h_bpstat) (void)hipHostFree(ctx->h_bpstat);
+    if (ctx->ev_pack) (void)hipEventDestroy(ctx->ev_pack);
     for (int b = 0; b < 2; b++) {
         if (ctx->h_stage[b]) (void)hipHostFree(ctx->h_stage[b]);
         if (ctx->ev_stage[b]) (void)hipEventDestroy(ctx->ev_stage[b]);
@@ -2154,6 +2156,35 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         if (!ctx->h_bpstat) MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_bpstat), BS_COUNT * sizeof(int),
                                                  hipHostMallocDefault));
         int *const hs = ctx->h_bpstat;  // pinned
+        if (!ctx->ev_pack) MC_HIP(hipEventCreateWithFlags(&ctx->ev_pack, hipEventDisableTiming));
+        // the host side of a batch (its masks and statistics appended from h_bppack) runs while the
+        // next batch computes: the batch's copy into h_bppack is stream-ordered before the next batch,
+        // whose own copy comes only after its statistics sync, i.e. after this unpack
+        struct PendingBatch {
+            bool valid = false;
+            int b0 = 0, Mb = 0, NS = 0, nnzb = 0;
+            int64_t nnz_base = 0;
+        } pend;
+        auto unpack = [&]() {
+            if (!pend.valid) return;
+            MC_HIP(hipEventSynchronize(ctx->ev_pack));
+            const int Mb = pend.Mb, NS = pend.NS, nnzb = pend.nnzb, bb = pend.b0;
+            const int *col = ctx->h_bppack, *lab = col + Mb, *off = lab + Mb;
+            const int *sf = off + Mb, *sid = sf + NS, *snp = sid + NS, *snv = snp + NS, *sm = snv + NS,
+                      *sns = sm + NS, *scov = sns + NS, *snn = scov + NS;
+            for (int g = 0; g < Mb; g++) {
+                ctx->bp_col.push_back(bb + col[g]);
+                ctx->bp_label.push_back(lab[g]);
+            }
+            for (int g = 0; g < Mb; g++) ctx->bp_off.push_back(pend.nnz_base + (g + 1 < Mb ? off[g + 1] : nnzb));
+            for (int x = 0; x < NS; x++) {
+                const int kept = snn[x] >= 0;
+                const int row[MC_BP_NSTAT] = {bb + sf[x], sid[x], snp[x], snv[x], sm[x], sns[x], -1,
+                                              sns[x] >= prm.few_points ? scov[x] : 0, kept ? snn[x] : 0, kept};
+                ctx->bp_stats.insert(ctx->bp_stats.end(), row, row + MC_BP_NSTAT);
+            }
+            pend.valid = false;
+        };
         for (int b0 = 0; b0 < F;) {
             const int fb = std::min(FB, F - b0);
             if (up) {
@@ -2266,6 +2297,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             MC_HIP(hipMemcpyAsync(hs, st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));
             upload_to(std::min(F, b0 + fb + FB));  // the host copies the next batch while this one computes
+            unpack();                               // and appends the previous batch's results
             MC_HIP(hipStreamSynchronize(s));
             ctx->timer.collect();
             if (hs[BS_ERRF] != INT_MAX) {
@@ -2314,25 +2346,19 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_slot_cov.as<int>(), ctx->d_slot_nn.as<int>(), ctx->d_bppack.as<int>());
                 MC_HIP(hipMemcpyAsync(ctx->h_bppack, ctx->d_bppack.ptr, npack * 4, hipMemcpyDeviceToHost, s));
             }
-            MC_HIP(hipStreamSynchronize(s));
-            const int *col = ctx->h_bppack, *lab = col + Mb, *off = lab + Mb;
-            const int *sf = off + Mb, *sid = sf + NS, *snp = sid + NS, *snv = snp + NS, *sm = snv + NS,
-                      *sns = sm + NS, *scov = sns + NS, *snn = scov + NS;
+            MC_HIP(hipEventRecord(ctx->ev_pack, s));
             bp_debug_sync(s, "bp_emit");
-            for (int g = 0; g < Mb; g++) {
-                ctx->bp_col.push_back(b0 + col[g]);
-                ctx->bp_label.push_back(lab[g]);
-            }
-            for (int g = 0; g < Mb; g++) ctx->bp_off.push_back(ctx->bp_nnz + (g + 1 < Mb ? off[g + 1] : nnzb));
-            for (int x = 0; x < NS; x++) {
-                const int kept = snn[x] >= 0;
-                const int row[MC_BP_NSTAT] = {b0 + sf[x], sid[x], snp[x], snv[x], sm[x], sns[x], -1,
-                                              sns[x] >= prm.few_points ? scov[x] : 0, kept ? snn[x] : 0, kept};
-                ctx->bp_stats.insert(ctx->bp_stats.end(), row, row + MC_BP_NSTAT);
-            }
+            pend.valid = true;
+            pend.b0 = b0;
+            pend.Mb = Mb;
+            pend.NS = NS;
+            pend.nnzb = nnzb;
+            pend.nnz_base = ctx->bp_nnz;
             ctx->bp_nnz += nnzb;
             b0 += fb;
         }
+        unpack();
+        MC_HIP(hipStreamSynchronize(s));
         ctx->have_bp = true;
     });
 }
