@@ -1924,6 +1924,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             put_mean(r, best);
         }
         bar();
+        BP_STAMP(34);  // k-NN: the list pass
 #ifdef MC_BP_STAMPS
         if (t == 0) atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(s_ndef));
 #endif
@@ -1964,6 +1965,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             put_mean(r, best);
         }
         bar();
+        BP_STAMP(35);  // k-NN: the ring search
         const int nfb = sfb[kFbCount];
         if (nfb > 2 * NW && kk == kBpKnnMax) {
             // many sparse points: one per lane, every kept point scanned in sorted order (the same

@@ -41,11 +41,12 @@ print("call ms", round(dt * 1e3, 2), groups)
 nslots = max(int(buf[14]), 1)
 print("LDS-class slots", int(buf[14]), "mean voxels", round(float(buf[15]) / nslots, 1))
 for off, kern in ((16, "k_bp_denoise_lds"), (0, "k_bp_denoise (large slots)")):
-    tot = float(buf[off:off + 13].sum())
+    tot = float(buf[off:off + 13].sum()) + (float(buf[34] + buf[35]) if off == 16 else 0.0)
     print(kern, "total workgroup-busy ms (100 MHz clock)", round(tot / 1e5, 2))
     for k, n in enumerate(names):
-        per = f"{float(buf[off + k]) / 100.0 / nslots:8.2f} us/slot" if off == 16 else ""
-        print(f"  {n:12s} {100.0 * float(buf[off + k]) / max(tot, 1):6.2f} % {per}")
+        v = float(buf[off + k]) + (float(buf[34] + buf[35]) if off == 16 and n == "knn" else 0.0)
+        per = f"{v / 100.0 / nslots:8.2f} us/slot" if off == 16 else ""
+        print(f"  {n:12s} {100.0 * v / max(tot, 1):6.2f} % {per}")
 print("k-NN sub-phases us/slot: main list pass", round(float(buf[34]) / 100.0 / nslots, 2), "ring search",
       round(float(buf[35]) / 100.0 / nslots, 2), "whole-cloud fallback", round(float(buf[26]) / 100.0 / nslots, 2))
 print("k-NN points deferred to the ring search", int(buf[30]), "(list overflow", int(buf[32]), "/ < k kept in the list",

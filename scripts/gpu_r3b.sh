@@ -13,8 +13,8 @@ step pytest_s1 300 python -u -m pytest tests/test_gpu_s1.py tests/test_gpu_frame
 step api_c2 300 python bench.py --variant api --shape c2 --steps 5 --warmup 2
 echo "== ktrace $(date +%T)"
 OUT=$OUT/kt timeout -k 10 700 bash scripts/gpu_ktrace_c3.sh || { echo "ktrace failed"; exit 1; }
+step stamps 240 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_stamps.so python scripts/bp_stamps.py c3 600 100
 echo "== env A/B $(date +%T)"
 OUT=$OUT/envab REPS=1 timeout -k 10 400 bash scripts/gpu_env_ab.sh || { echo "env A/B failed"; exit 1; }
 step n2_e2e_c2 420 env MC_BENCH_BACKEND=gloo MC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --shape c2 --steps 3 --warmup 1
-step api_c3 600 python bench.py --variant api --shape c3 --steps 3 --warmup 1
