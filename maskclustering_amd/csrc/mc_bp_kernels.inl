@@ -724,6 +724,9 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
+#ifndef MC_KNN_CULL
+#define MC_KNN_CULL 0  // ring search: skip cells no nearer than the current k-th distance (A/B knob)
+#endif
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
@@ -1947,13 +1950,31 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 sorted_insert(best, d2);
                 found++;
             };
+#if MC_KNN_CULL
+            // a cell whose nearest face is no nearer than the current k-th distance holds no point
+            // the insert would keep: skipped (a's offsets in its cell, gaps shrunk by 1e-9 ce so the
+            // bound stays below every point's computed distance)
+            const double ce = pr.ce, sl = 1e-9 * pr.ce;
+            const double ox = fmin(fmax(a.x - mn[0] - x * ce, 0.0), ce), oy = fmin(fmax(a.y - mn[1] - y * ce, 0.0), ce),
+                         oz = fmin(fmax(a.z - mn[2] - z * ce, 0.0), ce);
+            auto gap = [&](int d, double o) {
+                return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? d * ce - o : -d * ce - (ce - o)) - sl);
+            };
+#endif
             for (int R = 0; R <= 2 && !done; R++) {
                 for (int dz = -R; dz <= R; dz++)
                     for (int dy = -R; dy <= R; dy++) {
                         const bool edge = dz == -R || dz == R || dy == -R || dy == R;
                         const int step = (edge || R == 0) ? 1 : 2 * R;
-                        for (int dx = -R; dx <= R; dx += step)
+#if MC_KNN_CULL
+                        const double gyz = gap(dy, oy) * gap(dy, oy) + gap(dz, oz) * gap(dz, oz);
+#endif
+                        for (int dx = -R; dx <= R; dx += step) {
+#if MC_KNN_CULL
+                            if (gyz + gap(dx, ox) * gap(dx, ox) >= best[kBpKnnMax - 1]) continue;
+#endif
                             lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
+                        }
                     }
                 const double reach = static_cast<double>(R) * pr.ce;
                 done = found >= kk && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);

@@ -16,5 +16,8 @@ OUT=$OUT/kt timeout -k 10 700 bash scripts/gpu_ktrace_c3.sh || { echo "ktrace fa
 step stamps 240 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_stamps.so python scripts/bp_stamps.py c3 600 100
 echo "== env A/B $(date +%T)"
 OUT=$OUT/envab REPS=1 timeout -k 10 400 bash scripts/gpu_env_ab.sh || { echo "env A/B failed"; exit 1; }
-step n2_e2e_c2 420 env MC_BENCH_BACKEND=gloo MC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
-    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --shape c2 --steps 3 --warmup 1
+step pytest_cull 240 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_cull.so python -u -m pytest tests/test_gpu_s1.py -x -q \
+    --timeout 120 --timeout-method thread -m gpu
+echo "== cull A/B $(date +%T)"
+OUT=$OUT/ab_cull LIBS="maskclustering_amd/libmcgraph.so maskclustering_amd/libmcgraph_cull.so" REPS=1 \
+    timeout -k 10 400 bash scripts/gpu_ab_s1.sh || { echo "cull A/B failed"; exit 1; }
