@@ -724,8 +724,11 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
+#ifndef MC_EPS_CULL
+#define MC_EPS_CULL 1  // eps lists: neighbour cells beyond eps (face distance) not walked (0: A/B baseline)
+#endif
 #ifndef MC_KNN_CULL
-#define MC_KNN_CULL 0  // ring search: skip cells no nearer than the current k-th distance (A/B knob)
+#define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
 #endif
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
@@ -1347,17 +1350,45 @@ __device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
     return 3u - (d2 < pr.knn_r2[0] ? 1u : 0u) - (d2 < pr.knn_r2[1] ? 1u : 0u) - (d2 < pr.knn_r2[2] ? 1u : 0u);
 }
 
+// Lower bound on the squared distance from a point to any point of the neighbour cell at offset
+// (dx, dy, dz) in {-1, 0, 1}^3, from the point's offsets o in its own cell (cells of width ce): the
+// gaps to the shared faces, each shrunk by 1e-9 ce so the bound stays below the computed d2 of every
+// point of the cell (cell indices come from the same floor((p - min) / ce)).  A cell with a bound
+// >= eps2 holds no point within eps and is not walked (MC_EPS_CULL); the lists are unchanged.
+struct CellOff {
+    double o[3];
+    double ce;
+};
+__device__ __forceinline__ CellOff cell_off(double ax, double ay, double az, const double (&mn)[3], int x, int y, int z,
+                                            double ce)
+{
+    CellOff c;
+    c.o[0] = fmin(fmax(ax - mn[0] - x * ce, 0.0), ce);
+    c.o[1] = fmin(fmax(ay - mn[1] - y * ce, 0.0), ce);
+    c.o[2] = fmin(fmax(az - mn[2] - z * ce, 0.0), ce);
+    c.ce = ce;
+    return c;
+}
+__device__ __forceinline__ double cell_lb2(const CellOff &c, int dx, int dy, int dz)
+{
+    const double sl = 1e-9 * c.ce;
+    auto g = [&](int d, double o) { return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? c.ce - o : o) - sl); };
+    const double gx = g(dx, c.o[0]), gy = g(dy, c.o[1]), gz = g(dz, c.o[2]);
+    return (gx * gx + gy * gy) + gz * gz;
+}
+
 // The eps-neighbour list of sorted position q (point a, cell (x, y, z)): every point of the 27 cells
 // with d2 < eps2 (self included), in cell-walk order.  One predicate per candidate (cell key and
 // distance together, the record loaded whole) and one store; entries past kBpNbCap overwrite the
 // last slot (the list is unused then: the point walks its cells).  Returns the count.
 template <int N>
 __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q)
+                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q, const CellOff &co)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
         if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        if (MC_EPS_CULL && !(cell_lb2(co, d % 3 - 1, (d / 3) % 3 - 1, d / 9 - 1) < pr.eps2)) return make_int2(0, 0);
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(g.bs[b], g.bs[b + 1]);
@@ -1399,11 +1430,14 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 // (the union and the border labels are order-free, the k-NN sorts).
 template <int N>
 __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag)
+                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag,
+                                              const CellOff &co)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
         if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        if (MC_EPS_CULL && d != 13 && !(cell_lb2(co, d % 3 - 1, (d / 3) % 3 - 1, d / 9 - 1) < pr.eps2))
+            return make_int2(0, 0);
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
@@ -1680,7 +1714,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) {
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
-                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag);
+                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
+                                 cell_off(spt[q].x, spt[q].y, spt[q].z, mn, x, y, z, pr.ce));
             }
             sync_global();  // the lists hold other waves' stores
         } else {
@@ -1688,7 +1723,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
                 const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
+                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q, cell_off(ax, ay, az, mn, x, y, z, pr.ce));
                 spar[q] = q;
             }
         }
