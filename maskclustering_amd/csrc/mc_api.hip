@@ -322,25 +322,8 @@ int mc_ctx_create(int device, mc_ctx **out)
         MC_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
         MC_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-        // experiment knob MC_BP_BIG_CUS=n: the denoise classes of one workgroup per CU (2048 and up, and
-        // the side stream's 16384 class) restricted to the last n CUs, the 512 / 1024 classes to the
-        // others, so that the large slots need not wait for whole CUs to drain of small-slot workgroups
-        int big_cus = 0;
-        if (const char *e = getenv("MC_BP_BIG_CUS")) big_cus = std::max(0, std::min(ctx->num_cu - 1, atoi(e)));
-        std::vector<uint32_t> m_small, m_big;
-        if (big_cus > 0) {
-            const int words = (ctx->num_cu + 31) / 32;
-            m_small.assign(words, 0u);
-            m_big.assign(words, 0u);
-            for (int c = 0; c < ctx->num_cu; c++) (c >= ctx->num_cu - big_cus ? m_big : m_small)[c / 32] |= 1u << (c % 32);
-        }
         for (int c = 0; c < mc::kBpStreamClasses; c++) {
-            if (big_cus > 0) {
-                std::vector<uint32_t> &m = c >= 2 ? m_big : m_small;
-                MC_HIP(hipExtStreamCreateWithCUMask(&ctx->cls_stream[c], static_cast<uint32_t>(m.size()), m.data()));
-            } else {
-                MC_HIP(hipStreamCreateWithFlags(&ctx->cls_stream[c], hipStreamNonBlocking));
-            }
+            MC_HIP(hipStreamCreateWithFlags(&ctx->cls_stream[c], hipStreamNonBlocking));
             MC_HIP(hipEventCreateWithFlags(&ctx->ev_cls[c], hipEventDisableTiming));
         }
         MC_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stats), ST_COUNT * sizeof(int), hipHostMallocDefault));
