@@ -2096,10 +2096,12 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         BpUpload *const up = on_device ? ctx->bp_up : nullptr;
         int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
-        // frames arriving from the host: at least 8 batches, so all but the first batch's upload
-        // runs under the previous batch's compute (MC_BP_UPLOAD_BATCHES tunes; 1 = one upload first)
+        // frames arriving from the host: batch b + 1's upload runs under batch b's compute.  Splitting a
+        // scene that fits one batch into more batches only to overlap its upload did not pay (C2 API
+        // path: 1 batch 44.9 ms, 8 batches 46.2 ms, profiles/r03/api/), so by default only scenes of
+        // several batches overlap (C3: 7); MC_BP_UPLOAD_BATCHES=n forces at least n batches
         if (up) {
-            int nb = 8;
+            int nb = 1;
             if (const char *e = getenv("MC_BP_UPLOAD_BATCHES")) nb = std::max(1, atoi(e));
             FB = std::max(1, std::min(FB, (F + nb - 1) / nb));
         }

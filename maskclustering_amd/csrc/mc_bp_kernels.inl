@@ -1165,6 +1165,7 @@ __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks
 
 // acc + v(lane 0) + v(lane 1) + ... + v(lane 63), in lane order, skipping lanes with v <= 0 (a
 // std::accumulate step over 64 values); the lane values are read as scalars
+template <bool kSkipNonPos = true>
 __device__ __forceinline__ double seq_add64_pos(double acc, double v)
 {
     const long long bits = __double_as_longlong(v);
@@ -1174,7 +1175,11 @@ __device__ __forceinline__ double seq_add64_pos(double acc, double v)
         const unsigned long long b = (static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readlane(hi, j))) << 32) |
                                      static_cast<unsigned>(__builtin_amdgcn_readlane(lo, j));
         const double a = __longlong_as_double(static_cast<long long>(b));
-        if (a > 0) acc = acc + a;
+        if (kSkipNonPos) {
+            if (a > 0) acc = acc + a;
+        } else {
+            acc = acc + a;
+        }
     }
     return acc;
 }
@@ -1745,7 +1750,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             // the next entry's count and union-find parent are loaded before this one's find (a parent
             // read early is still a node of q2's component, so it is a valid place to start the find)
             nb_walk(w, cnt,
-                    [&](unsigned e) { return make_int2(sflag[e & kNbPos], ld_wg(spar + (e & kNbPos))); },
+                    [&](unsigned e) {  // only the entries the union takes (q2 < q) are loaded
+                        const int q2 = static_cast<int>(e & kNbPos);
+                        return q2 < q ? make_int2(sflag[q2], ld_wg(spar + q2)) : make_int2(0, 0);
+                    },
                     [&](int, unsigned e, int2 fp) {
                         const int q2 = static_cast<int>(e & kNbPos);
                         if (q2 < q && nb_cnt(fp.x) >= pr.minpts && fp.y != ra) {  // parent == root: joined already
@@ -2070,13 +2078,16 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         if (wv == 0) {
             double mean = 0.0, sq = 0.0;
             for (int r0 = 0; r0 < m; r0 += 64) {
-                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;  // 0 adds nothing below
-                mean = seq_add64_pos(mean, v);
+                // values that are not > 0 become +0.0, whose add leaves the (non-negative) sum as it is:
+                // the ordered chain is plain adds, the selects run lane-parallel before it
+                const double a = r0 + lane < m ? savg[r0 + lane] : 0.0;
+                mean = seq_add64_pos<false>(mean, a > 0 ? a : 0.0);
             }
             mean = mean / static_cast<double>(m);
             for (int r0 = 0; r0 < m; r0 += 64) {
                 const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;
-                sq = seq_add64_pos(sq, v > 0 ? (v - mean) * (v - mean) : 0.0);
+                const double d = v > 0 ? (v - mean) * (v - mean) : 0.0;
+                sq = seq_add64_pos<false>(sq, d > 0 ? d : 0.0);
             }
             const double sd = sqrt(sq / static_cast<double>(m - 1));
             if (lane == 0) s_thr = mean + pr.std_ratio * sd;
