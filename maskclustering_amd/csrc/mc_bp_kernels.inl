@@ -724,6 +724,9 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
+#ifndef MC_RING_SPREAD
+#define MC_RING_SPREAD 0  // ring search: deferred points dealt over the waves (A/B knob)
+#endif
 #ifndef MC_EPS_CULL
 #define MC_EPS_CULL 1  // eps lists: neighbour cells beyond eps (face distance) not walked (0: A/B baseline)
 #endif
@@ -1978,7 +1981,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         for (int f = t; f < s_ndef; f += T) sfb[atomicAdd(&sfb[kFbCount], 1)] = spar[sring[f]];
         if (false)
 #endif
-        for (int f = t; f < s_ndef; f += T) {
+        // deferred point f on lane f / NW of wave f % NW (MC_RING_SPREAD): every wave takes a few
+        // instead of the first wave all of them
+        for (int f = MC_RING_SPREAD ? (lane * NW + wv) : t; f < s_ndef; f += T) {
             const int q = sring[f];
             const int r = spar[q];
             const double4 a = spt[q];
