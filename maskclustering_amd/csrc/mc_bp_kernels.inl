@@ -141,15 +141,12 @@ __device__ __forceinline__ void block_minmax3_nw(double mn[3], double mx[3], dou
         }
     }
     __syncthreads();
+    // the NW partials of each component across the lanes of every wave, then a wave reduction (not
+    // 6 * NW values per lane: unrolled, those spilled to scratch in the 16-wave classes)
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-        double a = red[c * NW], b = red[3 * NW + c * NW];
-        for (int w = 1; w < NW; w++) {
-            a = fmin(a, red[c * NW + w]);
-            b = fmax(b, red[3 * NW + c * NW + w]);
-        }
-        mn[c] = a;
-        mx[c] = b;
+        mn[c] = wave_min_d(lane < NW ? red[c * NW + lane] : DBL_MAX);
+        mx[c] = wave_max_d(lane < NW ? red[3 * NW + c * NW + lane] : -DBL_MAX);
     }
     __syncthreads();
 }
