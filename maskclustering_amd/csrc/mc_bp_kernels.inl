@@ -562,6 +562,21 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
+#ifndef MC_RING_SPREAD
+#define MC_RING_SPREAD 0  // ring search: deferred points dealt over the waves (A/B knob)
+#endif
+#ifndef MC_EPS_CULL
+#define MC_EPS_CULL 1  // eps lists: neighbour cells beyond eps (face distance) not walked (0: A/B baseline)
+#endif
+#ifndef MC_KNN_CULL
+#define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
+#endif
+#ifndef MC_ABLATE_VX
+#define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
+#endif
+#ifndef MC_VX_RANGES
+#define MC_VX_RANGES 1  // voxel phase 3 by per-wave pixel ranges where the counts fit the hash space (0: A/B)
+#endif
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
 // (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
@@ -721,21 +736,59 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
-#ifndef MC_RING_SPREAD
-#define MC_RING_SPREAD 0  // ring search: deferred points dealt over the waves (A/B knob)
-#endif
-#ifndef MC_EPS_CULL
-#define MC_EPS_CULL 1  // eps lists: neighbour cells beyond eps (face distance) not walked (0: A/B baseline)
-#endif
-#ifndef MC_KNN_CULL
-#define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
-#endif
-#ifndef MC_ABLATE_VX
-#define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
-#endif
-        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the
-                                                  // LDS-only barriers below
-        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 ? 0 : n); c0 += kVxT) {
+        //    Where every wave's per-voxel counts fit the (now free) hash arrays (NW * nv <= 2 * kVxH):
+        //    wave w takes the contiguous pixel range [w n / NW, (w + 1) n / NW); (a) it counts its pixels
+        //    per voxel into a row of its own, (b) a thread per voxel turns the rows into start positions
+        //    (the voxel's offset + the counts of the waves before), (c) the wave walks its range again in
+        //    order and places each pixel at its row's cursor (ranks within a 64-pixel step by ballot
+        //    groups): pixel order within every voxel with two barriers instead of NW per 512-pixel chunk.
+        const bool ranges = MC_VX_RANGES && MC_ABLATE_VX != 1 && nv * NW <= 2 * kVxH;
+        if (ranges) {
+            sync_global();  // the ranges read voxel ids other waves stored in 1.
+            auto row = [&](int w) {
+                return reinterpret_cast<int *>(w < NW / 2 ? hkey : hval) + (w % (NW / 2)) * nv;
+            };
+            int *const mine = row(wv);
+            for (int i = lane; i < nv; i += 64) mine[i] = 0;
+            const int lo = static_cast<int>(static_cast<long long>(n) * wv / NW),
+                      hi = static_cast<int>(static_cast<long long>(n) * (wv + 1) / NW);
+            for (int k = lo + lane; k < hi; k += 64) atomicAdd(&mine[pvid[base + k]], 1);
+            __syncthreads();
+            for (int v = t; v < nv; v += kVxT) {
+                int run = vcur[v];
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    int *const r = row(w);
+                    const int c = r[v];
+                    r[v] = run;
+                    run += c;
+                }
+                vcur[v] = run;  // end of voxel v's list, as 4. expects
+            }
+            __syncthreads();
+            int vn = lo + lane < hi ? pvid[base + lo + lane] : -1;
+            for (int k0 = lo; k0 < hi; k0 += 64) {
+                const int k = k0 + lane;
+                const int v = vn;
+                vn = k + 64 < hi ? pvid[base + k + 64] : -1;
+                unsigned long long act = __ballot(v >= 0);
+                int pos = 0;
+                while (act) {
+                    const int L = __ffsll(static_cast<long long>(act)) - 1;
+                    const int vv = __shfl(v, L, 64);
+                    const unsigned long long m = __ballot(v == vv);
+                    int b = 0;
+                    if (lane == L) b = atomicAdd(&mine[vv], __popcll(m));
+                    b = __shfl(b, L, 64);
+                    if (v == vv) pos = b + __popcll(m & ((1ull << lane) - 1ull));
+                    act &= ~m;
+                }
+                if (v >= 0) vlist[base + pos] = k;
+            }
+        }
+        int vnext = !ranges && t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across
+                                                             // the LDS-only barriers below
+        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 || ranges ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
             const int v = vnext;
             vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
