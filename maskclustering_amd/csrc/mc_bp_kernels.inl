@@ -575,7 +575,7 @@ __device__ __forceinline__ void lds_barrier()
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
 #ifndef MC_VX_RANGES
-#define MC_VX_RANGES 1  // voxel phase 3 by per-wave pixel ranges where the counts fit the hash space (0: A/B)
+#define MC_VX_RANGES 0  // voxel phase 3 by per-wave pixel ranges where the counts fit the hash space (A/B knob)
 #endif
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
