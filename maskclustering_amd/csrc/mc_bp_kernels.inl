@@ -574,6 +574,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
+#ifndef MC_VX_SUM8
+#define MC_VX_SUM8 0  // voxel phase 4: eight points per step on long lists (A/B knob)
+#endif
 #ifndef MC_VX_RANGES
 #define MC_VX_RANGES 0  // voxel phase 3 by per-wave pixel ranges where the counts fit the hash space (A/B knob)
 #endif
@@ -822,6 +825,25 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
+#if MC_VX_SUM8
+            // long lists (close views: a voxel under 100+ pixels): eight points' loads in flight
+            for (; j + 8 <= b1; j += 8) {
+                double px[8], py[8], pz[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const double *q = pp + 3 * vl[j + u];
+                    px[u] = q[0];
+                    py[u] = q[1];
+                    pz[u] = q[2];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    ax = ax + px[u];
+                    ay = ay + py[u];
+                    az = az + pz[u];
+                }
+            }
+#endif
             for (; j + 4 <= b1; j += 4) {
                 const double *q[4];
 #pragma unroll
