@@ -574,6 +574,9 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
+#ifndef MC_VX_P1RANGES
+#define MC_VX_P1RANGES 0  // voxel phase 1 by per-wave pixel ranges (A/B knob)
+#endif
 #ifndef MC_VX_SUM8
 #define MC_VX_SUM8 0  // voxel phase 4: eight points per step on long lists (A/B knob)
 #endif
@@ -615,6 +618,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
     __shared__ double red[6 * NW];
     __shared__ int ws[NW];
     __shared__ int s_flag;
+    __shared__ int s_wcnt[NW];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
@@ -667,7 +671,90 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
         // 1. voxel ids in first-occurrence order, per-pixel ids, per-voxel counts
         int nv = 0;
-        for (int c0 = 0; c0 < n; c0 += kVxT) {
+        if (MC_VX_P1RANGES) {
+            // by per-wave pixel ranges with four barriers per slot instead of four per 512-pixel chunk:
+            // (a) keys into the hash, each entry's first pixel by atomicMin of the pixel index, the
+            // entry per pixel in pvid; (b) each wave flags and counts the first pixels of its range;
+            // (c) the first pixels numbered in pixel order (wave bases from the counts, ballot ranks
+            // within a wave), the number into the entry; (d) every pixel its voxel id and count
+            constexpr int kFirst = 1 << 30;
+            const int lo = static_cast<int>(static_cast<long long>(n) * wv / NW),
+                      hi = static_cast<int>(static_cast<long long>(n) * (wv + 1) / NW);
+            for (int k = lo + lane; k < hi; k += 64) {
+                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
+                unsigned key = 0;
+                bool fits = true;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const double r = floor((p[c] - vmin[c]) / pr.vs);
+                    fits = fits && r >= 0.0 && r < 1024.0;
+                    key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
+                }
+                int h = -1;
+                if (!fits) {
+                    s_flag = 1;
+                } else {
+                    unsigned e = mod_mul(key * 0x9E3779B1u, kVxH);
+                    for (int probe = 0; probe < kVxH; probe++) {
+                        unsigned cur = hkey[e];
+                        if (cur == kVxEmpty) {
+                            cur = atomicCAS(&hkey[e], kVxEmpty, key);
+                            if (cur == kVxEmpty) cur = key;
+                        }
+                        if (cur == key) {
+                            h = static_cast<int>(e);
+                            break;
+                        }
+                        e = e + 1 == kVxH ? 0u : e + 1;
+                    }
+                    if (h < 0) s_flag = 1;
+                    else atomicMin(&hval[h], static_cast<unsigned>(k));
+                }
+                pvid[base + k] = h;
+            }
+            sync_global();
+            int mine = 0;
+            for (int k = lo + lane; k < hi; k += 64) {
+                const int h = pvid[base + k];
+                if (h >= 0 && hval[h] == static_cast<unsigned>(k)) {
+                    pvid[base + k] = h | kFirst;
+                    mine++;
+                }
+            }
+            mine = wave_sum(mine);
+            if (lane == 0) s_wcnt[wv] = mine;
+            sync_global();
+            int run = 0;
+            for (int w = 0; w < NW; w++) {
+                nv += s_wcnt[w];
+                run += w < wv ? s_wcnt[w] : 0;
+            }
+            for (int k0 = lo; k0 < hi; k0 += 64) {
+                const int k = k0 + lane;
+                const int h = k < hi ? pvid[base + k] : -1;
+                const bool f = h >= 0 && (h & kFirst);
+                const unsigned long long m = __ballot(f);
+                if (f) {
+                    const int v = run + __popcll(m & ((1ull << lane) - 1ull));
+                    if (v < kVxV) hval[h & ~kFirst] = static_cast<unsigned>(v);
+                    else s_flag = 1;
+                }
+                run += __popcll(m);
+            }
+            __syncthreads();
+            for (int k = lo + lane; k < hi; k += 64) {
+                const int h = pvid[base + k] & ~kFirst;
+                if (h >= 0) {
+                    const unsigned v = hval[h];
+                    if (v < static_cast<unsigned>(kVxV)) {
+                        pvid[base + k] = static_cast<int>(v);
+                        atomicAdd(&vcur[v], 1);
+                    }
+                }
+            }
+            sync_global();  // 3. reads ids other waves stored
+        }
+        for (int c0 = 0; c0 < (MC_VX_P1RANGES ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
             int h = -1;
             if (k < n) {

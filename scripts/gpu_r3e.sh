@@ -13,8 +13,10 @@ OUT=$OUT/api timeout -k 10 900 bash scripts/gpu_api.sh || { echo "api failed"; e
 step n2_e2e_c2 300 env MC_BENCH_BACKEND=gloo MC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --shape c2 --steps 3 --warmup 1 --no-secondary
 step stamps 240 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_stamps.so python scripts/bp_stamps.py c3 600 100
-echo "== spread / minmax A/B $(date +%T)"
-OUT=$OUT/ab_spread_mm LIBS="maskclustering_amd/libmcgraph_prev.so maskclustering_amd/libmcgraph_spread.so maskclustering_amd/libmcgraph.so maskclustering_amd/libmcgraph_vr.so maskclustering_amd/libmcgraph_vs.so" SHAPES="c3:600:100 c2:0:250" REPS=1 \
-    timeout -k 10 600 bash scripts/gpu_ab_s1.sh || { echo "spread A/B failed"; exit 1; }
 step pytest_vr 200 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_vr.so python -u -m pytest tests/test_gpu_s1.py -x -q \
     --timeout 120 --timeout-method thread -m gpu
+step pytest_p1 200 env MCGRAPH_LIB=maskclustering_amd/libmcgraph_p1.so python -u -m pytest tests/test_gpu_s1.py -x -q \
+    --timeout 120 --timeout-method thread -m gpu
+echo "== spread / minmax A/B $(date +%T)"
+OUT=$OUT/ab_spread_mm LIBS="maskclustering_amd/libmcgraph_prev.so maskclustering_amd/libmcgraph_spread.so maskclustering_amd/libmcgraph.so maskclustering_amd/libmcgraph_vr.so maskclustering_amd/libmcgraph_vs.so maskclustering_amd/libmcgraph_p1.so" SHAPES="c3:600:100 c2:0:250" REPS=1 \
+    timeout -k 10 540 bash scripts/gpu_ab_s1.sh || { echo "spread A/B failed"; exit 1; }
