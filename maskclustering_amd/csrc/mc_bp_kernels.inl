@@ -562,26 +562,11 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
-#ifndef MC_RING_SPREAD
-#define MC_RING_SPREAD 0  // ring search: deferred points dealt over the waves (A/B knob)
-#endif
-#ifndef MC_EPS_CULL
-#define MC_EPS_CULL 1  // eps lists: neighbour cells beyond eps (face distance) not walked (0: A/B baseline)
-#endif
 #ifndef MC_KNN_CULL
 #define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
 #endif
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
-#endif
-#ifndef MC_VX_P1RANGES
-#define MC_VX_P1RANGES 0  // voxel phase 1 by per-wave pixel ranges (A/B knob)
-#endif
-#ifndef MC_VX_SUM8
-#define MC_VX_SUM8 0  // voxel phase 4: eight points per step on long lists (A/B knob)
-#endif
-#ifndef MC_VX_RANGES
-#define MC_VX_RANGES 0  // voxel phase 3 by per-wave pixel ranges where the counts fit the hash space (A/B knob)
 #endif
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
@@ -618,7 +603,6 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
     __shared__ double red[6 * NW];
     __shared__ int ws[NW];
     __shared__ int s_flag;
-    __shared__ int s_wcnt[NW];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
@@ -671,90 +655,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
         // 1. voxel ids in first-occurrence order, per-pixel ids, per-voxel counts
         int nv = 0;
-        if (MC_VX_P1RANGES) {
-            // by per-wave pixel ranges with four barriers per slot instead of four per 512-pixel chunk:
-            // (a) keys into the hash, each entry's first pixel by atomicMin of the pixel index, the
-            // entry per pixel in pvid; (b) each wave flags and counts the first pixels of its range;
-            // (c) the first pixels numbered in pixel order (wave bases from the counts, ballot ranks
-            // within a wave), the number into the entry; (d) every pixel its voxel id and count
-            constexpr int kFirst = 1 << 30;
-            const int lo = static_cast<int>(static_cast<long long>(n) * wv / NW),
-                      hi = static_cast<int>(static_cast<long long>(n) * (wv + 1) / NW);
-            for (int k = lo + lane; k < hi; k += 64) {
-                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
-                unsigned key = 0;
-                bool fits = true;
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    const double r = floor((p[c] - vmin[c]) / pr.vs);
-                    fits = fits && r >= 0.0 && r < 1024.0;
-                    key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
-                }
-                int h = -1;
-                if (!fits) {
-                    s_flag = 1;
-                } else {
-                    unsigned e = mod_mul(key * 0x9E3779B1u, kVxH);
-                    for (int probe = 0; probe < kVxH; probe++) {
-                        unsigned cur = hkey[e];
-                        if (cur == kVxEmpty) {
-                            cur = atomicCAS(&hkey[e], kVxEmpty, key);
-                            if (cur == kVxEmpty) cur = key;
-                        }
-                        if (cur == key) {
-                            h = static_cast<int>(e);
-                            break;
-                        }
-                        e = e + 1 == kVxH ? 0u : e + 1;
-                    }
-                    if (h < 0) s_flag = 1;
-                    else atomicMin(&hval[h], static_cast<unsigned>(k));
-                }
-                pvid[base + k] = h;
-            }
-            sync_global();
-            int mine = 0;
-            for (int k = lo + lane; k < hi; k += 64) {
-                const int h = pvid[base + k];
-                if (h >= 0 && hval[h] == static_cast<unsigned>(k)) {
-                    pvid[base + k] = h | kFirst;
-                    mine++;
-                }
-            }
-            mine = wave_sum(mine);
-            if (lane == 0) s_wcnt[wv] = mine;
-            sync_global();
-            int run = 0;
-            for (int w = 0; w < NW; w++) {
-                nv += s_wcnt[w];
-                run += w < wv ? s_wcnt[w] : 0;
-            }
-            for (int k0 = lo; k0 < hi; k0 += 64) {
-                const int k = k0 + lane;
-                const int h = k < hi ? pvid[base + k] : -1;
-                const bool f = h >= 0 && (h & kFirst);
-                const unsigned long long m = __ballot(f);
-                if (f) {
-                    const int v = run + __popcll(m & ((1ull << lane) - 1ull));
-                    if (v < kVxV) hval[h & ~kFirst] = static_cast<unsigned>(v);
-                    else s_flag = 1;
-                }
-                run += __popcll(m);
-            }
-            __syncthreads();
-            for (int k = lo + lane; k < hi; k += 64) {
-                const int h = pvid[base + k] & ~kFirst;
-                if (h >= 0) {
-                    const unsigned v = hval[h];
-                    if (v < static_cast<unsigned>(kVxV)) {
-                        pvid[base + k] = static_cast<int>(v);
-                        atomicAdd(&vcur[v], 1);
-                    }
-                }
-            }
-            sync_global();  // 3. reads ids other waves stored
-        }
-        for (int c0 = 0; c0 < (MC_VX_P1RANGES ? 0 : n); c0 += kVxT) {
+        for (int c0 = 0; c0 < n; c0 += kVxT) {
             const int k = c0 + t;
             int h = -1;
             if (k < n) {
@@ -826,59 +727,9 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
-        //    Where every wave's per-voxel counts fit the (now free) hash arrays (NW * nv <= 2 * kVxH):
-        //    wave w takes the contiguous pixel range [w n / NW, (w + 1) n / NW); (a) it counts its pixels
-        //    per voxel into a row of its own, (b) a thread per voxel turns the rows into start positions
-        //    (the voxel's offset + the counts of the waves before), (c) the wave walks its range again in
-        //    order and places each pixel at its row's cursor (ranks within a 64-pixel step by ballot
-        //    groups): pixel order within every voxel with two barriers instead of NW per 512-pixel chunk.
-        const bool ranges = MC_VX_RANGES && MC_ABLATE_VX != 1 && nv * NW <= 2 * kVxH;
-        if (ranges) {
-            sync_global();  // the ranges read voxel ids other waves stored in 1.
-            auto row = [&](int w) {
-                return reinterpret_cast<int *>(w < NW / 2 ? hkey : hval) + (w % (NW / 2)) * nv;
-            };
-            int *const mine = row(wv);
-            for (int i = lane; i < nv; i += 64) mine[i] = 0;
-            const int lo = static_cast<int>(static_cast<long long>(n) * wv / NW),
-                      hi = static_cast<int>(static_cast<long long>(n) * (wv + 1) / NW);
-            for (int k = lo + lane; k < hi; k += 64) atomicAdd(&mine[pvid[base + k]], 1);
-            __syncthreads();
-            for (int v = t; v < nv; v += kVxT) {
-                int run = vcur[v];
-#pragma unroll
-                for (int w = 0; w < NW; w++) {
-                    int *const r = row(w);
-                    const int c = r[v];
-                    r[v] = run;
-                    run += c;
-                }
-                vcur[v] = run;  // end of voxel v's list, as 4. expects
-            }
-            __syncthreads();
-            int vn = lo + lane < hi ? pvid[base + lo + lane] : -1;
-            for (int k0 = lo; k0 < hi; k0 += 64) {
-                const int k = k0 + lane;
-                const int v = vn;
-                vn = k + 64 < hi ? pvid[base + k + 64] : -1;
-                unsigned long long act = __ballot(v >= 0);
-                int pos = 0;
-                while (act) {
-                    const int L = __ffsll(static_cast<long long>(act)) - 1;
-                    const int vv = __shfl(v, L, 64);
-                    const unsigned long long m = __ballot(v == vv);
-                    int b = 0;
-                    if (lane == L) b = atomicAdd(&mine[vv], __popcll(m));
-                    b = __shfl(b, L, 64);
-                    if (v == vv) pos = b + __popcll(m & ((1ull << lane) - 1ull));
-                    act &= ~m;
-                }
-                if (v >= 0) vlist[base + pos] = k;
-            }
-        }
-        int vnext = !ranges && t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across
-                                                             // the LDS-only barriers below
-        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 || ranges ? 0 : n); c0 += kVxT) {
+        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the
+                                                  // LDS-only barriers below
+        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
             const int v = vnext;
             vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
@@ -912,25 +763,6 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
-#if MC_VX_SUM8
-            // long lists (close views: a voxel under 100+ pixels): eight points' loads in flight
-            for (; j + 8 <= b1; j += 8) {
-                double px[8], py[8], pz[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const double *q = pp + 3 * vl[j + u];
-                    px[u] = q[0];
-                    py[u] = q[1];
-                    pz[u] = q[2];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    ax = ax + px[u];
-                    ay = ay + py[u];
-                    az = az + pz[u];
-                }
-            }
-#endif
             for (; j + 4 <= b1; j += 4) {
                 const double *q[4];
 #pragma unroll
@@ -1517,45 +1349,17 @@ __device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
     return 3u - (d2 < pr.knn_r2[0] ? 1u : 0u) - (d2 < pr.knn_r2[1] ? 1u : 0u) - (d2 < pr.knn_r2[2] ? 1u : 0u);
 }
 
-// Lower bound on the squared distance from a point to any point of the neighbour cell at offset
-// (dx, dy, dz) in {-1, 0, 1}^3, from the point's offsets o in its own cell (cells of width ce): the
-// gaps to the shared faces, each shrunk by 1e-9 ce so the bound stays below the computed d2 of every
-// point of the cell (cell indices come from the same floor((p - min) / ce)).  A cell with a bound
-// >= eps2 holds no point within eps and is not walked (MC_EPS_CULL); the lists are unchanged.
-struct CellOff {
-    double o[3];
-    double ce;
-};
-__device__ __forceinline__ CellOff cell_off(double ax, double ay, double az, const double (&mn)[3], int x, int y, int z,
-                                            double ce)
-{
-    CellOff c;
-    c.o[0] = fmin(fmax(ax - mn[0] - x * ce, 0.0), ce);
-    c.o[1] = fmin(fmax(ay - mn[1] - y * ce, 0.0), ce);
-    c.o[2] = fmin(fmax(az - mn[2] - z * ce, 0.0), ce);
-    c.ce = ce;
-    return c;
-}
-__device__ __forceinline__ double cell_lb2(const CellOff &c, int dx, int dy, int dz)
-{
-    const double sl = 1e-9 * c.ce;
-    auto g = [&](int d, double o) { return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? c.ce - o : o) - sl); };
-    const double gx = g(dx, c.o[0]), gy = g(dy, c.o[1]), gz = g(dz, c.o[2]);
-    return (gx * gx + gy * gy) + gz * gz;
-}
-
 // The eps-neighbour list of sorted position q (point a, cell (x, y, z)): every point of the 27 cells
 // with d2 < eps2 (self included), in cell-walk order.  One predicate per candidate (cell key and
 // distance together, the record loaded whole) and one store; entries past kBpNbCap overwrite the
 // last slot (the list is unused then: the point walks its cells).  Returns the count.
 template <int N>
 __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q, const CellOff &co)
+                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
         if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
-        if (MC_EPS_CULL && !(cell_lb2(co, d % 3 - 1, (d / 3) % 3 - 1, d / 9 - 1) < pr.eps2)) return make_int2(0, 0);
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(g.bs[b], g.bs[b + 1]);
@@ -1597,14 +1401,11 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 // (the union and the border labels are order-free, the k-NN sorts).
 template <int N>
 __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag,
-                                              const CellOff &co)
+                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
         if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
-        if (MC_EPS_CULL && d != 13 && !(cell_lb2(co, d % 3 - 1, (d / 3) % 3 - 1, d / 9 - 1) < pr.eps2))
-            return make_int2(0, 0);
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
@@ -1881,8 +1682,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) {
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
-                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
-                                 cell_off(spt[q].x, spt[q].y, spt[q].z, mn, x, y, z, pr.ce));
+                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag);
             }
             sync_global();  // the lists hold other waves' stores
         } else {
@@ -1890,7 +1690,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
                 const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q, cell_off(ax, ay, az, mn, x, y, z, pr.ce));
+                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
                 spar[q] = q;
             }
         }
@@ -2140,9 +1940,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         for (int f = t; f < s_ndef; f += T) sfb[atomicAdd(&sfb[kFbCount], 1)] = spar[sring[f]];
         if (false)
 #endif
-        // deferred point f on lane f / NW of wave f % NW (MC_RING_SPREAD): every wave takes a few
-        // instead of the first wave all of them
-        for (int f = MC_RING_SPREAD ? (lane * NW + wv) : t; f < s_ndef; f += T) {
+        for (int f = t; f < s_ndef; f += T) {
             const int q = sring[f];
             const int r = spar[q];
             const double4 a = spt[q];
