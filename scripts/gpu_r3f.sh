@@ -1,0 +1,5 @@
+#!/usr/bin/env bash
+# Final round-3 measurement on the default build: every GPU test, smoke, bench, rocprofv3 stats, PMC traffic.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${OUT:-gpurun_out/v7} bash scripts/gpu_round.sh
