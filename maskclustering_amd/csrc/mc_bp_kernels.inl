@@ -1944,12 +1944,15 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         if (false)
 #endif
 #if MC_RING_PAIRS
-        // two lanes per deferred point (lanes 2i and 2i + 1): they take the cells of each ring in
-        // turn; the even lane keeps the point's list, the odd lane's list of the ring is merged into
-        // it at the ring's end (values by shuffles, sorted inserts) and emptied, so the even lane's
-        // k-th distance is the pair's, which both lanes cull against and the ring test reads
-        for (int f = t >> 1; f < s_ndef; f += T >> 1) {  // the same f on both lanes of a pair
-            const int half = t & 1;
+        // G = MC_RING_PAIRS lanes per deferred point (lanes Gi .. Gi + G - 1): they take the cells of
+        // each ring in turn; the first lane keeps the point's list, the others' lists of the ring are
+        // merged into it at the ring's end (values by shuffles, sorted inserts) and emptied, so the
+        // first lane's k-th distance is the group's, which all cull against and the ring test reads
+        constexpr int G = MC_RING_PAIRS;
+        static_assert(G == 2 || G == 4, "lane groups of 2 or 4");
+        for (int f = t / G; f < s_ndef; f += T / G) {  // the same f on every lane of a group
+            const int half = t % G;
+            const int lead = lane & ~(G - 1);
             const int q = sring[f];
             const int r = spar[q];
             const double4 a = spt[q];
@@ -1979,23 +1982,28 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         const int step = (edge || R == 0) ? 1 : 2 * R;
                         const double gyz = gap(dy, oy) * gap(dy, oy) + gap(dz, oz) * gap(dz, oz);
                         for (int dx = -R; dx <= R; dx += step) {
-                            const bool mine = (cidx++ & 1) == half;
+                            const bool mine = (cidx++ % G) == half;
                             if (!mine || gyz + gap(dx, ox) * gap(dx, ox) >= fmin(th, best[kBpKnnMax - 1])) continue;
                             lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
                         }
                     }
 #pragma unroll
-                for (int k = 0; k < kBpKnnMax; k++) {
-                    const double v = __shfl_xor(best[k], 1, 64);
-                    if (half == 0) sorted_insert(best, v);
-                }
-                if (half == 1) {
+                for (int j = 1; j < G; j++)
+#pragma unroll
+                    for (int k = 0; k < kBpKnnMax; k++) {
+                        const double v = __shfl(best[k], lead + j, 64);
+                        if (half == 0) sorted_insert(best, v);
+                    }
+                if (half != 0) {
 #pragma unroll
                     for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
                 }
-                found_all += found + __shfl_xor(found, 1, 64);
+                int fs = found;
+#pragma unroll
+                for (int d = 1; d < G; d <<= 1) fs += __shfl_xor(fs, d, 64);
+                found_all += fs;
                 found = 0;
-                th = __shfl(best[kBpKnnMax - 1], lane & ~1, 64);
+                th = __shfl(best[kBpKnnMax - 1], lead, 64);
                 const double reach = static_cast<double>(R) * pr.ce;
                 done = found_all >= kk && th < reach * reach * (1.0 - 1e-9);
             }
