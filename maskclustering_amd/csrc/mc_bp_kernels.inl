@@ -562,9 +562,6 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
-#ifndef MC_RING_PAIRS
-#define MC_RING_PAIRS 0  // ring search by lane pairs (A/B knob)
-#endif
 #ifndef MC_KNN_CULL
 #define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
 #endif
@@ -1941,78 +1938,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #endif
 #if MC_KNN_RING == 0
         for (int f = t; f < s_ndef; f += T) sfb[atomicAdd(&sfb[kFbCount], 1)] = spar[sring[f]];
-        if (false)
-#endif
-#if MC_RING_PAIRS
-        // G = MC_RING_PAIRS lanes per deferred point (lanes Gi .. Gi + G - 1): they take the cells of
-        // each ring in turn; the first lane keeps the point's list, the others' lists of the ring are
-        // merged into it at the ring's end (values by shuffles, sorted inserts) and emptied, so the
-        // first lane's k-th distance is the group's, which all cull against and the ring test reads
-        constexpr int G = MC_RING_PAIRS;
-        static_assert(G == 2 || G == 4, "lane groups of 2 or 4");
-        for (int f = t / G; f < s_ndef; f += T / G) {  // the same f on every lane of a group
-            const int half = t % G;
-            const int lead = lane & ~(G - 1);
-            const int q = sring[f];
-            const int r = spar[q];
-            const double4 a = spt[q];
-            double best[kBpKnnMax];
-#pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-            int found = 0, found_all = 0;
-            bool done = false;
-            int x, y, z;
-            unpack3(keyof(q), x, y, z);
-            auto take = [&](int, double d2) {
-                sorted_insert(best, d2);
-                found++;
-            };
-            const double ce = pr.ce, sl = 1e-9 * pr.ce;
-            const double ox = fmin(fmax(a.x - mn[0] - x * ce, 0.0), ce), oy = fmin(fmax(a.y - mn[1] - y * ce, 0.0), ce),
-                         oz = fmin(fmax(a.z - mn[2] - z * ce, 0.0), ce);
-            auto gap = [&](int d, double o) {
-                return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? d * ce - o : -d * ce - (ce - o)) - sl);
-            };
-            double th = DBL_MAX;  // the pair's k-th distance at the last ring end
-            int cidx = 0;
-            for (int R = 0; R <= 2 && !done; R++) {
-                for (int dz = -R; dz <= R; dz++)
-                    for (int dy = -R; dy <= R; dy++) {
-                        const bool edge = dz == -R || dz == R || dy == -R || dy == R;
-                        const int step = (edge || R == 0) ? 1 : 2 * R;
-                        const double gyz = gap(dy, oy) * gap(dy, oy) + gap(dz, oz) * gap(dz, oz);
-                        for (int dx = -R; dx <= R; dx += step) {
-                            const bool mine = (cidx++ % G) == half;
-                            if (!mine || gyz + gap(dx, ox) * gap(dx, ox) >= fmin(th, best[kBpKnnMax - 1])) continue;
-                            lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
-                        }
-                    }
-#pragma unroll
-                for (int j = 1; j < G; j++)
-#pragma unroll
-                    for (int k = 0; k < kBpKnnMax; k++) {
-                        const double v = __shfl(best[k], lead + j, 64);
-                        if (half == 0) sorted_insert(best, v);
-                    }
-                if (half != 0) {
-#pragma unroll
-                    for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-                }
-                int fs = found;
-#pragma unroll
-                for (int d = 1; d < G; d <<= 1) fs += __shfl_xor(fs, d, 64);
-                found_all += fs;
-                found = 0;
-                th = __shfl(best[kBpKnnMax - 1], lead, 64);
-                const double reach = static_cast<double>(R) * pr.ce;
-                done = found_all >= kk && th < reach * reach * (1.0 - 1e-9);
-            }
-            if (!done) {
-                if (half == 0) sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
-                continue;
-            }
-            if (half == 0) put_mean(r, best);
-        }
         if (false)
 #endif
         for (int f = t; f < s_ndef; f += T) {
