@@ -2084,18 +2084,25 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         const int vx_global = getenv("MC_VX_GLOBAL") ? atoi(getenv("MC_VX_GLOBAL")) : 0;
         // frames per batch: bounded pixel capacity of the per-slot arrays (≈ 200 B of per-batch arrays
         // per pixel).  Large batches amortise every group's slot tail and the per-batch sync (C3 E2E:
-        // 192 M pixels 215 ms, 400 M 184 ms, 600 M 175 ms per scene), so the batch takes up to 640 M
-        // pixels (≈ 130 GB of the 288 GB) or 45 % of the free HBM, whichever is less.
-        size_t budget = static_cast<size_t>(640) << 20;
+        // 192 M pixels 215 ms, 400 M 184 ms, 600 M 175 ms per scene in round 2; 1 G 115 ms against
+        // 118 ms at the old 640 M / 45 % cap in round 3, profiles/r03/ab19_batch_pixels.jsonl), so the
+        // batch takes up to 1 G pixels or 65 % of the free HBM (≈ 170 GB of a fresh 288 GB device),
+        // whichever is less; the frames are then dealt into equal batches, so that no batch is a small
+        // remainder with its own tails
+        size_t budget = static_cast<size_t>(1) << 30;
         if (ctx->bp_px_cap < budget) {
             size_t free_b = 0, total_b = 0;
             if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
                 budget = std::max<size_t>(static_cast<size_t>(16) << 20,
-                                          std::min(budget, (free_b + ctx->bp_px_cap * 200) / 100 * 45 / 200));
+                                          std::min(budget, (free_b + ctx->bp_px_cap * 200) / 100 * 65 / 200));
         }
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         BpUpload *const up = on_device ? ctx->bp_up : nullptr;
         int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
+        {
+            const int nb = (std::max(F, 1) + FB - 1) / FB;
+            FB = (std::max(F, 1) + nb - 1) / nb;
+        }
         // frames arriving from the host: batch b + 1's upload runs under batch b's compute.  Splitting a
         // scene that fits one batch into more batches only to overlap its upload did not pay (C2 API
         // path: 1 batch 44.9 ms, 8 batches 46.2 ms, profiles/r03/api/), so by default only scenes of
