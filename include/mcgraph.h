@@ -118,6 +118,9 @@ int mc_ctx_set_timing(mc_ctx *ctx, int enable);
 int mc_ctx_set_timing_filter(mc_ctx *ctx, const char *kernel);  /* NULL/"" = every kernel group */
 int mc_ctx_get_kernel_time(mc_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int mc_ctx_reset_kernel_times(mc_ctx *ctx);
+/* diagnostics: out[0] = 1 if the library was built with in-kernel invariant checks
+   (-DMC_DBG_CHECK=1), out[1 + k] = failures of check kind k so far; n <= 9 */
+int mc_debug_counters(mc_ctx *ctx, int64_t *out, int32_t n, int reset);
 
 /* ---- scene input (the S1 output: per-frame mask point sets) ---------------
  * mask_col/label/off are host arrays of length M_in, M_in, M_in+1.

@@ -467,6 +467,24 @@ int mc_ctx_reset_kernel_times(mc_ctx *ctx)
     });
 }
 
+int mc_debug_counters(mc_ctx *ctx, int64_t *out, int32_t n, int reset)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(out && n >= 1 && n <= 9, MC_ERR_INVALID, "bad counter array");
+        MC_HIP(hipDeviceSynchronize());
+        unsigned long long c[8] = {};
+        MC_HIP(hipMemcpyFromSymbol(c, HIP_SYMBOL(mc::g_bp_dbg), sizeof(c)));
+        out[0] = MC_DBG_CHECK ? 1 : 0;
+        for (int k = 1; k < n; k++) out[k] = static_cast<int64_t>(c[k - 1]);
+        if (reset) {
+            const unsigned long long z[8] = {};
+            const unsigned zp = 0;
+            MC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_dbg), z, sizeof(z)));
+            MC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_dbg_printed), &zp, sizeof(zp)));
+        }
+    });
+}
+
 // ---------------------------------------------------------------------------------------------
 // scene input
 // ---------------------------------------------------------------------------------------------
@@ -2158,6 +2176,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         dv.nbands = nbands;
         // the pixel kernels' uchar4 / float4 loads need aligned frames (a caller's tensor view may start
         // at any element); every batch starts HW pixels further on, a multiple of 4 when W is
+        // test knob: eps lists read only up to MC_BP_NBCAP entries (the rest take the cell walks)
+        dv.nbcap = mc::kBpNbCap;
+        if (const char *e = getenv("MC_BP_NBCAP")) dv.nbcap = std::min(mc::kBpNbCap, std::max(1, atoi(e)));
         dv.vec4 = (W % 4 == 0 && reinterpret_cast<uintptr_t>(dep) % 16 == 0 && reinterpret_cast<uintptr_t>(sg) % 4 == 0)
                       ? 1 : 0;
 

@@ -37,6 +37,7 @@ struct BpDev {
     float r2, scene_inv;
     int minpts, knn, kball, few;
     int H, W, nbands;
+    int nbcap;  // eps lists read only for counts <= nbcap (<= kBpNbCap; smaller: a test knob for the cell-walk paths)
     int vec4;  // W % 4 == 0 with a 16-byte aligned depth and a 4-byte aligned seg pointer: 4 pixels per lane
 };
 
@@ -1178,9 +1179,6 @@ __device__ __forceinline__ double seq_add64_pos(double acc, double v)
     return acc;
 }
 
-#ifndef MC_DBG_CHECK
-#define MC_DBG_CHECK 0
-#endif
 // Size classes of the LDS-resident kernel: capacity N points, T threads, and the workgroups per CU
 // the LDS footprint (72 B per point) admits.  Slots of more than kBpLdsN voxels take k_bp_denoise.
 constexpr int kBpLdsN = 16384;  // largest class of the LDS-kernel template
@@ -1486,6 +1484,111 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
     z = static_cast<int>(k & 0x1FFFFF);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Diagnostics build only (-DMC_DBG_CHECK=1: scripts/build_variant.sh dbg): invariant checks inside the
+// LDS denoise classes, each against a direct recomputation from the cell-sorted points.  Kinds:
+//   0  a point's eps-neighbour count != the points within eps in its 27 cells
+//   1  a list the consumers read (count <= nbcap) whose entries (position | radius class) differ
+//      from those points as a multiset (sum and xor of a 64-bit mix of each entry)
+//   2  two core points within eps in different union-find components
+//   3  a kept point's mean k-NN distance != the brute-force mean over every kept point (bits)
+// Each failure is counted in g_bp_dbg[kind] (read by mc_debug_counters) and the first 16 printed.
+// ---------------------------------------------------------------------------------------------
+#ifndef MC_DBG_CHECK
+#define MC_DBG_CHECK 0
+#endif
+__device__ unsigned long long g_bp_dbg[8];
+__device__ unsigned g_bp_dbg_printed;
+__device__ __forceinline__ bool bp_dbg_fail(int kind)
+{
+    atomicAdd(&g_bp_dbg[kind], 1ull);
+    return atomicAdd(&g_bp_dbg_printed, 1u) < 16u;
+}
+__device__ __forceinline__ unsigned long long bp_dbg_mix(unsigned long long k)
+{
+    k *= 0x9E3779B97F4A7C15ull;
+    k ^= k >> 29;
+    k *= 0xBF58476D1CE4E5B9ull;
+    return k ^ (k >> 32);
+}
+template <int N>
+__device__ __noinline__ void bp_dbg_lists(const BpLdsGrid &g, const int *sflag, const unsigned short *nbw, int n,
+                                          const BpDev &pr, int slot)
+{
+    for (int q = threadIdx.x; q < n; q += blockDim.x) {
+        const double4 a = g.pt[q];
+        int x, y, z;
+        unpack3(static_cast<unsigned long long>(__double_as_longlong(a.w)) & ~kKeptBit, x, y, z);
+        int c = 0;
+        unsigned long long sum = 0, xr = 0;
+        lds_cells27(g, x, y, z, 0ull, a.x, a.y, a.z, [&](int q2, double d2) {
+            if (d2 < pr.eps2) {
+                const unsigned long long e = static_cast<unsigned>(q2) | (nb_class(d2, pr) << 14);
+                c++;
+                sum += bp_dbg_mix(e);
+                xr ^= bp_dbg_mix(e + 0x51ED2701ull);
+            }
+        });
+        const int cnt = nb_cnt(sflag[q]);
+        if (cnt != c) {
+            if (bp_dbg_fail(0)) printf("[bp dbg] N=%d slot=%d n=%d q=%d: list count %d, cells %d\n", N, slot, n, q, cnt, c);
+            continue;
+        }
+        if (cnt > pr.nbcap) continue;
+        unsigned long long s2 = 0, x2 = 0;
+        for (int k = 0; k < cnt; k++) {
+            const unsigned long long e = nbw[(static_cast<size_t>(k >> 3) * N + q) * 8 + (k & 7)];
+            s2 += bp_dbg_mix(e);
+            x2 ^= bp_dbg_mix(e + 0x51ED2701ull);
+        }
+        if (s2 != sum || x2 != xr)
+            if (bp_dbg_fail(1)) printf("[bp dbg] N=%d slot=%d n=%d q=%d: list entries differ (count %d)\n", N, slot, n, q, cnt);
+    }
+    sync_global();
+}
+template <int N>
+__device__ __noinline__ void bp_dbg_union(const BpLdsGrid &g, const int *spar, int n, const BpDev &pr, int slot)
+{
+    for (int q = threadIdx.x; q < n; q += blockDim.x) {
+        const int ra = spar[q];
+        if (ra < 0) continue;
+        const double4 a = g.pt[q];
+        int x, y, z;
+        unpack3(static_cast<unsigned long long>(__double_as_longlong(a.w)) & ~kKeptBit, x, y, z);
+        lds_cells27(g, x, y, z, 0ull, a.x, a.y, a.z, [&](int q2, double d2) {
+            const int rb = spar[q2];
+            if (d2 < pr.eps2 && rb >= 0 && rb != ra)
+                if (bp_dbg_fail(2)) printf("[bp dbg] N=%d slot=%d n=%d: core %d (root %d) and %d (root %d) apart\n", N, slot, n,
+                                           q, ra, q2, rb);
+        });
+    }
+    sync_global();
+}
+// kept point at sorted position q has rank spar[q] (< m) and its mean in savg[rank]
+template <int N>
+__device__ __noinline__ void bp_dbg_knn(const BpLdsGrid &g, const int *spar, const double *savg, int n, int kk, int slot)
+{
+    for (int q = threadIdx.x; q < n; q += blockDim.x) {
+        const double4 a = g.pt[q];
+        if (!(static_cast<unsigned long long>(__double_as_longlong(a.w)) & kKeptBit)) continue;
+        double best[kBpKnnMax];
+        for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+        for (int q2 = 0; q2 < n; q2++) {
+            const double4 p = g.pt[q2];
+            if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
+            const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+            sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
+        }
+        double sum = 0.0;
+        for (int k = 0; k < kk; k++) sum = sum + sqrt(best[k]);
+        const double want = sum / static_cast<double>(kk), got = savg[spar[q]];
+        if (__double_as_longlong(want) != __double_as_longlong(got))
+            if (bp_dbg_fail(3)) printf("[bp dbg] N=%d slot=%d n=%d q=%d: k-NN mean %.17g, brute force %.17g\n", N, slot, n, q,
+                                       got, want);
+    }
+    sync_global();
+}
+
 // Slots of each size class (unordered: every slot is processed independently); class kBpClasses =
 // more than kBpLdsN voxels (the global-memory kernel).  min_cls > 0 sends small slots to a larger
 // class (tests: every class gives the same results).  cls_cnt[kBpClasses + 1] must be zero.
@@ -1696,6 +1799,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         bar();
         BP_STAMP(21);
+        if constexpr (MC_DBG_CHECK) bp_dbg_lists<N>(g, sflag, nbw, n, pr, s);
         // 6. connected core points: list points first; points with more than kBpNbCap neighbours
         //    are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
         if (t == 0) s_ndef = 0;
@@ -1703,7 +1807,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         for (int q = t; q < n; q += T) {
             const int fl = sflag[q], cnt = nb_cnt(fl);
             if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
-            if (cnt > kBpNbCap) {
+            if (cnt > pr.nbcap) {
                 sX[atomicAdd(&s_ndef, 1)] = q;
                 continue;
             }
@@ -1782,6 +1886,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         bar();
         BP_STAMP(23);
+        if constexpr (MC_DBG_CHECK) bp_dbg_union<N>(g, spar, n, pr, s);
         // 8. labels and class counts (a border point joins the adjacent cluster of smallest key)
         for (int q = t; q < n; q += T) {
             int l;
@@ -1797,7 +1902,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         broot = r2;
                     }
                 };
-                if (cnt <= kBpNbCap) {
+                if (cnt <= pr.nbcap) {
                     nb_load<N>(nbw, q, cnt, w);
                     nb_walk(w, cnt, [](unsigned e) { return e; },
                             [&](int, unsigned e, unsigned) { near(static_cast<int>(e & kNbPos)); });
@@ -1839,13 +1944,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         bar();
         BP_STAMP(25);
         const bool all_kept = m == n;
-#if MC_DBG_CHECK
-        __shared__ int s_dbg_m;
-        if (t == 0) s_dbg_m = m;
-        for (int r = t; r < m; r += T) savg[r] = -7.0;
-        bar();
-        if (s_dbg_m != m) printf("DBG m mismatch N=%d s=%d t=%d m=%d m0=%d\n", N, s, t, m, s_dbg_m);
-#endif
         // 10. k nearest kept points: the eps list when it holds >= k kept points; else (deferred to a
         //     compacted pass, so that few waves walk cells) grid rings up to R = 2; else (sparse
         //     point, or m < k) all of S, by a whole wave or one lane per point
@@ -1875,7 +1973,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
                 continue;
             }
-            if (cnt > kBpNbCap) {
+            if (cnt > pr.nbcap) {
                 sring[atomicAdd(&s_ndef, 1)] = q;
                 continue;
             }
@@ -2028,11 +2126,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         bar();
         BP_STAMP(26);
-#if MC_DBG_CHECK
-        for (int r = t; r < m; r += T)
-            if (!(savg[r] > 0.0) || savg[r] > 1.0) printf("DBG savg N=%d s=%d n=%d m=%d r=%d v=%g nfb=%d\n", N, s, n, m, r, savg[r], nfb);
-        bar();
-#endif
+        if constexpr (MC_DBG_CHECK) bp_dbg_knn<N>(g, spar, savg, n, kk, s);
         // 11. cloud mean and Bessel std, sequential in index order (std::accumulate), by wave 0:
         //     64 values per step are read at once, then added in order (lane reads are scalar).
         //     (Measured and not kept: one lane loading eight values ahead of its eight dependent adds,
@@ -2092,10 +2186,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         }
         bar();
         BP_STAMP(28);
-#if MC_DBG_CHECK
-        if (ns > m || ns < 0) printf("DBG ns N=%d s=%d t=%d n=%d m=%d ns=%d thr=%g\n", N, s, t, n, m, ns, thr);
-        if (t == 0 && N == 2048) printf("DBG slot N=%d s=%d n=%d m=%d ns=%d thr=%.17g nfb=%d\n", N, s, n, m, ns, thr, nfb);
-#endif
 #ifdef MC_BP_STAMPS
         if (t == 0 && s < (1 << 16)) g_bp_slot_time[s] = static_cast<unsigned>(__builtin_amdgcn_s_memrealtime() - slot_t0);
 #endif

@@ -15,7 +15,10 @@ import sys
 
 # timed group of mc_api.hip (TimedScope names) -> (kernel-name prefixes, anchor prefixes): a group
 # launch is one launch of an anchor kernel (TimedScope count), and its bytes are the total bytes of
-# all the group's kernels over the anchor launches
+# all the group's kernels over the anchor launches.  An anchor must launch exactly once per timed
+# scope: k_bp_vox_order launches twice per batch (once in bp_voxel's scope, once in bp_denoise's,
+# mc_api.hip), so bp_voxel anchors on its first LDS tier and SHARED splits vox_order between the two.
+SHARED = {"mc::k_bp_vox_order": {"bp_voxel": 0.5, "bp_denoise": 0.5}}
 GROUPS = {
     "s3_masks": (["mc::k_s3_masks"], ["mc::k_s3_masks<1>"]),
     "s2_point_lists": (["mc::k_s2_degree", "mc::k_s2_scatter", "mc::k_s2_points", "mc::k_scan_reduce",
@@ -29,8 +32,8 @@ GROUPS = {
     "s6_merge": (["mc::k6_merge"], ["mc::k6_merge"]),
     "s7_points": (["mc::k7"], ["mc::k7_words", "mc::k7_count"]),
     "bp_pixels": (["mc::k_bp_count", "mc::k_bp_frames", "mc::k_bp_slots", "mc::k_bp_compact"], ["mc::k_bp_count"]),
-    "bp_voxel": (["mc::k_bp_vox", "mc::k_bp_voxel"], ["mc::k_bp_vox_order"]),
-    "bp_denoise": (["mc::k_bp_denoise", "mc::k_bp_classify"], ["mc::k_bp_classify"]),
+    "bp_voxel": (["mc::k_bp_voxel", "mc::k_bp_vox_order"], ["mc::k_bp_voxel_lds<6144"]),
+    "bp_denoise": (["mc::k_bp_denoise", "mc::k_bp_classify", "mc::k_bp_vox_order"], ["mc::k_bp_classify"]),
     "bp_query": (["mc::k_bp_query", "mc::k_bp_keepflags", "mc::k_bp_emit"], ["mc::k_bp_query", "mc::k_bp_emit"]),
 }
 
@@ -60,8 +63,11 @@ def main():
         if not ks or not n:
             continue
         kk = res["kernels"]
-        b = sum((2 * kk[k]["fetch_kb_avg"] + kk[k]["write_kb_avg"]) * 1024 * kk[k]["launches"] for k in ks) / n
-        res["groups"][g] = {"bytes_per_launch": b, "kernels": ks, "group_launches": n}
+        share = {k: next((w[g] for p, w in SHARED.items() if k.startswith(p) and g in w), 1.0) for k in ks}
+        per_k = {k: share[k] * (2 * kk[k]["fetch_kb_avg"] + kk[k]["write_kb_avg"]) * 1024 * kk[k]["launches"] / n
+                 for k in ks}
+        res["groups"][g] = {"bytes_per_launch": sum(per_k.values()), "kernels": ks, "group_launches": n,
+                            "bytes_per_launch_by_kernel": per_k}
     json.dump(res, open(out, "w"), indent=1)
     for g, v in res["groups"].items():
         print(f"{g:20s} {v['bytes_per_launch'] / 1e6:10.2f} MB/launch")

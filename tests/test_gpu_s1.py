@@ -218,3 +218,63 @@ def test_misaligned_device_frames_match_aligned(ctx):
     torch.cuda.synchronize()
     for x, y in zip(want, ctx.bp_masks()):
         np.testing.assert_array_equal(x, y)
+
+
+def _dense_inputs():
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    z = dict(np.load(os.path.join(GOLDEN, "s1_dense.npz")))
+    fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
+    return [(z["in_scene"], z["in_depth"], z["in_seg"], z["in_intrinsics"], z["in_poses"]),
+            (fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)]
+
+
+@pytest.mark.parametrize("nbcap", [1, 8, 24, 63])
+def test_list_overflow_paths_agree(ctx, monkeypatch, nbcap):
+    """The eps-neighbour lists are read only for counts <= nbcap; every longer list takes the cell-walk
+    paths of the union, the border labels and the k-NN ring search.  Forcing the cap down sends most
+    points (nbcap 1, 8) or the dense ones (24, 63) down those paths, in every size class: the masks must
+    not change.  (A list whose count passed the cap holds an atomic-order-dependent subset, so a
+    consumer reading one would show here as a run-dependent difference.)"""
+    for inp in _dense_inputs():
+        want = _run(ctx, *inp)
+        sa = ctx.bp_candidates()
+        for min_cls in ("0", "2", "5"):
+            monkeypatch.setenv("MC_BP_NBCAP", str(nbcap))
+            monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
+            got = _run(ctx, *inp)
+            np.testing.assert_array_equal(sa, ctx.bp_candidates(), err_msg=f"nbcap {nbcap} class {min_cls}")
+            for x, y in zip(want, got):
+                np.testing.assert_array_equal(x, y)
+            monkeypatch.delenv("MC_BP_NBCAP")
+            monkeypatch.delenv("MC_BP_MIN_CLASS")
+
+
+def test_repeated_runs_identical(ctx):
+    """Run-to-run determinism of the concurrent size classes (their lists are built with LDS-atomic
+    slots, so any read of a slot before its store lands would vary between runs): the dense inputs
+    six times each, every run bit-identical to the first."""
+    for inp in _dense_inputs():
+        want = _run(ctx, *inp)
+        sa = ctx.bp_candidates()
+        for _ in range(5):
+            got = _run(ctx, *inp)
+            np.testing.assert_array_equal(sa, ctx.bp_candidates())
+            for x, y in zip(want, got):
+                np.testing.assert_array_equal(x, y)
+
+
+def test_in_kernel_invariants(ctx, monkeypatch):
+    """Only with a -DMC_DBG_CHECK=1 library (MCGRAPH_LIB=maskclustering_amd/libmcgraph_dbg.so,
+    scripts/build_variant.sh dbg): every list, union and k-NN mean of every slot in every size class
+    equals its direct recomputation, also with the lists capped."""
+    on, _ = ctx.debug_counters(reset=True)
+    if not on:
+        pytest.skip("library built without in-kernel checks")
+    for inp in _dense_inputs():
+        for min_cls in ("0", "1", "2", "3", "4", "5"):
+            for nbcap in ("64", "8"):
+                monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
+                monkeypatch.setenv("MC_BP_NBCAP", nbcap)
+                _run(ctx, *inp)
+                _, bad = ctx.debug_counters(reset=True)
+                assert not bad.any(), f"class >= {min_cls}, nbcap {nbcap}: failures per kind {bad.tolist()}"
