@@ -337,6 +337,23 @@ int mc_openvoc_query(mc_ctx *ctx, int32_t num_objects, const int64_t *obj_off, c
  * graph/construction.py:40,52), split over host threads.                                      */
 int mc_bits_unpack(const uint64_t *words, int64_t rows, int32_t words_per_row, int32_t ncols, uint8_t *out);
 
+/* host utility: the reference's container ORDERS of the clustering result (graph/iterative_clustering.py:5-10
+ * + graph/node.py:24-37 under networkx 3.x's _plain_bfs and CPython's set tables; mc_setorder.inl).
+ * Iterations t = 0 .. num_levels-1 with level_sizes[t] nodes; iteration t's edges (a, b), a != b, are
+ * edge_a/edge_b[edge_off[t] .. edge_off[t+1]) (level_sizes[t+1] must be the number of components of t).
+ * Level-0 node i's point set was made by adding pts[pt_off[i] .. pt_off[i+1]) in order to an empty set.
+ * Out (caller-allocated, K = *num_objects = components of the last iteration <= level_sizes[T-1]):
+ *   obj_mask_off [K+1] + mask_order [level_sizes[0]]: final node k's mask_list as level-0 node indices;
+ *   obj_pt_off [K+1] + obj_pts [<= pt_off[level_sizes[0]]]: list(final node k's point_ids);
+ *   son_off [K+1] + son_order [level_sizes[T-1]]: the last iteration's members of k in set order;
+ *   labels [sum_t level_sizes[t]] (NULL: not returned): component of every node of every iteration.
+ * num_threads <= 0: all host threads.                                                                 */
+int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
+                       const int32_t *edge_a, const int32_t *edge_b, const int64_t *pt_off, const int32_t *pts,
+                       int32_t num_threads, int32_t *num_objects, int64_t *obj_mask_off, int32_t *mask_order,
+                       int64_t *obj_pt_off, int32_t *obj_pts, int64_t *son_off, int32_t *son_order,
+                       int32_t *labels);
+
 #ifdef __cplusplus
 }
 #endif

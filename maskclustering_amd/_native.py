@@ -37,7 +37,7 @@ EXPORTED = [
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
-    "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query", "mc_bits_unpack",
+    "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query", "mc_bits_unpack", "mc_setorder_replay",
     "mc_comm_unique_id", "mc_ctx_comm_init", "mc_ctx_attach_comm",
 ]
 MC_COMM_ID_BYTES = 128
@@ -174,6 +174,7 @@ def load():
         "mc_cluster_set_edge_capture": (ctypes.c_int, [vp, i64]),
         "mc_openvoc_query": (ctypes.c_int, [vp, i32, vp, vp, i32, i32, vp, i32, vp, ctypes.c_float, vp]),
         "mc_bits_unpack": (ctypes.c_int, [vp, ctypes.c_int64, i32, i32, vp]),
+        "mc_setorder_replay": (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, i32, P(i32), vp, vp, vp, vp, vp, vp, vp]),
         "mc_cluster_get_edges": (ctypes.c_int, [vp, vp, P(i64)]),
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
@@ -201,6 +202,36 @@ def comm_unique_id() -> bytes:
 
 def _ptr(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def setorder_replay(level_sizes, edge_off, edge_a, edge_b, pt_off, pts, threads=0, labels=False):
+    """mc_setorder_replay (host only, no device): the reference's container orders of a clustering run
+    (include/mcgraph.h).  Returns dict(mask_off, mask_order, pt_off, pts, son_off, son_order[, labels])."""
+    L = load()
+    T = len(level_sizes)
+    sz = np.ascontiguousarray(level_sizes, np.int32)
+    eo = np.ascontiguousarray(edge_off, np.int64)
+    ea = np.ascontiguousarray(edge_a, np.int32)
+    eb = np.ascontiguousarray(edge_b, np.int32)
+    po = np.ascontiguousarray(pt_off, np.int64)
+    pp = np.ascontiguousarray(pts, np.int32)
+    N0, NL = int(sz[0]), int(sz[T - 1])
+    K = ctypes.c_int32()
+    mo, mord = np.zeros(NL + 1, np.int64), np.zeros(max(N0, 1), np.int32)
+    oo, opts = np.zeros(NL + 1, np.int64), np.zeros(max(int(po[N0]), 1), np.int32)
+    so, sord = np.zeros(NL + 1, np.int64), np.zeros(max(NL, 1), np.int32)
+    lab = np.zeros(max(int(sz.sum()), 1), np.int32) if labels else None
+    rc = L.mc_setorder_replay(T, _ptr(sz), _ptr(eo), _ptr(ea), _ptr(eb), _ptr(po), _ptr(pp), int(threads),
+                              ctypes.byref(K), _ptr(mo), _ptr(mord), _ptr(oo), _ptr(opts), _ptr(so), _ptr(sord),
+                              _ptr(lab))
+    if rc != MC_OK:
+        raise McError(rc, "mc_setorder_replay: inconsistent levels / edges / point sets")
+    k = K.value
+    out = dict(mask_off=mo[:k + 1], mask_order=mord[:N0], pt_off=oo[:k + 1], pts=opts[:int(oo[k])],
+               son_off=so[:k + 1], son_order=sord[:NL])
+    if labels:
+        out["labels"] = lab[:int(sz.sum())]
+    return out
 
 
 class Context:

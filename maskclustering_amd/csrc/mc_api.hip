@@ -19,6 +19,7 @@
 #include "mc_io_kernels.inl"
 #include "mc_shard_kernels.inl"
 #include "mc_ov_kernels.inl"
+#include "mc_setorder.inl"
 
 using mc::DevBuf;
 using mc::McError;

@@ -1,0 +1,301 @@
+// mc_setorder.inl — reference-exact orders of the clustered containers, restated natively (host
+// code; included by mc_api.hip).
+//
+// The reference's final objects are Python containers whose ITERATION ORDER its exports follow:
+//   * networkx connected_components (graph/iterative_clustering.py:7) yields every component as the
+//     `seen` set of _plain_bfs (networkx 3.x: BFS from the smallest unseen node, `seen.add` in
+//     discovery order, neighbours ascending because from_numpy_array inserts the row-major edges of
+//     A, :30-32);
+//   * Node.create_node_from_list (graph/node.py:24-37) walks that set: mask_list += member.mask_list,
+//     point_ids = point_ids.union(member.point_ids), son_node_info.add(member.node_info);
+//   * the level-0 point sets are set(ndarray of ascending scene ids) (utils/mask_backprojection.py:
+//     139-148), aliased by init_nodes (graph/construction.py:66-78);
+//   * post_process reads list(point_ids) (graph/node.py:45, utils/post_process.py:185) and mask_list.
+// CPython's set (Objects/setobject.c) fixes those orders as a function of the keys' hashes (an int,
+// np.int64 included, hashes to itself) and the insertion history.  PySet below replays exactly that
+// history on int keys: open addressing from hash & mask, up to 9 linear probes (only when they do not
+// wrap), then perturbed probing i = 5i + 1 + (perturb >>= 5); a table resized when fill * 5 >= mask * 3
+// after an insert (to the smallest power of two > 4 * used, > 2 * used above 50000 entries; the old
+// entries re-inserted in slot order); union = copy (a new set merged from the left operand) + merge of
+// the right operand with one up-front resize when (fill + other.used) * 5 >= mask * 3 (to > 2 * (used +
+// other.used)); a merge into an empty set copies the table verbatim when the masks agree, else
+// re-inserts in slot order.  The reference never removes from these sets, so no table ever holds a
+// dummy.  Pinned against the running interpreter (tests/test_setorder_cpu.py: random histories and the
+// reference's own exports, tests/golden/e2e_pp_small_*).
+#include <atomic>
+#include <thread>
+#include <vector>
+
+namespace mcso {
+
+constexpr size_t kLinearProbes = 9;
+constexpr int kPerturbShift = 5;
+constexpr size_t kMinSize = 8;
+
+struct PySet {
+    std::vector<int32_t> t;  // key, or -1 = empty slot
+    size_t mask = kMinSize - 1;
+    size_t used = 0;         // == fill (no dummies)
+    PySet() : t(kMinSize, -1) {}
+};
+
+// set_insert_clean: the first empty slot of key's probe sequence (no key comparisons)
+inline void insert_clean(int32_t *tab, size_t mask, int32_t key)
+{
+    size_t perturb = static_cast<size_t>(key);
+    size_t i = static_cast<size_t>(key) & mask;
+    while (true) {
+        if (tab[i] < 0) {
+            tab[i] = key;
+            return;
+        }
+        if (i + kLinearProbes <= mask) {
+            for (size_t j = 1; j <= kLinearProbes; j++)
+                if (tab[i + j] < 0) {
+                    tab[i + j] = key;
+                    return;
+                }
+        }
+        perturb >>= kPerturbShift;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// set_table_resize(so, minused)
+inline void resize(PySet &s, size_t minused)
+{
+    size_t ns = kMinSize;
+    while (ns <= minused) ns <<= 1;
+    if (ns == kMinSize && s.mask == kMinSize - 1) return;  // the small table, no dummies: nothing to do
+    std::vector<int32_t> nt(ns, -1);
+    for (int32_t k : s.t)
+        if (k >= 0) insert_clean(nt.data(), ns - 1, k);
+    s.t.swap(nt);
+    s.mask = ns - 1;
+}
+
+// set_add_entry (keys are distinct ints: an equal hash is an equal key)
+inline void add(PySet &s, int32_t key)
+{
+    int32_t *tab = s.t.data();
+    const size_t mask = s.mask;
+    size_t i = static_cast<size_t>(key) & mask;
+    size_t at;
+    if (tab[i] < 0) {
+        at = i;
+    } else {
+        size_t perturb = static_cast<size_t>(key);
+        while (true) {
+            if (tab[i] == key) return;
+            if (i + kLinearProbes <= mask) {
+                for (size_t j = 1; j <= kLinearProbes; j++) {
+                    if (tab[i + j] < 0) {
+                        at = i + j;
+                        goto found;
+                    }
+                    if (tab[i + j] == key) return;
+                }
+            }
+            perturb >>= kPerturbShift;
+            i = (i * 5 + 1 + perturb) & mask;
+            if (tab[i] < 0) {
+                at = i;
+                goto found;
+            }
+        }
+    }
+found:
+    tab[at] = key;
+    s.used++;
+    if (s.used * 5 < mask * 3) return;
+    resize(s, s.used > 50000 ? s.used * 2 : s.used * 4);
+}
+
+// set_merge(so, other)
+inline void merge(PySet &s, const PySet &o)
+{
+    if (o.used == 0) return;
+    if ((s.used + o.used) * 5 >= s.mask * 3) resize(s, (s.used + o.used) * 2);
+    if (s.used == 0) {
+        if (s.mask == o.mask) {
+            s.t = o.t;  // verbatim copy
+        } else {
+            for (int32_t k : o.t)
+                if (k >= 0) insert_clean(s.t.data(), s.mask, k);
+        }
+        s.used = o.used;
+        return;
+    }
+    for (int32_t k : o.t)
+        if (k >= 0) add(s, k);
+}
+
+// a.union(b) when the caller no longer needs a: the copy step (make_new_set + set_merge into the
+// empty set) keeps a's table when its mask is what the copy would size, else re-inserts in slot order
+inline PySet union_consume(PySet &&a, const PySet &b)
+{
+    PySet r;
+    if (a.used) {
+        size_t ns = kMinSize;
+        if (a.used * 5 >= (kMinSize - 1) * 3)
+            while (ns <= a.used * 2) ns <<= 1;
+        if (ns - 1 == a.mask) {
+            r = std::move(a);
+        } else {
+            r.t.assign(ns, -1);
+            r.mask = ns - 1;
+            for (int32_t k : a.t)
+                if (k >= 0) insert_clean(r.t.data(), r.mask, k);
+            r.used = a.used;
+        }
+    }
+    merge(r, b);
+    return r;
+}
+
+// set(iterable): empty set, add in order
+inline PySet from_sequence(const int32_t *v, int64_t n)
+{
+    PySet s;
+    for (int64_t i = 0; i < n; i++) add(s, v[i]);
+    return s;
+}
+
+}  // namespace mcso
+
+extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
+                                  const int32_t *edge_a, const int32_t *edge_b, const int64_t *pt_off,
+                                  const int32_t *pts, int32_t num_threads, int32_t *num_objects,
+                                  int64_t *obj_mask_off, int32_t *mask_order, int64_t *obj_pt_off, int32_t *obj_pts,
+                                  int64_t *son_off, int32_t *son_order, int32_t *labels)
+{
+    using mcso::PySet;
+    try {
+        if (num_levels < 1 || !level_sizes || !edge_off || !pt_off || !num_objects || !obj_mask_off || !mask_order ||
+            !obj_pt_off || !obj_pts || !son_off || !son_order)
+            return MC_ERR_INVALID;
+        const int T = num_levels;
+        for (int t = 0; t < T; t++)
+            if (level_sizes[t] < 0 || edge_off[t + 1] < edge_off[t]) return MC_ERR_INVALID;
+        if (edge_off[0] != 0 || (edge_off[T] && (!edge_a || !edge_b))) return MC_ERR_INVALID;
+        const int N0 = level_sizes[0];
+        if (pt_off[0] != 0) return MC_ERR_INVALID;
+        for (int i = 0; i < N0; i++)
+            if (pt_off[i + 1] < pt_off[i]) return MC_ERR_INVALID;
+        if (pt_off[N0] && !pts) return MC_ERR_INVALID;
+        for (int64_t k = 0; k < pt_off[N0]; k++)
+            if (pts[k] < 0) return MC_ERR_INVALID;
+        int nth = num_threads > 0 ? num_threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        nth = std::max(1, std::min(nth, 64));
+
+        // per node of the current level: its mask order (level-0 indices) and point set; level 0's
+        // sets are made by the worker that consumes them (each is read by exactly one component)
+        std::vector<std::vector<int32_t>> morder(N0);
+        for (int i = 0; i < N0; i++) morder[i].assign(1, i);
+        std::vector<PySet> sets;
+        std::vector<int32_t> comp_off, comp_mem;  // the last level's components (member order)
+        int64_t lab_base = 0;
+        for (int t = 0; t < T; t++) {
+            const int N = level_sizes[t];
+            if (static_cast<int>(morder.size()) != N) return MC_ERR_INVALID;  // != components of t - 1
+            // adjacency, ascending neighbours (from_numpy_array's row-major edge insertion)
+            const int64_t e0 = edge_off[t], e1 = edge_off[t + 1];
+            std::vector<int64_t> aoff(static_cast<size_t>(N) + 1, 0);
+            for (int64_t e = e0; e < e1; e++) {
+                const int a = edge_a[e], b = edge_b[e];
+                if (a < 0 || b < 0 || a >= N || b >= N || a == b) return MC_ERR_INVALID;
+                aoff[a + 1]++;
+                aoff[b + 1]++;
+            }
+            for (int v = 0; v < N; v++) aoff[v + 1] += aoff[v];
+            std::vector<int32_t> adj(static_cast<size_t>(aoff[N]));
+            {
+                std::vector<int64_t> cur(aoff.begin(), aoff.end() - 1);
+                for (int64_t e = e0; e < e1; e++) {
+                    adj[cur[edge_a[e]]++] = edge_b[e];
+                    adj[cur[edge_b[e]]++] = edge_a[e];
+                }
+            }
+            for (int v = 0; v < N; v++) std::sort(adj.begin() + aoff[v], adj.begin() + aoff[v + 1]);
+            // components: _plain_bfs from every unseen node in order; `seen` is a set of node ints
+            std::vector<int32_t> lab(static_cast<size_t>(N), -1);
+            comp_off.assign(1, 0);
+            comp_mem.clear();
+            std::vector<int32_t> level, next;
+            for (int v = 0; v < N; v++) {
+                if (lab[v] >= 0) continue;
+                const int k = static_cast<int>(comp_off.size()) - 1;
+                PySet seen;
+                mcso::add(seen, v);
+                lab[v] = k;
+                next.assign(1, v);
+                while (!next.empty()) {
+                    level.swap(next);
+                    next.clear();
+                    for (int32_t u : level)
+                        for (int64_t j = aoff[u]; j < aoff[u + 1]; j++) {
+                            const int32_t w = adj[j];
+                            if (lab[w] < 0) {
+                                lab[w] = k;
+                                mcso::add(seen, w);
+                                next.push_back(w);
+                            } else if (lab[w] != k) {
+                                return MC_ERR_INVALID;  // unreachable: BFS stays in its component
+                            }
+                        }
+                }
+                for (int32_t x : seen.t)
+                    if (x >= 0) comp_mem.push_back(x);  // iteration order of the component set
+                comp_off.push_back(static_cast<int32_t>(comp_mem.size()));
+            }
+            if (labels) std::copy(lab.begin(), lab.end(), labels + lab_base);
+            lab_base += N;
+            const int K = static_cast<int>(comp_off.size()) - 1;
+            // create_node_from_list per component, in parallel over components
+            std::vector<std::vector<int32_t>> nmorder(K);
+            std::vector<PySet> nsets(K);
+            std::atomic<int> next_k{0};
+            auto work = [&]() {
+                for (int k = next_k++; k < K; k = next_k++) {
+                    std::vector<int32_t> &mo = nmorder[k];
+                    PySet acc;  // point_ids = set()
+                    for (int32_t j = comp_off[k]; j < comp_off[k + 1]; j++) {
+                        const int32_t m = comp_mem[j];
+                        mo.insert(mo.end(), morder[m].begin(), morder[m].end());
+                        if (t == 0) {
+                            const PySet s0 = mcso::from_sequence(pts + pt_off[m], pt_off[m + 1] - pt_off[m]);
+                            acc = mcso::union_consume(std::move(acc), s0);
+                        } else {
+                            acc = mcso::union_consume(std::move(acc), sets[m]);
+                        }
+                    }
+                    nsets[k] = std::move(acc);
+                }
+            };
+            const int nw = std::min(nth, std::max(1, K / 4));
+            std::vector<std::thread> th;
+            for (int w = 1; w < nw; w++) th.emplace_back(work);
+            work();
+            for (auto &x : th) x.join();
+            morder.swap(nmorder);
+            sets.swap(nsets);
+        }
+        const int K = static_cast<int>(morder.size());
+        *num_objects = K;
+        obj_mask_off[0] = obj_pt_off[0] = son_off[0] = 0;
+        int64_t mo = 0, po = 0;
+        for (int k = 0; k < K; k++) {
+            std::copy(morder[k].begin(), morder[k].end(), mask_order + mo);
+            mo += static_cast<int64_t>(morder[k].size());
+            obj_mask_off[k + 1] = mo;
+            for (int32_t x : sets[k].t)
+                if (x >= 0) obj_pts[po++] = x;
+            obj_pt_off[k + 1] = po;
+            son_off[k + 1] = comp_off[k + 1];
+        }
+        std::copy(comp_mem.begin(), comp_mem.end(), son_order);
+        return MC_OK;
+    } catch (const std::bad_alloc &) {
+        return MC_ERR_HIP;
+    }
+}
