@@ -241,6 +241,19 @@ void orcs_observer_hist(int M, int FW, const uint64_t *vf, uint64_t *hist, int F
  * labels_out[t * N0 + i]: component of level-t node i; level_sizes[t]; final_label[i];
  * edges_out[t] = number of undirected edges.  Returns the number of final nodes; the final
  * VF rows and C rows are left in vf_out [K][FW] and (c_off_out, c_idx_out). */
+/* optional edge sink of orcs_cluster (test infrastructure: tests/test_setorder_cpu.py feeds the per-iteration
+ * edges to the set-order restatement): keys (t << 48) | (a << 24) | b, a < b, up to cap; the count is
+ * the total even past cap */
+static uint64_t *g_edge_sink;
+static int64_t g_edge_cap, g_edge_n;
+void orcs_set_edge_sink(uint64_t *buf, int64_t cap)
+{
+    g_edge_sink = buf;
+    g_edge_cap = cap;
+    g_edge_n = 0;
+}
+int64_t orcs_edge_sink_count(void) { return g_edge_n; }
+
 int orcs_cluster(int N0, int FW, int Mn, const uint64_t *vf0, const int64_t *c_off0, const int32_t *c_idx0,
                  int n_thr, const float *thr, double ct, int32_t *labels_out, int32_t *level_sizes,
                  int32_t *final_label, int64_t *edges_out, uint64_t *vf_out, int64_t *c_off_out, int32_t *c_idx_out)
@@ -328,6 +341,12 @@ int orcs_cluster(int N0, int FW, int Mn, const uint64_t *vf0, const int64_t *c_o
         int64_t E = 0;
         for (int k = 0; k < nthreads; k++) E += tedge_n[k];
         edges_out[t] = E;
+        if (g_edge_sink)
+            for (int k = 0; k < nthreads; k++)
+                for (int64_t x = 0; x < tedge_n[k]; x++, g_edge_n++)
+                    if (g_edge_n < g_edge_cap)
+                        g_edge_sink[g_edge_n] = ((uint64_t)t << 48) | ((uint64_t)(tedges[k][x] >> 32) << 24) |
+                                                (uint64_t)(tedges[k][x] & 0xffffffff);
         int64_t *aoff = (int64_t *)calloc((size_t)N + 1, sizeof(int64_t));
         for (int k = 0; k < nthreads; k++)
             for (int64_t x = 0; x < tedge_n[k]; x++) {

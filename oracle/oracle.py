@@ -213,6 +213,10 @@ def lib():
         L.orcs_cluster.restype = ctypes.c_int
         L.orcs_cluster.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _i64p, _i32p, ctypes.c_int, _f32p,
                                    ctypes.c_double, _i32p, _i32p, _i32p, _i64p, _u64p, _i64p, _i32p]
+        L.orcs_set_edge_sink.restype = None
+        L.orcs_set_edge_sink.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        L.orcs_edge_sink_count.restype = ctypes.c_int64
+        L.orcs_edge_sink_count.argtypes = []
         _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
         L.orc_s1_batch.restype = ctypes.c_void_p
         L.orc_s1_batch.argtypes = [ctypes.c_int64, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -374,10 +378,27 @@ def _bits_rows(cols_per_row, n_rows, F):
 
 def run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
                mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
-               contained_threshold, timings: dict | None = None):
+               contained_threshold, timings: dict | None = None, edge_cap: int = 0):
     """Whole S2-S6 path on the CPU with sparse rows (oracle/graph_sparse.c): the golden-fixture
-    dictionary of run() without the dense point-in-mask entries (pim_*), for C3/C4-sized scenes."""
+    dictionary of run() without the dense point-in-mask entries (pim_*), for C3/C4-sized scenes.
+    edge_cap > 0 also returns every S6 iteration's edges as out["edges"] = (t, a, b) sorted."""
     L = lib()
+    if edge_cap > 0:
+        sink = np.zeros(int(edge_cap), np.uint64)
+        L.orcs_set_edge_sink(sink.ctypes.data, int(edge_cap))
+        try:
+            out = run_sparse(num_points, num_frames, mask_col, mask_label, mask_off, mask_pts,
+                             mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
+                             contained_threshold, timings)
+            n = L.orcs_edge_sink_count()
+        finally:
+            L.orcs_set_edge_sink(None, 0)
+        if n > edge_cap:
+            raise ValueError(f"{n} edges exceed edge_cap {edge_cap}")
+        k = np.sort(sink[:n])
+        out["edges"] = ((k >> np.uint64(48)).astype(np.int64), ((k >> np.uint64(24)) & np.uint64(0xFFFFFF)).astype(np.int64),
+                        (k & np.uint64(0xFFFFFF)).astype(np.int64))
+        return out
     P, F = int(num_points), int(num_frames)
     col = np.ascontiguousarray(mask_col, np.int32)
     label = np.ascontiguousarray(mask_label, np.int32)

@@ -134,3 +134,41 @@ def test_inconsistent_levels_raise():
         _native.setorder_replay([3, 3], [0, 1, 1], [0], [1], [0, 1, 2, 3], [0, 1, 2])  # 2 components, not 3
     with pytest.raises(_native.McError):
         _native.setorder_replay([3], [0, 1], [0], [0], [0, 1, 2, 3], [0, 1, 2])        # self edge
+
+
+@pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
+def test_reference_run_orders(cfg):
+    """The whole order chain on the CPU against the reference's own main path: the reference's mask
+    sets (api_small golden, S1 of the reference's glue) -> the S2-S6 oracle, whose per-iteration edges
+    feed mc_setorder_replay -> every final node's list(point_ids) and mask_list equal what the reference's
+    own iterative_clustering produced (e2e_pp_small golden, tests/golden/make_e2e_pp_golden.py)."""
+    import os
+    from conftest import GOLDEN
+    from oracle import oracle
+    z = np.load(os.path.join(GOLDEN, f"api_small_{cfg}.npz"))
+    g = np.load(os.path.join(GOLDEN, f"e2e_pp_small_{cfg}.npz"))
+    c = z["cfg"]
+    ct = int(c[2]) if bool(z["cfg_ct_is_int"]) else float(c[2])
+    P, F = len(z["in_scene"]), len(z["in_frame_ids"])
+    col, lab, off, idx = z["mpc_col"], z["mpc_label"], z["mpc_off"], z["mpc_idx"]
+    out = oracle.run_sparse(P, F, col, lab, off, idx, mask_visible_threshold=float(c[0]),
+                            undersegment_filter_threshold=float(c[1]), view_consensus_threshold=ct,
+                            contained_threshold=float(c[3]), edge_cap=1 << 20)
+    assert len(out["gl_col"]) == len(col)            # every reference mask is a global mask
+    T = int(out["num_iters"])
+    tt, aa, bb = out["edges"]
+    eo = np.searchsorted(tt, np.arange(T + 1))
+    node0 = out["node0_g"]
+    po = np.zeros(len(node0) + 1, np.int64)
+    np.cumsum(np.diff(off)[node0], out=po[1:])
+    seqs = np.concatenate([idx[off[m]:off[m + 1]] for m in node0])
+    got = _native.setorder_replay(out["level_sizes"][:T], eo, aa, bb, po, seqs, labels=True)
+    np.testing.assert_array_equal(got["labels"], np.concatenate([out[f"part_{t}"] for t in range(T)]))
+    fids = z["in_frame_ids"]
+    no, ni = g["node_order_off"], g["node_order_idx"]
+    assert len(got["pt_off"]) == len(no) > 10
+    for k in range(len(no) - 1):
+        np.testing.assert_array_equal(got["pts"][got["pt_off"][k]:got["pt_off"][k + 1]], ni[no[k]:no[k + 1]],
+                                      err_msg=f"node {k}: list(point_ids)")
+        ml = [node0[i] for i in got["mask_order"][got["mask_off"][k]:got["mask_off"][k + 1]]]
+        assert ";".join(f"{fids[col[m]]}_{lab[m]}" for m in ml) == str(g["node_mask_lists"][k]), f"node {k} mask_list"
