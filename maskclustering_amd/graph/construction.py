@@ -56,12 +56,14 @@ class PointFrameMatrix(np.ndarray):
 class GraphHandle:
     """Identifies the device graph a level-0 node list came from (fast S6 path)."""
 
-    def __init__(self, token, num_nodes, num_frames, num_masks, num_points):
+    def __init__(self, token, num_nodes, num_frames, num_masks, num_points, src=None, node0=None):
         self.token = token
         self.num_nodes = num_nodes
         self.num_frames = num_frames
         self.num_masks = num_masks
         self.num_points = num_points
+        self.src = src      # Level0Source of the level-0 nodes
+        self.node0 = node0  # global mask of every level-0 node
 
 
 _current = {"token": None}
@@ -269,8 +271,8 @@ def _mask_graph_construction(args, scene_points, frame_list, dataset):
     node0 = ctx.nodes0(gi.num_nodes0)
     token = next(_tokens)
     _current["token"] = token
-    handle = GraphHandle(token, len(node0), F, M, P)
     src = Level0Source(gl, keys, vf, c_off, c_idx, M, mpc)
+    handle = GraphHandle(token, len(node0), F, M, P, src, node0)
     level0 = Node.level0
     nodes = [level0(src, i, g, handle) for i, g in enumerate(node0.tolist())]
     return nodes, _thresholds(thr, isint), mpc, pfm

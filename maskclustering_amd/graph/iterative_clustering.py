@@ -11,24 +11,23 @@ on-device merge).  Nodes that come straight from this package's
 ``mask_graph_construction`` are clustered from the device graph without a
 host round trip; any other node list is packed into CSR rows first.
 
-Two contracts for the containers whose order follows CPython set iteration in the
-reference:
+Container orders.  The reference's ``Node.mask_list`` order and ``point_ids``
+iteration order follow CPython's set tables (networkx's BFS ``seen`` set, iterative_clustering.py:7;
+the chained ``set.union``, graph/node.py:31-36), and post_process numbers its DBSCAN objects by
+``list(point_ids)`` (graph/node.py:45), so the exports depend on them.
 
-* default (canonical): ``mask_list`` of a merged node lists its members' masks in
-  ascending member order and ``point_ids`` is the union set, built from the device's
-  sorted ids on its first read.  Contents are the reference's; their iteration order is not
-  (post_process numbers its DBSCAN objects by ``list(point_ids)``, graph/node.py:45,
-  so its exports can differ at DBSCAN border ties and in object order).
-* replay (``replay=True``, or MASKCLUSTERING_REPLAY_SET_ORDER=1): the device also
-  records every edge of every iteration; the host then replays exactly what the
-  reference's Python does with them: ``nx.connected_components``' BFS from the smallest
-  unseen node over ascending neighbours (``from_numpy_array``'s row-major insertion,
-  iterative_clustering.py:7,32) into a set, and ``Node.create_node_from_list``'s
-  ``mask_list +=`` / chained ``set.union`` / ``son_node_info.add`` in that set's
-  iteration order (graph/node.py:31-36).  The containers are then the reference's
-  objects in CPython's own iteration order, so post_process exports what the reference
-  exports (tests/test_gpu_api.py, golden from the reference's own S1->S6->post_process).
-  It costs what the reference's set unions cost (a fraction of a second at C2).
+* reference order (default): the device also records every edge of every iteration; the host
+  restates what the reference's Python does with them natively (``mc_setorder_replay``: networkx
+  3.x's ``_plain_bfs`` + CPython's set tables, include/mcgraph.h), so ``mask_list`` is the
+  reference's list and ``point_ids`` a set that iterates in the reference's order
+  (node.RefOrderSet); post_process then exports exactly what the reference exports
+  (tests/test_gpu_api.py, golden from the reference's own S1 -> S6 -> post_process;
+  tests/test_setorder_cpu.py against the interpreter).  Node lists that do not come from this
+  package's ``mask_graph_construction`` (point sets of unknown history) take the same steps with
+  real Python sets (``_replay``).
+* canonical (``replay=False``, or MASKCLUSTERING_SET_ORDER=canonical): contents only -- a merged
+  node's ``mask_list`` in ascending member order and ``point_ids`` built from the device's sorted
+  ids; no edge capture, no host replay.
 """
 from __future__ import annotations
 
@@ -36,7 +35,7 @@ import os
 
 import numpy as np
 
-from .. import _device
+from .. import _device, _native
 from .._hostutil import no_gc
 from ..pipeline import bits_to_bool, bool_to_bits
 from .node import Node, level0_masks
@@ -73,7 +72,8 @@ def _pack(ctx, nodes):
     return F, M
 
 
-REPLAY_SET_ORDER = os.environ.get("MASKCLUSTERING_REPLAY_SET_ORDER", "0") == "1"
+REFERENCE_SET_ORDER = os.environ.get("MASKCLUSTERING_SET_ORDER", "reference").lower() != "canonical"
+REPLAY_SET_ORDER = REFERENCE_SET_ORDER  # (round-3 name)
 _EDGE_CAP0 = 1 << 22
 
 
@@ -138,6 +138,33 @@ def _replay(nodes, T, sizes, edges, parts):
     return out
 
 
+def _level0_sequences(h):
+    """(pt_off, pts) of the level-0 nodes of device graph h: each node's point set as the reference
+    made it, set(ascending scene ids) (utils/mask_backprojection.py:147, aliased by init_nodes); None
+    when the mapping or a materialised set changed since construction (unknown history)."""
+    src, node0 = h.src, h.node0
+    mpc = src.mpc
+    csr = getattr(mpc, "csr", None)
+    if csr is None or node0 is None:
+        return None
+    row_of, off, pts = csr
+    rows = np.fromiter((row_of[src.keys[g]] for g in node0.tolist()), np.int64, count=len(node0))
+    lens = off[rows + 1] - off[rows]
+    made = getattr(mpc, "_made", {})
+    for k, v in made.items():                     # a set read and changed in place by the caller
+        if len(v) != off[row_of[k] + 1] - off[row_of[k]]:
+            return None
+    pt_off = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(lens, out=pt_off[1:])
+    idx = np.repeat(off[rows] - pt_off[:-1], lens) + np.arange(int(pt_off[-1]), dtype=np.int64)
+    return pt_off, np.asarray(pts)[idx].astype(np.int32)
+
+
+def _edge_levels(edges, T):
+    tt, aa, bb = edges
+    return np.searchsorted(tt, np.arange(T + 1)).astype(np.int64), aa, bb
+
+
 def iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay=None):
     with no_gc():
         return _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, debug, replay)
@@ -160,6 +187,7 @@ def _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, deb
         construction._current["token"] = None  # set_nodes replaces the device graph's nodes
         F, M = _pack(ctx, nodes)
     thr = np.array([float(t) for t in observer_num_thresholds], np.float32)
+    seqs = _level0_sequences(h) if (replay and h is not None) else None
     if replay:
         cap = _EDGE_CAP0
         while True:
@@ -182,6 +210,28 @@ def _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, deb
     obj = ctx.objects(ci, F)
     last = ctx.partition(T - 1, int(sizes[T - 1]))
     vf = bits_to_bool(obj["vf_bits"], F)
+    if replay and seqs is not None:
+        # native restatement of the reference's container building (mc_setorder_replay)
+        eo, ea, eb = _edge_levels(edges, T)
+        so = _native.setorder_replay(sizes[:T], eo, ea, eb, seqs[0], seqs[1], labels=True)
+        lab = so["labels"]
+        base = 0
+        for t in range(T):
+            if not np.array_equal(lab[base:base + int(sizes[t])], ctx.partition(t, int(sizes[t]))):
+                raise RuntimeError(f"set-order replay: components of iteration {t} differ from the device's")
+            base += int(sizes[t])
+        gl, node0 = h.src.gl, h.node0
+        mo, mord, po, pts, sf, sord = (so["mask_off"], so["mask_order"], so["pt_off"], so["pts"], so["son_off"],
+                                       so["son_order"])
+        gmask = node0[mord].tolist()
+        sord = sord.tolist()
+        out = []
+        for k in range(len(mo) - 1):
+            mask_list = [gl[g] for g in gmask[mo[k]:mo[k + 1]]]
+            sons = {(T - 1, j) for j in sord[sf[k]:sf[k + 1]]}      # son_node_info.add in member order
+            out.append(Node.compact_lazy_points(mask_list, vf[k], obj["c_idx"][obj["c_off"][k]:obj["c_off"][k + 1]], M,
+                                                pts[po[k]:po[k + 1]], (T, k), sons, ordered=True))
+        return out
     if replay:
         parts = [ctx.partition(t, int(sizes[t])) for t in range(T)]
         rep = _replay(nodes, T, sizes, edges, parts)

@@ -64,12 +64,15 @@ class Node:
         return v
 
     @classmethod
-    def compact_lazy_points(cls, mask_list, vf_bool, contained_ids, num_masks, point_array, node_info, son_node_info):
-        """compact() whose ``point_ids`` set is made from ``point_array`` (the device's sorted ids)
-        on first read"""
+    def compact_lazy_points(cls, mask_list, vf_bool, contained_ids, num_masks, point_array, node_info, son_node_info,
+                            ordered=False):
+        """compact() whose ``point_ids`` set is made from ``point_array`` on first read: the device's
+        sorted ids (a plain set), or with ``ordered`` the reference's iteration order of the set
+        (mc_setorder_replay; a RefOrderSet that iterates in that order)"""
         n = cls.compact(mask_list, vf_bool, contained_ids, num_masks, None, node_info, son_node_info)
         del n.__dict__["_point_ids"]
         n.__dict__["_pts_arr"] = point_array
+        n.__dict__["_pts_ordered"] = bool(ordered)
         return n
 
     @property
@@ -80,8 +83,18 @@ class Node:
                 src, g = d["_src0"]
                 d["_point_ids"] = src.mpc.original(src.keys[g])
             elif "_pts_arr" in d:
-                d["_point_ids"] = set(d.pop("_pts_arr").tolist())
+                a = d.pop("_pts_arr").tolist()
+                d["_point_ids"] = RefOrderSet(a) if d.pop("_pts_ordered", False) else set(a)
         return d.get("_point_ids")
+
+    def point_order(self) -> np.ndarray:
+        """np.int64 ids in list(self.point_ids) order, without making the set when it is still the
+        ordered array the clustering returned"""
+        d = self.__dict__
+        if "_point_ids" not in d and d.get("_pts_ordered") and "_pts_arr" in d:
+            return np.asarray(d["_pts_arr"], np.int64)
+        p = self.point_ids
+        return np.fromiter(p, np.int64, count=len(p))
 
     @point_ids.setter
     def point_ids(self, v):
@@ -147,7 +160,7 @@ class Node:
 
     def get_point_cloud(self, scene_points):
         """graph/node.py:39-49 (an Open3D PointCloud when open3d is importable)."""
-        point_ids = list(self.point_ids)
+        point_ids = self.point_order().tolist()
         points = np.asarray(scene_points)[point_ids]
         try:
             import open3d as o3d
@@ -159,6 +172,40 @@ class Node:
             pcld = _PointCloud()
             pcld.points = points
         return pcld, point_ids
+
+
+class RefOrderSet(set):
+    """A set that iterates in a given order: the order CPython's table gives the reference's own
+    set of the same contents and history (graph/node.py:35, restated by mc_setorder_replay), so that
+    ``list(node.point_ids)`` (graph/node.py:45, utils/post_process.py:185), ``for`` loops and
+    np.fromiter see the reference's order.  Contents, ``len``, ``in`` and the set algebra are the
+    plain set's; any in-place change drops the order (iteration is then the table's own)."""
+
+    __slots__ = ("_order",)
+
+    def __init__(self, order=()):
+        order = list(order)
+        super().__init__(order)
+        self._order = order if len(order) == len(self) else None
+
+    def __iter__(self):
+        o = self._order
+        return iter(o) if o is not None else set.__iter__(self)
+
+
+def _dropping_order(name):
+    base = getattr(set, name)
+
+    def f(self, *a, **kw):
+        self._order = None
+        return base(self, *a, **kw)
+    f.__name__ = name
+    return f
+
+
+for _n in ("add", "discard", "remove", "pop", "clear", "update", "difference_update", "intersection_update",
+           "symmetric_difference_update", "__ior__", "__iand__", "__isub__", "__ixor__"):
+    setattr(RefOrderSet, _n, _dropping_order(_n))
 
 
 class Level0Source:

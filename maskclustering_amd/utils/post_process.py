@@ -114,7 +114,8 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
                 q_col.append(c)
                 q_key.append((f, m))
         vf_rows.append(vf)
-        orders.append(np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))  # list(point_ids), node.py:45
+        po = getattr(n, "point_order", None)                      # list(point_ids), node.py:45
+        orders.append(po() if po is not None else np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))
     if not nodes:
         return [], []
     scene = np.ascontiguousarray(_host(scene_points), np.float64).reshape(-1, 3)

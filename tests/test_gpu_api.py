@@ -108,7 +108,7 @@ def test_dropin_frame_backprojection_matches_reference():
 def _pp_golden(cfg):
     import json
     meta = json.load(open(os.path.join(GOLDEN, "e2e_pp_small.meta.json")))
-    # the replay restates networkx 3.x's _plain_bfs set orders (iterative_clustering._replay)
+    # the orders restate networkx 3.x's _plain_bfs set orders (mc_setorder.inl, iterative_clustering._replay)
     assert meta["generated_with"]["networkx"].split(".")[0] == "3", meta
     return np.load(os.path.join(GOLDEN, f"e2e_pp_small_{cfg}.npz"))
 
@@ -130,24 +130,29 @@ def _golden_exports(g):
     return pts, masks
 
 
+def _check_reference_orders(objects, g):
+    no, ni = g["node_order_off"], g["node_order_idx"]
+    assert len(objects) == len(no) - 1
+    for k, o in enumerate(objects):
+        assert [int(x) for x in o.point_ids] == ni[no[k]:no[k + 1]].tolist(), f"node {k} point order"
+        assert ";".join(f"{f}_{m}" for f, m in o.mask_list) == str(g["node_mask_lists"][k]), f"node {k} mask_list"
+
+
 @pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
 def test_dropin_main_path_exports_match_reference(cfg):
-    """main.py:17-21 through the drop-ins with the set-order replay (S1 -> S6 -> post_process) exports
+    """main.py:17-21 through the drop-ins in their DEFAULT mode (S1 -> S6 -> post_process) exports
     exactly what the reference's own run exports (tests/golden/make_e2e_pp_golden.py): the same
     objects in the same order, their point ids in the same order, the same mask lists and
-    coverages; every final node's list(point_ids) is the reference's iteration order."""
+    coverages; every final node's list(point_ids) is the reference's iteration order (the native
+    set-order restatement, mc_setorder_replay)."""
     import make_api_golden as ag
     from maskclustering_amd.graph import construction, iterative_clustering
     z, frames, fids, args = _load(f"api_small_{cfg}")
     g = _pp_golden(cfg)
     nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
                                                                 ag.FrameDataset(frames, fids, PinholeIntrinsic))
-    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False, replay=True)
-    no, ni = g["node_order_off"], g["node_order_idx"]
-    assert len(objects) == len(no) - 1
-    for k, o in enumerate(objects):
-        assert [int(x) for x in o.point_ids] == ni[no[k]:no[k + 1]].tolist(), f"node {k} point order"
-        assert ";".join(f"{f}_{m}" for f, m in o.mask_list) == str(g["node_mask_lists"][k]), f"node {k} mask_list"
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+    _check_reference_orders(objects, g)
     gp, gm = _exports(objects, mpc, frames, pfm, fids, float(g["pp_thr"]))
     wp, wm = _golden_exports(g)
     assert len(gp) == len(wp) > 5
@@ -157,17 +162,35 @@ def test_dropin_main_path_exports_match_reference(cfg):
 
 
 @pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
-def test_dropin_default_exports_canonical(cfg):
-    """Without the replay the drop-in's containers hold the reference's contents in another order;
-    on these scenes the exported objects still equal the reference's as sets of point sets with
-    the same mask lists (order-free comparison: the canonical contract)."""
+def test_dropin_general_nodes_reference_orders(cfg):
+    """Node objects built by the caller (point sets of unknown history) take the Python-set replay
+    of the same steps: the same reference orders."""
+    import make_api_golden as ag
+    from maskclustering_amd.graph import construction, iterative_clustering
+    from maskclustering_amd.graph.node import Node
+    z, frames, fids, args = _load(f"api_small_{cfg}")
+    g = _pp_golden(cfg)
+    nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
+                                                                ag.FrameDataset(frames, fids, PinholeIntrinsic))
+    plain = [Node(n.mask_list, n.visible_frame.clone(), n.contained_mask.clone(), n.point_ids, n.node_info, None)
+             for n in nodes]
+    objects = iterative_clustering.iterative_clustering(plain, thr, args.view_consensus_threshold, False)
+    _check_reference_orders(objects, g)
+
+
+@pytest.mark.parametrize("cfg", ["scannet", "scannetpp"])
+def test_dropin_canonical_exports(cfg):
+    """replay=False (canonical: no edge capture, no host replay): the containers hold the reference's
+    contents in another order; on these scenes the exported objects still equal the reference's as
+    sets of point sets with the same mask lists (order-free comparison)."""
     import make_api_golden as ag
     from maskclustering_amd.graph import construction, iterative_clustering
     z, frames, fids, args = _load(f"api_small_{cfg}")
     g = _pp_golden(cfg)
     nodes, thr, mpc, pfm = construction.mask_graph_construction(args, frames.scene_points, fids,
                                                                 ag.FrameDataset(frames, fids, PinholeIntrinsic))
-    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
+    objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False,
+                                                        replay=False)
     gp, gm = _exports(objects, mpc, frames, pfm, fids, float(g["pp_thr"]))
     wp, wm = _golden_exports(g)
     got = sorted((tuple(sorted(p.tolist())), tuple(sorted(m))) for p, m in zip(gp, gm))
