@@ -1153,10 +1153,9 @@ int mc_cluster_run(mc_ctx *ctx, const float *thresholds, int32_t n, double conne
 {
     return guarded(ctx, [&] {
         MC_REQUIRE(ctx->have_nodes, MC_ERR_STATE, "mc_cluster_run before mc_graph_build / mc_nodes_set");
-        // a sharded level 0 evaluates only this rank's pair rows, so a capture would miss the other
-        // ranks' edges (replay mode is single-process)
-        MC_REQUIRE(!(ctx->cap_edges > 0 && sharded(ctx)), MC_ERR_UNSUPPORTED,
-                   "edge capture (set-order replay) needs an unsharded context (mc_shard_set world 1)");
+        // (edge capture on a sharded context: iteration 0 evaluates only this rank's pair rows, so its
+        // capture holds those rows' edges and the driver gathers them, graph_shard.ShardedGraph.edges;
+        // the later iterations run replicated and every rank captures all of their edges)
         hipStream_t s = ctx->stream;
         int *stats = ctx->d_stats.as<int>();
         if (ctx->nodes_from_graph) {

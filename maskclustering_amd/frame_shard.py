@@ -99,7 +99,7 @@ def gather_frame_costs(local_costs, num_frames: int, group=None) -> np.ndarray:
         raise ValueError(f"rank {rank} holds {len(t)} frame costs, its slice is [{lo}, {hi})")
     if world == 1:
         return t.cpu().numpy()
-    dev = _comm_device(group, t.device if t.device.type == "cuda" else torch.device("cpu"))
+    dev = _comm_device(group, t.device)
     width = -(-int(num_frames) // world)  # slices differ by at most one frame
     buf = torch.zeros(width, dtype=torch.float64, device=dev)
     buf[:len(t)] = t.to(dev)
@@ -111,8 +111,11 @@ def gather_frame_costs(local_costs, num_frames: int, group=None) -> np.ndarray:
 
 
 def _comm_device(group, like: torch.device) -> torch.device:
-    """Tensors for the collective: device tensors under RCCL ("nccl"), host tensors under gloo."""
-    return like if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    """Tensors for the collective: device tensors under RCCL ("nccl": ``like`` when it is a GPU,
+    else the current GPU, so host inputs work too), host tensors under gloo."""
+    if dist.get_backend(group) != "nccl":
+        return torch.device("cpu")
+    return like if like.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
 
 
 def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
@@ -175,6 +178,22 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
     return g_col, g_lab, g_off, g_pts
 
 
+def _check_same_on_all_ranks(costs: np.ndarray, group=None):
+    """Raise on every rank if the ranks hold different cost vectors (their slices would overlap or
+    leave frames out, and gather_masks would concatenate them without an error): a min and a max
+    all-reduce of an order-sensitive checksum of the float64 bits."""
+    bits = costs.view(np.uint64)
+    w = np.arange(1, len(bits) + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    h = int(np.bitwise_xor.reduce(bits * w) if len(bits) else 0) & ((1 << 62) - 1)
+    dev = _comm_device(group, torch.device("cpu"))
+    lo = torch.tensor([h], dtype=torch.int64, device=dev)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    if int(lo.item()) != int(hi.item()):
+        raise ValueError("the ranks hold different frame cost vectors: their frame slices would disagree")
+
+
 class FrameShardedScene:
     """S1 on this rank's frames, all-gather, then the replicated graph path.
 
@@ -193,11 +212,16 @@ class FrameShardedScene:
         on = dist.is_initialized()
         self.rank = dist.get_rank(group) if on else 0
         self.world = dist.get_world_size(group) if on else 1
-        # costs (per-frame, e.g. gather_frame_costs(frame_costs(...))): cost-balanced slices
+        # costs (per-frame, e.g. gather_frame_costs(frame_costs(...))): cost-balanced slices; every
+        # rank must cut the same slices, so the cost vectors are compared across the ranks first
+        if costs is not None:
+            costs = np.asarray(costs, np.float64).reshape(-1)
+            if len(costs) != self.F:
+                raise ValueError(f"{len(costs)} frame costs for {self.F} frames")
+            if self.world > 1:
+                _check_same_on_all_ranks(costs, group)
         self.slices = (balanced_frame_slices(costs, self.world) if costs is not None
                        else [frame_slice(self.F, self.world, r) for r in range(self.world)])
-        if costs is not None and len(costs) != self.F:
-            raise ValueError(f"{len(costs)} frame costs for {self.F} frames")
         self.lo, self.hi = self.slices[self.rank]
         # the mask block bound of gather_masks for S1 output: 255 ids per frame of the largest slice
         self.max_masks = 255 * max(1, max(hi - lo for lo, hi in self.slices))

@@ -122,6 +122,34 @@ class ShardedGraph:
         if not self._same_stream():
             self.ctx.synchronize()  # the imported blocks are read before torch may reuse them
 
+    # ---- edges of the clustering run (for the reference's container orders) -----------------
+    def set_edge_capture(self, capacity):
+        self.ctx.set_edge_capture(capacity)
+
+    def edges(self):
+        """Every iteration's edges as (t, a, b) int64 arrays sorted by (t, a, b), the same on every
+        rank: iteration 0's come from the ranks' pair rows (each rank captured its own rows' edges,
+        all-gathered here), the later iterations ran replicated (this rank's capture)."""
+        import numpy as np
+        tt, aa, bb = self.ctx.edges()
+        if self.world == 1:
+            return tt, aa, bb
+        z = tt == 0
+        key = ((aa[z] << 24) | bb[z]).astype(np.int64)
+        n = torch.tensor([len(key)], dtype=torch.int64, device=self.comm_dev)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=self.group)
+        w = max(int(n.item()), 1)
+        buf = torch.full((w,), -1, dtype=torch.int64)
+        buf[:len(key)] = torch.from_numpy(key)
+        allk = torch.empty(self.world * w, dtype=torch.int64, device=self.comm_dev)
+        dist.all_gather_into_tensor(allk, buf.to(self.comm_dev), group=self.group)
+        allk = allk.cpu().numpy()
+        allk = np.unique(allk[allk >= 0])
+        self.bytes_moved += 8 * w * self.world
+        t0 = np.zeros(len(allk), np.int64)
+        return (np.concatenate([t0, tt[~z]]), np.concatenate([allk >> 24, aa[~z]]),
+                np.concatenate([allk & 0xFFFFFF, bb[~z]]))
+
     # ---- the reference-shaped steps ----------------------------------------------------------
     def build(self, mask_visible_threshold, contained_threshold, undersegment_filter_threshold):
         self.ctx.build(mask_visible_threshold, contained_threshold, undersegment_filter_threshold)

@@ -79,6 +79,7 @@ class SceneMasks:
 
 # Shapes of SURVEY.md §8(d) (C1 is the synthetic stand-in for the demo scene).
 SHAPES = {
+    "few": dict(num_points=3_000, num_frames=6, num_objects=10, win=0.45),   # fewer frames than ranks (tests)
     "tiny": dict(num_points=2_000, num_frames=24, num_objects=24, win=0.12),
     "c1": dict(num_points=20_000, num_frames=100, num_objects=240, win=0.05),
     "c2": dict(num_points=240_000, num_frames=250, num_objects=600, win=0.05),

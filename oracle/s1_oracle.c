@@ -178,7 +178,9 @@ static void dbscan(const double *p, int n, double eps, int minpts, int32_t *labe
  * keep[i] for i < m.  Returns the number kept. */
 static int statistical_outlier(const double *p, const int32_t *idx, int m, int k, double std_ratio, uint8_t *keep)
 {
-    if (m == 0) return 0;
+    /* nb_neighbors < 1 is an illegal input to Open3D's RemoveStatisticalOutliers (the C-ABI rejects
+       it with MC_ERR_UNSUPPORTED); nothing is kept here, and no d[kk - 1] read happens with kk = 0 */
+    if (m == 0 || k < 1) return 0;
     const int kk = k < m ? k : m;                     /* nanoflann returns min(k, n) */
     double *avg = (double *)malloc((size_t)m * sizeof(double));
     double *d = (double *)malloc((size_t)(kk + 1) * sizeof(double));

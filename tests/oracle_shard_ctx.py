@@ -41,6 +41,31 @@ class OracleShardCtx:
 
     def __init__(self):
         self.rank, self.world, self.pending = 0, 1, 0
+        self.cap = 0
+        self.e0 = np.zeros(0, np.int64)
+        self.later = np.zeros(0, np.uint64)
+
+    # ---- edge capture (mc_cluster_set_edge_capture / mc_cluster_get_edges) ----
+    def set_edge_capture(self, capacity):
+        self.cap = int(capacity)
+
+    def edges(self):
+        """(t, a, b) sorted: iteration 0's of this rank's pair rows, the later iterations' all"""
+        a0, b0 = self.e0 >> 32, self.e0 & 0xffffffff
+        k = self.later
+        key = np.sort(np.concatenate([(a0.astype(np.uint64) << np.uint64(24)) | b0.astype(np.uint64), k]))
+        return ((key >> np.uint64(48)).astype(np.int64), ((key >> np.uint64(24)) & np.uint64(0xFFFFFF)).astype(np.int64),
+                (key & np.uint64(0xFFFFFF)).astype(np.int64))
+
+    def level0_sequences(self):
+        """each level-0 node's point set as the reference made it (ascending ids), as (pt_off, pts)"""
+        keep_idx = np.nonzero(self.kept)[0]
+        rows = keep_idx[self.node0]
+        lens = np.diff(self.off)[rows]
+        po = np.zeros(len(rows) + 1, np.int64)
+        np.cumsum(lens, out=po[1:])
+        pts = np.concatenate([self.pts[self.off[r]:self.off[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.int32)
+        return po, pts.astype(np.int32)
 
     # ---- context plumbing the driver reads ----
     def stream(self):
@@ -160,6 +185,7 @@ class OracleShardCtx:
             for x in e[:n]:
                 self.dsu.unite(int(x >> 32), int(x & 0xffffffff))
             self.edges0 = int(n)
+            self.e0 = e[:n].copy()
             if self.world > 1:
                 self.pending = FOREST
                 return
@@ -170,7 +196,7 @@ class OracleShardCtx:
         M, FW, N0 = self.M, self.FW, len(self.node0)
         T = len(self.thr_used)
         if T == 0:
-            self.parts, self.sizes, self.final, self.edges = [], np.array([N0], np.int32), np.arange(N0), []
+            self.parts, self.sizes, self.final, self.edge_n = [], np.array([N0], np.int32), np.arange(N0), []
             self.vf_fin, self.c_off_fin, self.c_idx_fin = self.vf0[:N0], self.c_off0, self.c_idx0[:self.c_off0[-1]]
             return
         roots = np.array([self.dsu.find(i) for i in range(N0)], np.int64)
@@ -194,13 +220,23 @@ class OracleShardCtx:
         vf_out = np.zeros((max(K1, 1), FW), np.uint64)
         co_out = np.zeros(max(K1, 1) + 1, np.int64)
         ci_out = np.zeros(max(int(co1[-1]), 1), np.int32)
-        K = L.orcs_cluster(K1, FW, M, np.ascontiguousarray(vf1), co1, np.ascontiguousarray(ci1), T1,
-                           np.ascontiguousarray(self.thr_used[1:]), self.ct, labels, sizes1, final1, edges1, vf_out,
-                           co_out, ci_out)
+        sink = np.zeros(max(self.cap, 1), np.uint64)
+        if self.cap:
+            L.orcs_set_edge_sink(sink.ctypes.data, self.cap)
+        try:
+            K = L.orcs_cluster(K1, FW, M, np.ascontiguousarray(vf1), co1, np.ascontiguousarray(ci1), T1,
+                               np.ascontiguousarray(self.thr_used[1:]), self.ct, labels, sizes1, final1, edges1, vf_out,
+                               co_out, ci_out)
+            n = L.orcs_edge_sink_count() if self.cap else 0
+        finally:
+            L.orcs_set_edge_sink(None, 0)
+        assert n <= self.cap or not self.cap, "edge capture overflow"
+        k = sink[:n]   # iteration t of this call is iteration t + 1 of the run
+        self.later = ((((k >> np.uint64(48)) + np.uint64(1)) << np.uint64(48)) | (k & np.uint64((1 << 48) - 1))).astype(np.uint64)
         self.parts = [lab0] + [labels[t, :sizes1[t]].copy() for t in range(T1)]
         self.sizes = np.concatenate([[N0], sizes1]).astype(np.int32)
         self.final = final1[lab0]
-        self.edges = [self.edges0] + edges1[:T1].tolist()
+        self.edge_n = [self.edges0] + edges1[:T1].tolist()
         self.vf_fin, self.c_off_fin, self.c_idx_fin = vf_out[:K], co_out[:K + 1], ci_out[:co_out[K]]
 
     # ---- exchange blocks ----
@@ -267,5 +303,5 @@ class OracleShardCtx:
     def canonical(self):
         return orc.assemble_sparse(self.P, self.F, self.col, self.label, self.off, self.pts, self.kept, self.bnd,
                                    self.c_rows, self.c_tgts, self.useg[:self.M], self.vfw, self.hist, self.thr,
-                                   self.thr_isint, self.node0, self.parts, self.sizes, self.final, self.edges,
+                                   self.thr_isint, self.node0, self.parts, self.sizes, self.final, self.edge_n,
                                    self.vf_fin, self.c_off_fin, self.c_idx_fin)

@@ -11,6 +11,9 @@ mode "graph:<shape>:<seed>:<cfg>" (CPU, gloo): every rank holds its frame slice'
 them and runs the sharded S2-S6 through ShardedGraph on the oracle-backed stand-in context
 (tests/oracle_shard_ctx.py); saves the canonical outputs.
 mode "gpugraph:<shape>:<seed>" (GPU, gloo, ranks share cuda:0): the same with the HIP context.
+mode "orders:<shape>:<seed>:<cfg>" (CPU, gloo): the "graph" run with edge capture; iteration 0's edges
+all-gathered (graph_shard.ShardedGraph.edges), the reference's container orders (mc_setorder_replay)
+saved.
 mode "skew:<shape>:<seed>" (CPU, gloo): a skewed scene (every mask of the first quarter of the
 frames, one in eight elsewhere); each rank costs its equal-count slice's frames by their mask
 points, the costs are all-gathered and the ranks take cost-balanced slices (frame_shard.
@@ -91,6 +94,26 @@ def main():
             sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
             sh.step(**CFGS[cfg])
             np.savez(out, **{k: np.asarray(v) for k, v in run.ctx.canonical().items()})
+        elif mode.startswith("orders:"):
+            # the sharded run's edges (iteration 0 gathered over the ranks) -> the reference's orders
+            from maskclustering_amd import _native
+            from maskclustering_amd.synthetic import make_shape
+            _, shape, seed, cfg = mode.split(":")
+            s = make_shape(shape, seed=int(seed))
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+            run = OracleRun()
+            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            sh.graph.set_edge_capture(1 << 20)
+            sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
+            sh.step(**CFGS[cfg])
+            c = run.ctx
+            T = len(c.thr_used)
+            tt, aa, bb = sh.graph.edges()
+            eo = np.searchsorted(tt, np.arange(T + 1))
+            po, seqs = c.level0_sequences()
+            o = _native.setorder_replay(c.sizes[:T], eo, aa, bb, po, seqs, labels=True)
+            np.savez(out, **o)
         elif mode.startswith("skew:"):
             from maskclustering_amd.synthetic import make_shape
             _, shape, seed = mode.split(":")

@@ -1,7 +1,8 @@
 """Frame sharding on the CPU: slice arithmetic, the all-gather of per-rank mask
 CSRs, and the row-block sharded S2-S6 (maskclustering_amd.graph_shard.ShardedGraph: S3 row blocks,
-S4 histogram shares summed, S6 level-0 union-find forests united) over gloo at world sizes 1-3,
-against the single-process result.  The per-rank compute is the sparse oracle behind the same
+S4 histogram shares summed, S6 level-0 union-find forests united) over gloo at world sizes 1-8 (a
+rank with no frames included), against the single-process result, and the reference's container
+orders from the sharded run's gathered edges.  The per-rank compute is the sparse oracle behind the same
 exchange API as the HIP library (tests/oracle_shard_ctx.py); the GPU twin is
 tests/test_gpu_frame_shard.py."""
 import numpy as np
@@ -64,7 +65,8 @@ def test_frame_costs_count_mask_pixels_and_footprints():
     np.testing.assert_allclose(c, [12 * (1 + 10 * foot(2.0)), 0.0, 1 + 10 * foot(1.0)], rtol=1e-6)
 
 
-def test_skewed_scene_balanced_slices_equal_single_process(tmp_path):
+@pytest.mark.parametrize("world", [3, 4, 8])
+def test_skewed_scene_balanced_slices_equal_single_process(tmp_path, world):
     """A scene whose masks crowd into the first quarter of the frames: the cost-balanced slices
     differ from the equal-count ones, and every rank still ends with the single-process result."""
     from maskclustering_amd.synthetic import make_shape
@@ -73,7 +75,6 @@ def test_skewed_scene_balanced_slices_equal_single_process(tmp_path):
     s = skewed(make_shape("c1", seed=1))
     want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts,
                              **KW["scannet"])
-    world = 3
     lens = np.diff(s.mask_off).astype(np.float64)
     costs = np.bincount(s.mask_col, weights=lens, minlength=s.num_frames)
     for out in run_ranks("skew:c1:1", world, tmp_path):
@@ -87,7 +88,7 @@ def test_skewed_scene_balanced_slices_equal_single_process(tmp_path):
             np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_gather_equals_global_mask_list(tmp_path, world):
     from maskclustering_amd.synthetic import make_shape
     s = make_shape("tiny", seed=4)
@@ -107,7 +108,8 @@ KW = {"scannet": dict(mask_visible_threshold=0.3, undersegment_filter_threshold=
 
 @pytest.mark.parametrize("world,shape,seed,cfg", [(1, "tiny", 4, "scannet"), (2, "tiny", 4, "scannet"),
                                                   (3, "tiny", 5, "scannetpp"), (2, "c1", 1, "scannet"),
-                                                  (3, "c1", 2, "scannet")])
+                                                  (3, "c1", 2, "scannet"), (4, "c1", 3, "scannet"),
+                                                  (8, "c1", 1, "scannetpp"), (8, "few", 0, "scannet")])
 def test_sharded_graph_equals_single_process(tmp_path, world, shape, seed, cfg):
     """Every rank ends with exactly the single-process S2-S6 outputs (every stage, canonical form)."""
     from maskclustering_amd.synthetic import make_shape
@@ -120,3 +122,30 @@ def test_sharded_graph_equals_single_process(tmp_path, world, shape, seed, cfg):
         assert sorted(got.files) == sorted(want)
         for k in want:
             np.testing.assert_array_equal(got[k], np.asarray(want[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("world,shape,seed,cfg", [(2, "c1", 1, "scannet"), (4, "tiny", 5, "scannetpp"),
+                                                  (8, "few", 0, "scannet")])
+def test_sharded_reference_orders_equal_single_process(tmp_path, world, shape, seed, cfg):
+    """The reference's container orders (mc_setorder_replay) from a sharded run, whose iteration-0
+    edges are gathered from the ranks' pair rows, equal those of the single-process run's edges."""
+    from maskclustering_amd import _native
+    from maskclustering_amd.synthetic import make_shape
+    from oracle import oracle
+    s = make_shape(shape, seed=seed)
+    want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts,
+                             edge_cap=1 << 20, **KW[cfg])
+    T = int(want["num_iters"])
+    assert T > 1
+    tt, aa, bb = want["edges"]
+    node0 = want["node0_g"]            # every input mask is global in these scenes
+    assert len(want["gl_col"]) == len(s.mask_col)
+    po = np.zeros(len(node0) + 1, np.int64)
+    np.cumsum(np.diff(s.mask_off)[node0], out=po[1:])
+    seqs = np.concatenate([s.mask_points(g) for g in node0]).astype(np.int32)
+    ref = _native.setorder_replay(want["level_sizes"][:T], np.searchsorted(tt, np.arange(T + 1)), aa, bb, po, seqs,
+                                  labels=True)
+    for out in run_ranks(f"orders:{shape}:{seed}:{cfg}", world, tmp_path):
+        got = np.load(out)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
