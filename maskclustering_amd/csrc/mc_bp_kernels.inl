@@ -1491,7 +1491,8 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
 //   1  a list the consumers read (count <= nbcap) whose entries (position | radius class) differ
 //      from those points as a multiset (sum and xor of a 64-bit mix of each entry)
 //   2  two core points within eps in different union-find components
-//   3  a kept point's mean k-NN distance != the brute-force mean over every kept point (bits)
+//   3  a kept point's mean k-NN distance != the brute-force mean over every kept point (bits; checked in
+//      k_bp_denoise_tail, after the ring-search kernel)
 // Each failure is counted in g_bp_dbg[kind] (read by mc_debug_counters) and the first 16 printed.
 // ---------------------------------------------------------------------------------------------
 #ifndef MC_DBG_CHECK
@@ -1564,29 +1565,24 @@ __device__ __noinline__ void bp_dbg_union(const BpLdsGrid &g, const int *spar, i
     }
     sync_global();
 }
-// kept point at sorted position q has rank spar[q] (< m) and its mean in savg[rank]
-template <int N>
-__device__ __noinline__ void bp_dbg_knn(const BpLdsGrid &g, const int *spar, const double *savg, int n, int kk, int slot)
+// (in k_bp_denoise_tail, a wave per slot) kept point of rank r: original index sx[r], mean av[r]
+__device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, const double *av, int m, int kk, int slot)
 {
-    for (int q = threadIdx.x; q < n; q += blockDim.x) {
-        const double4 a = g.pt[q];
-        if (!(static_cast<unsigned long long>(__double_as_longlong(a.w)) & kKeptBit)) continue;
+    for (int r = lane_id(); r < m; r += 64) {
+        const double *a = P + 3 * sx[r];
         double best[kBpKnnMax];
         for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-        for (int q2 = 0; q2 < n; q2++) {
-            const double4 p = g.pt[q2];
-            if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
-            const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+        for (int j = 0; j < m; j++) {
+            const double *p = P + 3 * sx[j];
+            const double ex = a[0] - p[0], ey = a[1] - p[1], ez = a[2] - p[2];
             sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
         }
         double sum = 0.0;
         for (int k = 0; k < kk; k++) sum = sum + sqrt(best[k]);
-        const double want = sum / static_cast<double>(kk), got = savg[spar[q]];
+        const double want = sum / static_cast<double>(kk), got = av[r];
         if (__double_as_longlong(want) != __double_as_longlong(got))
-            if (bp_dbg_fail(3)) printf("[bp dbg] N=%d slot=%d n=%d q=%d: k-NN mean %.17g, brute force %.17g\n", N, slot, n, q,
-                                       got, want);
+            if (bp_dbg_fail(3)) printf("[bp dbg] slot=%d m=%d r=%d: k-NN mean %.17g, brute force %.17g\n", slot, m, r, got, want);
     }
-    sync_global();
 }
 
 // Slots of each size class (unordered: every slot is processed independently); class kBpClasses =
@@ -1640,8 +1636,9 @@ template <int N>
 __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsClass<N>::T / 256) void k_bp_denoise_lds(
     const int *__restrict__ cls_cnt, const int *__restrict__ cls_list, int *__restrict__ ticket,
     const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
-    unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, float *__restrict__ qpts, int *__restrict__ slot_m,
-    int *__restrict__ slot_ns, float *__restrict__ slot_box)
+    unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, int *__restrict__ slot_m, double *__restrict__ gavg,
+    int *__restrict__ gsx, double4 *__restrict__ grec, int *__restrict__ gbs, int *__restrict__ gitem,
+    int *__restrict__ dq, int *__restrict__ dq_cnt, double *__restrict__ slot_grid)
 {
     constexpr int T = BpLdsClass<N>::T;
     constexpr int NW = T / 64;
@@ -1664,12 +1661,12 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     __shared__ int sflag_l[NL2];         // eps-neighbour count | kept bit 30
     __shared__ int spar_l[NL2];          // union-find over positions, then roots, then kept ranks
     __shared__ int sX_l[NL];             // bucket per point; rank per root; S list
-    __shared__ double savg_l[NL];        // labels (int view); then mean distances
+    __shared__ int slab_l[NL];           // labels (the k-NN means go to the slot's range of gavg)
     int *const gs0 = lean_scr + static_cast<size_t>(blockIdx.x) * kBpLeanInts<N>;
     double4 *const spt = kLean3 ? reinterpret_cast<double4 *>(gs0) : spt_l;
     int *const sA = kLean3 ? gs0 + 8 * N : sA_l;
     int *const gs = gs0 + kBpLean3Pre<N>;
-    double *const savg = kLean ? reinterpret_cast<double *>(gs) : savg_l;
+    int *const slab = kLean ? gs : slab_l;
     int *const sB = kLean ? gs + 2 * N : sB_l;
     int *const sX = kLean ? gs + 4 * N + 2 : sX_l;
     short *const sorig = kLean ? reinterpret_cast<short *>(gs + 5 * N + 2) : sorig_l;
@@ -1677,11 +1674,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     int *const sflag = kBpLean2<N> ? gs + 6 * N + 2 : sflag_l;
     int *const spar = kBpLean2<N> ? gs + 7 * N + 2 : spar_l;
     __shared__ double red[6 * NW];
-    __shared__ float fred[6 * NW];
     __shared__ int ws[NW];
-    __shared__ double s_thr;
     __shared__ int s_slot, s_ndef;
-    int *slab = reinterpret_cast<int *>(savg);
     int *ccnt = sB + N;
     int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
     const int cnt_cls = *cls_cnt;
@@ -1937,6 +1931,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const int ex = block_excl_scan<T>(keep, ws, tot);
             if (keep) {
                 sX[m + ex] = i;
+                gsx[base + m + ex] = i;   // rank -> original index, for k_bp_denoise_tail
                 spar[spos[i]] = m + ex;
             }
             m += tot;
@@ -1944,28 +1939,28 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         bar();
         BP_STAMP(25);
         const bool all_kept = m == n;
-        // 10. k nearest kept points: the eps list when it holds >= k kept points; else (deferred to a
-        //     compacted pass, so that few waves walk cells) grid rings up to R = 2; else (sparse
-        //     point, or m < k) all of S, by a whole wave or one lane per point
+        // 10. k nearest kept points, the list pass: a point whose eps list holds >= k kept points
+        //     takes the k nearest among them (every other kept point is >= eps away).  The others (a
+        //     list longer than nbcap, or fewer than k kept entries) are deferred to the batch's
+        //     ring-search kernel (k_bp_knn_ring: after every class, a lane per point over the whole
+        //     chip, instead of the few lanes of one wave while the rest of this workgroup waits at a
+        //     barrier), with the slot's cell grid written out for it; a slot of m < k kept points
+        //     takes its whole-cloud means here.  The means go to the slot's range of gavg; the cloud
+        //     statistics and the survivors follow in k_bp_denoise_tail (a wave per slot).
         const int kk = min(pr.knn, m);
-        int *const sring = sB + N;  // deferred ring-search positions (sB is free after the filter)
+        int *const sring = sB + N;  // deferred positions (sB is free after the filter)
         if (t == 0) {
             sfb[kFbCount] = 0;
             s_ndef = 0;
         }
         bar();
-        auto put_mean = [&](int r, const double(&best)[kBpKnnMax]) {
-            double sum = 0.0;
-#pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
-            savg[r] = sum / static_cast<double>(kk);
-        };
+        double *const mavg = gavg + base;
         for (int q = t; q < n; q += T) {
             const int fl = sflag[q];
             if (!(fl & (1 << 30))) continue;
             const int r = spar[q];
 #if MC_ABLATE_BP == 1
-            savg[r] = 1.0;
+            mavg[r] = 1.0;
             continue;
 #endif
             const int cnt = nb_cnt(fl);
@@ -2007,10 +2002,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             if (found >= kk) {
                 const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
                 auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)] & kNbPos); };
-                // (Not kept: the first 20 candidates straight into best and one 101-comparator sorting
-                // network.  With the pair-built lists its results in the 1024-thread class varied from
-                // run to run although the network sorts every input (0-1 principle, all 2^20 cases);
-                // the sorted inserts alone are exact and as fast with these lists.)
                 double4 nxt = pm ? spt[entry(__ffsll(static_cast<long long>(pm)) - 1)] : make_double4(0.0, 0.0, 0.0, 0.0);
                 while (pm) {
                     pm &= pm - 1;
@@ -2027,183 +2018,218 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 sring[atomicAdd(&s_ndef, 1)] = q;
                 continue;
             }
-            put_mean(r, best);
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
+            mavg[r] = sum / static_cast<double>(kk);
         }
         bar();
         BP_STAMP(34);  // k-NN: the list pass
 #ifdef MC_BP_STAMPS
         if (t == 0) atomicAdd(&g_bp_stamps[30], static_cast<unsigned long long>(s_ndef));
 #endif
-#if MC_KNN_RING == 0
-        for (int f = t; f < s_ndef; f += T) sfb[atomicAdd(&sfb[kFbCount], 1)] = spar[sring[f]];
-        if (false)
+        // m < k kept points: every kept point's mean over the whole cloud, a wave per point
+        const int nfb = sfb[kFbCount];
+        for (int f = wv; f < nfb; f += NW) {
+            const int r = sfb[f];
+            const double4 a = spt[spos[sX[r]]];
+            const double mean = wave_knn_mean(m, kk, [&](int j) {
+                const double4 p = spt[spos[sX[j]]];
+                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                return ((ex * ex) + (ey * ey)) + (ez * ez);
+            });
+            if (lane == 0) mavg[r] = mean;
+        }
+        // the deferred points: the slot's grid (cell-sorted records with kept bits, bucket starts,
+        // origin and extent) and its items (position | rank << 14) to its own ranges, the slot to the
+        // ring-search queue
+        const int nd = s_ndef;
+        if (nd > 0) {
+            double4 *gr = grec + base;
+            for (int i = t; i < n; i += T) gr[i] = spt[i];
+            int *gb = gbs + 2 * static_cast<size_t>(base) + s;
+            for (int b = t; b <= NBK * n; b += T) gb[b] = sA[b];
+            for (int f = t; f < nd; f += T) {
+                const int q = sring[f];
+                gitem[base + f] = q | (spar[q] << 14);
+            }
+            if (t == 0) {
+                const int e = atomicAdd(dq_cnt, 1);
+                dq[2 * e] = s;
+                dq[2 * e + 1] = nd;
+                double *gm = slot_grid + 8 * static_cast<size_t>(s);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    gm[c] = mn[c];
+                    gm[3 + c] = static_cast<double>(g.cmax[c]);
+                }
+                gm[6] = static_cast<double>(g.nb);
+                gm[7] = static_cast<double>(n);
+            }
+        }
+#ifdef MC_BP_STAMPS
+        if (t == 0 && s < (1 << 16)) g_bp_slot_time[s] = static_cast<unsigned>(__builtin_amdgcn_s_memrealtime() - slot_t0);
 #endif
-        for (int f = t; f < s_ndef; f += T) {
-            const int q = sring[f];
-            const int r = spar[q];
-            const double4 a = spt[q];
+        if (t == 0) slot_m[s] = m;
+        bar();
+    }
+}
+
+// (a4) k-NN of the deferred points of every LDS-class slot of a batch (k_bp_denoise_lds's list pass
+// could not serve them): a wave per deferred slot, a lane per point, over the slot's grid in global
+// memory.  Grid rings up to R = 2 (cells whose nearest face is no nearer than the current k-th
+// distance skipped: a's offsets in its cell, gaps shrunk by 1e-9 ce so the bound stays below every
+// point's computed distance); a point the rings cannot settle (sparse) scans every kept point.
+__global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_cnt, const int *__restrict__ dq,
+                                                     const int *__restrict__ slot_pix, BpDev pr,
+                                                     const double4 *__restrict__ grec, const int *__restrict__ gbs,
+                                                     const int *__restrict__ gitem, const double *__restrict__ slot_grid,
+                                                     double *__restrict__ gavg)
+{
+    const int ne = *dq_cnt;
+    const int lane = lane_id();
+    const int nwaves = gridDim.x * 4;
+    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < ne; e += nwaves) {
+        const int s = dq[2 * e], nd = dq[2 * e + 1];
+        const int base = slot_pix[s];
+        const double *gm = slot_grid + 8 * static_cast<size_t>(s);
+        const double mn[3] = {gm[0], gm[1], gm[2]};
+        BpLdsGrid g;
+        g.pt = grec + base;
+        g.bs = gbs + 2 * static_cast<size_t>(base) + s;
+        g.nb = static_cast<unsigned>(gm[6]);
+        const int n = static_cast<int>(gm[7]);
+#pragma unroll
+        for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(gm[3 + c]);
+        for (int f = lane; f < nd; f += 64) {
+            const int item = gitem[base + f];
+            const int q = item & 0x3FFF, r = item >> 14;
+            const double4 a = g.pt[q];
             double best[kBpKnnMax];
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
             int found = 0;
             bool done = false;
             int x, y, z;
-            unpack3(keyof(q), x, y, z);
+            unpack3(static_cast<unsigned long long>(__double_as_longlong(a.w)) & ~kKeptBit, x, y, z);
             auto take = [&](int, double d2) {
                 sorted_insert(best, d2);
                 found++;
             };
-#if MC_KNN_CULL
-            // a cell whose nearest face is no nearer than the current k-th distance holds no point
-            // the insert would keep: skipped (a's offsets in its cell, gaps shrunk by 1e-9 ce so the
-            // bound stays below every point's computed distance)
             const double ce = pr.ce, sl = 1e-9 * pr.ce;
             const double ox = fmin(fmax(a.x - mn[0] - x * ce, 0.0), ce), oy = fmin(fmax(a.y - mn[1] - y * ce, 0.0), ce),
                          oz = fmin(fmax(a.z - mn[2] - z * ce, 0.0), ce);
             auto gap = [&](int d, double o) {
                 return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? d * ce - o : -d * ce - (ce - o)) - sl);
             };
-#endif
             for (int R = 0; R <= 2 && !done; R++) {
                 for (int dz = -R; dz <= R; dz++)
                     for (int dy = -R; dy <= R; dy++) {
                         const bool edge = dz == -R || dz == R || dy == -R || dy == R;
                         const int step = (edge || R == 0) ? 1 : 2 * R;
-#if MC_KNN_CULL
                         const double gyz = gap(dy, oy) * gap(dy, oy) + gap(dz, oz) * gap(dz, oz);
-#endif
                         for (int dx = -R; dx <= R; dx += step) {
-#if MC_KNN_CULL
-                            if (gyz + gap(dx, ox) * gap(dx, ox) >= best[kBpKnnMax - 1]) continue;
-#endif
+                            if (MC_KNN_CULL && gyz + gap(dx, ox) * gap(dx, ox) >= best[kBpKnnMax - 1]) continue;
                             lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
                         }
                     }
-                const double reach = static_cast<double>(R) * pr.ce;
-                done = found >= kk && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
+                const double reach = static_cast<double>(R) * ce;
+                done = found >= kBpKnnMax && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
             }
-            if (!done) {
-                sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
-                continue;
-            }
-            put_mean(r, best);
-        }
-        bar();
-        BP_STAMP(35);  // k-NN: the ring search
-        const int nfb = sfb[kFbCount];
-        if (nfb > 2 * NW && kk == kBpKnnMax) {
-            // many sparse points: one per lane, every kept point scanned in sorted order (the same
-            // position for all lanes at once: LDS broadcast reads)
-            for (int f0 = 0; f0 < nfb; f0 += T) {
-                const int f = f0 + t;
-                const int r = f < nfb ? sfb[f] : -1;
-                const double4 a = spt[r >= 0 ? spos[sX[r]] : 0];
-                double best[kBpKnnMax];
+            if (!done) {  // sparse point: every kept point of the slot, in sorted order
 #pragma unroll
                 for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
                 for (int q2 = 0; q2 < n; q2++) {
-                    const double4 p = spt[q2];
+                    const double4 p = g.pt[q2];
                     if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
                     const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
                     sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
                 }
-                double sum = 0.0;
+            }
+            double sum = 0.0;
 #pragma unroll
-                for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
-                if (r >= 0) savg[r] = sum / static_cast<double>(kk);
-            }
-        } else {
-            for (int f = wv; f < nfb; f += NW) {
-                const int r = sfb[f];
-                const double4 a = spt[spos[sX[r]]];
-                const double mean = wave_knn_mean(m, kk, [&](int j) {
-                    const double4 p = spt[spos[sX[j]]];
-                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                    return ((ex * ex) + (ey * ey)) + (ez * ez);
-                });
-                if (lane == 0) savg[r] = mean;
-            }
+            for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
+            gavg[base + r] = sum / static_cast<double>(kBpKnnMax);
         }
-        bar();
-        BP_STAMP(26);
-        if constexpr (MC_DBG_CHECK) bp_dbg_knn<N>(g, spar, savg, n, kk, s);
-        // 11. cloud mean and Bessel std, sequential in index order (std::accumulate), by wave 0:
-        //     64 values per step are read at once, then added in order (lane reads are scalar).
-        //     (Measured and not kept: one lane loading eight values ahead of its eight dependent adds,
-        //     30 us per slot against 19.)
-        if (wv == 0) {
-            double mean = 0.0, sq = 0.0;
-            for (int r0 = 0; r0 < m; r0 += 64) {
-                // values that are not > 0 become +0.0, whose add leaves the (non-negative) sum as it is:
-                // the ordered chain is plain adds, the selects run lane-parallel before it
-                const double a = r0 + lane < m ? savg[r0 + lane] : 0.0;
-                mean = seq_add64_pos<false>(mean, a > 0 ? a : 0.0);
-            }
-            mean = mean / static_cast<double>(m);
-            for (int r0 = 0; r0 < m; r0 += 64) {
-                const double v = r0 + lane < m ? savg[r0 + lane] : 0.0;
-                const double d = v > 0 ? (v - mean) * (v - mean) : 0.0;
-                sq = seq_add64_pos<false>(sq, d > 0 ? d : 0.0);
-            }
-            const double sd = sqrt(sq / static_cast<double>(m - 1));
-            if (lane == 0) s_thr = mean + pr.std_ratio * sd;
+    }
+}
+
+// (a4) the end of denoise for every LDS-class slot (classes 0 .. kBpClasses-1), a wave per slot:
+// remove_statistical_outlier's cloud mean and Bessel std of the m mean distances as sequential sums
+// in index order (std::accumulate: 64 values read at once, then added in order as scalars), the
+// survivors 0 < d < mean + std_ratio * std in index order -> float32 mask points and their AABB.
+__global__ __launch_bounds__(256) void k_bp_denoise_tail(const int *__restrict__ cls_cnt, const int *__restrict__ cls_list,
+                                                         int cap, const int *__restrict__ slot_pix,
+                                                         const int *__restrict__ slot_m, BpDev pr,
+                                                         const double *__restrict__ vpts, const double *__restrict__ gavg,
+                                                         const int *__restrict__ gsx, float *__restrict__ qpts,
+                                                         int *__restrict__ slot_ns, float *__restrict__ slot_box)
+{
+    int cnt[kBpClasses];
+    int total = 0;
+#pragma unroll
+    for (int c = 0; c < kBpClasses; c++) {
+        cnt[c] = cls_cnt[c];
+        total += cnt[c];
+    }
+    const int lane = lane_id();
+    const int nwaves = gridDim.x * 4;
+    for (int x = blockIdx.x * 4 + (threadIdx.x >> 6); x < total; x += nwaves) {
+        int c = 0, o = x;
+        while (o >= cnt[c]) o -= cnt[c++];
+        const int s = cls_list[static_cast<size_t>(c) * cap + o];
+        const int base = slot_pix[s], m = slot_m[s];
+        const double *av = gavg + base;
+        const double *P = vpts + 3 * static_cast<size_t>(base);
+        if constexpr (MC_DBG_CHECK) bp_dbg_knn_tail(P, gsx + base, av, m, min(pr.knn, m), s);
+        double mean = 0.0, sq = 0.0;
+        for (int r0 = 0; r0 < m; r0 += 64) {
+            // values that are not > 0 become +0.0, whose add leaves the (non-negative) sum as it is:
+            // the ordered chain is plain adds, the selects run lane-parallel before it
+            const double a = r0 + lane < m ? av[r0 + lane] : 0.0;
+            mean = seq_add64_pos<false>(mean, a > 0 ? a : 0.0);
         }
-        bar();
-        const double thr = s_thr;
-        BP_STAMP(27);
-        // 12. survivors -> float32 mask points and their AABB
+        mean = mean / static_cast<double>(m);
+        for (int r0 = 0; r0 < m; r0 += 64) {
+            const double v = r0 + lane < m ? av[r0 + lane] : 0.0;
+            const double d = v > 0 ? (v - mean) * (v - mean) : 0.0;
+            sq = seq_add64_pos<false>(sq, d > 0 ? d : 0.0);
+        }
+        const double sd = sqrt(sq / static_cast<double>(m - 1));
+        const double thr = mean + pr.std_ratio * sd;
         int ns = 0;
         float flo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, fhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (int r0 = 0; r0 < m; r0 += T) {
-            const int r = r0 + t;
-            const int keep = (r < m && savg[r] > 0 && savg[r] < thr) ? 1 : 0;
-            int tot;
-            const int ex = block_excl_scan<T>(keep, ws, tot);
+        for (int r0 = 0; r0 < m; r0 += 64) {
+            const int r = r0 + lane;
+            const double v = r < m ? av[r] : 0.0;
+            const bool keep = r < m && v > 0 && v < thr;
+            const unsigned long long bal = __ballot(keep);
             if (keep) {
-                const int i = sX[r];
-                float *qo = qpts + 3 * (static_cast<size_t>(base) + ns + ex);
+                const int i = gsx[base + r];
+                float *qo = qpts + 3 * (static_cast<size_t>(base) + ns + __popcll(bal & ((1ull << lane) - 1ull)));
 #pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    qo[c] = static_cast<float>(P[3 * i + c]);
-                    flo[c] = fminf(flo[c], qo[c]);
-                    fhi[c] = fmaxf(fhi[c], qo[c]);
+                for (int cc = 0; cc < 3; cc++) {
+                    qo[cc] = static_cast<float>(P[3 * i + cc]);
+                    flo[cc] = fminf(flo[cc], qo[cc]);
+                    fhi[cc] = fmaxf(fhi[cc], qo[cc]);
                 }
             }
-            ns += tot;
+            ns += __popcll(bal);
         }
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            float a = flo[c], b = fhi[c];
+        for (int cc = 0; cc < 3; cc++) {
+            float a = flo[cc], b = fhi[cc];
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
                 a = fminf(a, __shfl_xor(a, d, 64));
                 b = fmaxf(b, __shfl_xor(b, d, 64));
             }
             if (lane == 0) {
-                fred[c * NW + wv] = a;
-                fred[3 * NW + c * NW + wv] = b;
+                slot_box[6 * s + cc] = a;
+                slot_box[6 * s + 3 + cc] = b;
             }
         }
-        bar();
-        BP_STAMP(28);
-#ifdef MC_BP_STAMPS
-        if (t == 0 && s < (1 << 16)) g_bp_slot_time[s] = static_cast<unsigned>(__builtin_amdgcn_s_memrealtime() - slot_t0);
-#endif
-        if (t == 0) {
-            slot_m[s] = m;
-            slot_ns[s] = ns;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                float a = fred[c * NW], b = fred[3 * NW + c * NW];
-                for (int w = 1; w < NW; w++) {
-                    a = fminf(a, fred[c * NW + w]);
-                    b = fmaxf(b, fred[3 * NW + c * NW + w]);
-                }
-                slot_box[6 * s + c] = a;
-                slot_box[6 * s + 3 + c] = b;
-            }
-        }
-        bar();
+        if (lane == 0) slot_ns[s] = ns;
     }
 }
 
