@@ -49,6 +49,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def own_device_budget(ctx, share=0.65):
+    """The bench owns its device: S1's batches may take `share` of the free HBM (the library's
+    default for callers that share the device is 40 % of it at most, mc_ctx_set_memory_budget)."""
+    import torch
+    free, _ = torch.cuda.mem_get_info()
+    ctx.set_memory_budget(int(free * share))
+
+
 def graph_work(ctx, mask_pts, P, F):
     """Per-launch algorithmic work of every graph kernel group.
 
@@ -278,6 +286,7 @@ class EndToEndStep:
         self.ctx = self.run.ctx
         self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+        own_device_budget(self.ctx)
         self.prm = _native.bp_params()
         self.groups = BP_GROUPS + G_GROUPS
         F, H, W = fr.depth.shape
@@ -381,6 +390,8 @@ class ShardedEndToEndStep(EndToEndStep):
         self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
         self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+        # one device per rank; the one-GPU rehearsal (MC_BENCH_DEVICE) splits it between the ranks
+        own_device_budget(self.ctx, 0.65 / (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
         self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs)
         assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731

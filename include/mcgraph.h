@@ -118,6 +118,10 @@ int mc_ctx_set_timing(mc_ctx *ctx, int enable);
 int mc_ctx_set_timing_filter(mc_ctx *ctx, const char *kernel);  /* NULL/"" = every kernel group */
 int mc_ctx_get_kernel_time(mc_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int mc_ctx_reset_kernel_times(mc_ctx *ctx);
+/* HBM the back-projection's per-batch arrays may take (bytes; 0 = the default: 40 % of the device
+   or 65 % of the free memory, whichever is less).  Batches are sized from it (~224 B per pixel);
+   a caller sharing the device with its own allocator (or other contexts) keeps the rest. */
+int mc_ctx_set_memory_budget(mc_ctx *ctx, int64_t bytes);
 /* diagnostics: out[0] = 1 if the library was built with in-kernel invariant checks
    (-DMC_DBG_CHECK=1), out[1 + k] = failures of check kind k so far; n <= 9 */
 int mc_debug_counters(mc_ctx *ctx, int64_t *out, int32_t n, int reset);

@@ -27,7 +27,25 @@ def context() -> _native.Context:
         except ImportError:
             pass
         _ctx = _native.Context(dev)
+        b = hbm_budget_from_env(dev)
+        if b:
+            _ctx.set_memory_budget(b)
     return _ctx
+
+
+def hbm_budget_from_env(device: int = 0) -> int:
+    """MASKCLUSTERING_HBM_BUDGET: the HBM bytes S1's per-batch arrays may take in the drop-in's
+    context, as bytes ("60e9") or as a fraction of the device (e.g. "0.3"); unset: the library's
+    default share (mc_ctx_set_memory_budget)."""
+    import os
+    v = os.environ.get("MASKCLUSTERING_HBM_BUDGET")
+    if not v:
+        return 0
+    x = float(v)
+    if 0 < x <= 1:
+        import torch
+        return int(x * torch.cuda.get_device_properties(device).total_memory)
+    return int(x)
 
 
 def as_numpy(x) -> np.ndarray:

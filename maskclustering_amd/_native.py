@@ -25,7 +25,7 @@ MC_ERR_NO_NODES = 6
 EXPORTED = [
     "mc_ctx_create", "mc_ctx_destroy", "mc_ctx_set_stream", "mc_ctx_get_stream", "mc_ctx_synchronize",
     "mc_ctx_last_error", "mc_ctx_set_timing", "mc_ctx_set_timing_filter", "mc_ctx_get_kernel_time", "mc_ctx_reset_kernel_times",
-    "mc_debug_counters", "mc_scene_set_masks", "mc_graph_build", "mc_graph_get_info", "mc_graph_get_global_masks",
+    "mc_debug_counters", "mc_ctx_set_memory_budget", "mc_scene_set_masks", "mc_graph_build", "mc_graph_get_info", "mc_graph_get_global_masks",
     "mc_graph_get_boundary", "mc_graph_get_point_in_mask", "mc_graph_get_point_frame_bits",
     "mc_graph_get_visible_frame_bits", "mc_graph_get_contained", "mc_graph_get_undersegment",
     "mc_graph_get_nodes0", "mc_graph_get_observer_hist", "mc_graph_get_thresholds", "mc_observer_thresholds",
@@ -133,6 +133,7 @@ def load():
         "mc_ctx_get_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
         "mc_ctx_reset_kernel_times": (ctypes.c_int, [vp]),
         "mc_debug_counters": (ctypes.c_int, [vp, vp, i32, ctypes.c_int]),
+        "mc_ctx_set_memory_budget": (ctypes.c_int, [vp, i64]),
         "mc_scene_set_masks": (ctypes.c_int, [vp, i64, i32, i32, vp, vp, vp, vp, ctypes.c_int]),
         "mc_graph_build": (ctypes.c_int, [vp, P(GraphParams)]),
         "mc_graph_get_info": (ctypes.c_int, [vp, P(GraphInfo)]),
@@ -284,6 +285,10 @@ class Context:
 
     def reset_kernel_times(self):
         self._check(self.L.mc_ctx_reset_kernel_times(self.h))
+
+    def set_memory_budget(self, nbytes: int):
+        """mc_ctx_set_memory_budget: HBM bytes S1's per-batch arrays may take (0 = the default share)."""
+        self._check(self.L.mc_ctx_set_memory_budget(self.h, int(nbytes)))
 
     def debug_counters(self, reset: bool = False):
         """(checks compiled in, failures per check kind): the in-kernel invariant checks of a

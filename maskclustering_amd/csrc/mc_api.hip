@@ -132,6 +132,7 @@ struct mc_ctx {
     DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt, d_bppack;
     DevBuf d_dq, d_slot_grid;  // denoise: deferred k-NN slots (slot, count) and their grid origin / extent
     int num_cu = 256;
+    int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
     int bp_bm_blocks = 0;
@@ -467,6 +468,14 @@ int mc_ctx_reset_kernel_times(mc_ctx *ctx)
         MC_HIP(hipStreamSynchronize(ctx->stream));
         ctx->timer.collect();
         ctx->timer.totals.clear();
+    });
+}
+
+int mc_ctx_set_memory_budget(mc_ctx *ctx, int64_t bytes)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(bytes >= 0, MC_ERR_INVALID, "negative memory budget");
+        ctx->mem_budget = bytes;
     });
 }
 
@@ -1750,6 +1759,9 @@ enum BpStat : int {
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
+// HBM of the per-batch S1 arrays per pixel of the batch (bp_reserve: the per-pixel arrays sum to 219 B;
+// the per-slot and per-frame ones are small against them)
+constexpr size_t kBpBytesPerPixel = 224;
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
 // Workgroups per resident slot of a denoise class (the classes take slots from tickets): the extra
@@ -2113,12 +2125,21 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // batch takes up to 1 G pixels or 65 % of the free HBM (≈ 170 GB of a fresh 288 GB device),
         // whichever is less; the frames are then dealt into equal batches, so that no batch is a small
         // remainder with its own tails
+        // The per-batch arrays take at most the context's HBM budget (mc_ctx_set_memory_budget), by
+        // default 40 % of the device or 65 % of what is free (plus what this context already holds),
+        // whichever is less, so a caller's own allocator keeps room (a fresh 288 GB MI355X: ~115 GB,
+        // ~530 M pixels per batch); a caller that owns the device (bench.py) sets a larger one.
         size_t budget = static_cast<size_t>(1) << 30;
-        if (ctx->bp_px_cap < budget) {
-            size_t free_b = 0, total_b = 0;
-            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
-                budget = std::max<size_t>(static_cast<size_t>(16) << 20,
-                                          std::min(budget, (free_b + ctx->bp_px_cap * 200) / 100 * 65 / 200));
+        {
+            const size_t held = ctx->bp_px_cap * kBpBytesPerPixel;
+            size_t bytes = static_cast<size_t>(ctx->mem_budget);
+            if (ctx->mem_budget <= 0) {
+                size_t free_b = 0, total_b = 0;
+                bytes = held;
+                if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b)
+                    bytes = std::min(total_b / 100 * 40, (free_b + held) / 100 * 65);
+            }
+            budget = std::max<size_t>(HW, std::min(budget, bytes / kBpBytesPerPixel));  // >= one frame
         }
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         BpUpload *const up = on_device ? ctx->bp_up : nullptr;

@@ -278,3 +278,23 @@ def test_in_kernel_invariants(ctx, monkeypatch):
                 _run(ctx, *inp)
                 _, bad = ctx.debug_counters(reset=True)
                 assert not bad.any(), f"class >= {min_cls}, nbcap {nbcap}: failures per kind {bad.tolist()}"
+
+
+def test_two_contexts_share_a_device_under_budgets():
+    """Two live contexts on one device, each within its own HBM budget (mc_ctx_set_memory_budget;
+    no MC_BP_BATCH_PIXELS): a budget that admits only a few frames per batch gives the same masks as
+    the default one, whichever context runs, interleaved."""
+    from maskclustering_amd import _native
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=2)
+    F, H, W = fr.depth.shape
+    a, b = _native.Context(0), _native.Context(0)
+    b.set_memory_budget(224 * 3 * H * W)            # three frames per batch
+    want = _run(a, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    got = _run(b, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    again = _run(a, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    for x, y, z in zip(want, got, again):
+        np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(x, z)
+    with pytest.raises(_native.McError):
+        b.set_memory_budget(-1)
