@@ -528,13 +528,13 @@ class FrameDataset:  # dataset/scannet.py:34-73 over arrays
         return self.fr.seg[self.col[f]]
 
 
-def run_api(a):
-    """--variant api: the reference-API boundary exactly as main.py:17-21 calls it, on the synthetic
-    RGB-D scene whose dataset object serves decoded frames from host memory (dataset/scannet.py:
-    get_depth / get_segmentation / get_intrinsics / get_extrinsic): one step =
-    mask_graph_construction + iterative_clustering (+ post_process's compute, without the file
-    export).  ms_per_step is the wall time of that Python call sequence, host packing and PCIe
-    included; the device part is the S1-S6 of the e2e variant."""
+def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=False, fr=None):
+    """The reference-API boundary exactly as main.py:17-21 calls it, on the synthetic RGB-D scene
+    whose dataset object serves decoded frames from host memory (dataset/scannet.py: get_depth /
+    get_segmentation / get_intrinsics / get_extrinsic): one step = mask_graph_construction +
+    iterative_clustering (replay=None: the default, the reference's container orders; False:
+    canonical) (+ post_process's compute, without the file export).  Wall time of that Python call
+    sequence, host packing and PCIe included, per part.  Returns (record, frames)."""
     import cProfile
     import pstats
 
@@ -543,10 +543,11 @@ def run_api(a):
     from maskclustering_amd.synthetic_frames import make_frames_shape
     from maskclustering_amd.utils import post_process as pp
 
-    t0 = time.perf_counter()
-    fr = make_frames_shape(a.shape, seed=a.seed, device="cuda:0")
+    if fr is None:
+        t0 = time.perf_counter()
+        fr = make_frames_shape(shape, seed=seed, device="cuda:0")
+        log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
     fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
-    log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
     args = SimpleNamespace(debug=False, point_filter_threshold=0.5, **CFG)
     ds = FrameDataset(fr, fids)
     parts = {"graph": [], "cluster": [], "post_process": []}
@@ -556,44 +557,57 @@ def run_api(a):
         nodes, thr, mpc, pfm = construction.mask_graph_construction(args, fr.scene_points, fids, ds)
         t1 = time.perf_counter()
         objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False,
-                                                            replay=a.replay)
+                                                            replay=replay)
         t2 = time.perf_counter()
         out = pp.post_process_objects(objects, mpc, fr.scene_points, pfm, fids, args.point_filter_threshold) \
-            if a.with_pp else None
+            if with_pp else None
         t3 = time.perf_counter()
         parts["graph"].append(t1 - t)
         parts["cluster"].append(t2 - t1)
         parts["post_process"].append(t3 - t2)
         return nodes, objects, out
 
-    for _ in range(max(a.warmup, 1)):
+    for _ in range(max(warmup, 1)):
         nodes, objects, _ = step()
     for v in parts.values():
         v.clear()
     torch.cuda.synchronize()
     walls = []
-    for _ in range(a.steps):
+    for _ in range(steps):
         t = time.perf_counter()
         step()
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t)
-    if a.profile:
+    if profile:
         pr = cProfile.Profile()
         pr.enable()
         step()
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
     ms = 1e3 * float(np.mean(walls))
+    mode = "reference" if replay is None or replay else "canonical"
+    rec = {"scene_ms": round(ms, 3), "set_order": mode, "with_post_process": bool(with_pp),
+           "part_ms": {k: round(1e3 * float(np.mean(v)), 3) for k, v in parts.items() if v and (k != "post_process"
+                                                                                              or with_pp)},
+           "workload": f"{shape}: synthetic RGB-D scene, {fr.num_frames} frames {fr.depth.shape[2]}x{fr.depth.shape[1]}, "
+                       f"P={fr.num_points}, {len(nodes)} nodes -> {len(objects)} objects; frames served from host "
+                       f"memory by the dataset (PCIe and host packing in the time)"}
+    return rec, fr
+
+
+def run_api(a):
+    """--variant api: the reference-API call sequence (api_timing) as its own line; ms_per_step is the
+    wall time of main.py:17-21's calls, host packing and PCIe included (the device part is the
+    e2e variant's S1-S6)."""
+    rec, _ = api_timing(a.shape, a.seed, a.steps, a.warmup, replay=False if a.canonical else None,
+                        with_pp=a.with_pp, profile=a.profile)
+    ms = rec["scene_ms"]
     res = {"metric": "reference-API graph path ms per scene (main.py:17-21 through the drop-in modules)",
-           "value": round(ms, 3), "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-           "ms_per_step": round(ms, 3), "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
+           "value": ms, "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": ms, "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
            "dtype": "int32", "data": "synthetic",
-           "config": {"workload": f"{a.shape}: synthetic RGB-D scene, {fr.num_frames} frames "
-                                  f"{fr.depth.shape[2]}x{fr.depth.shape[1]}, P={fr.num_points}, "
-                                  f"{len(nodes)} nodes -> {len(objects)} objects", "variant": "api",
-                      "replay": bool(a.replay),
-                      "with_post_process": bool(a.with_pp),
-                      "part_ms": {k: round(1e3 * float(np.mean(v)), 3) for k, v in parts.items() if v}}}
+           "config": {"workload": rec["workload"], "variant": "api", "set_order": rec["set_order"],
+                      "with_post_process": rec["with_post_process"], "part_ms": rec["part_ms"]}}
     print(json.dumps(res), flush=True)
 
 
@@ -774,8 +788,9 @@ def main():
     ap.add_argument("--pool", type=int, default=4, help="sweep: distinct rendered scenes per rank")
     ap.add_argument("--with-pp", action="store_true", help="api: include post_process's compute")
     ap.add_argument("--profile", action="store_true", help="api: cProfile one extra step to stderr")
-    ap.add_argument("--replay", action="store_true", help="api: iterative_clustering(replay=True), the "
-                                                          "reference-exact set orders (INTEGRATION.md §4)")
+    ap.add_argument("--canonical", action="store_true", help="api: iterative_clustering(replay=False), contents "
+                                                             "only (the default is the reference's set orders, "
+                                                             "INTEGRATION.md §4)")
     ap.add_argument("--shape", default=None, help="default: c3 (g, e2e), c2 (api, pp, sweep)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -864,6 +879,7 @@ def main():
     elapsed = float(t.item())
 
     gi = ctx.graph_info()
+    s6_ms = sum(calib.get(g, (0.0, 0))[0] for g in ("s6_columns", "s6_pairs", "s6_components", "s6_merge"))
     total_pairs = pairs_per_step * args.steps * (1 if frames else world)
     value = total_pairs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -912,6 +928,19 @@ def main():
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary and args.variant in ("e2e", "g"):
         secondary = c2_record(local, max(3, min(args.steps, 10)), args.warmup)
+        # the boundary main.py calls (reference-API drop-ins, frames from host memory) on the same C2
+        # scene: default (the reference's container orders) with post_process, and canonical
+        n_api = max(3, min(args.steps, 5))
+        api, fr_c2 = api_timing("c2", 0, n_api, 2, replay=None, with_pp=True)
+        can, _ = api_timing("c2", 0, n_api, 2, replay=False, fr=fr_c2)
+        e2e_ms = secondary["c2_e2e"]["scene_ms"]
+        api["over_device_e2e"] = round((api["scene_ms"] - api["part_ms"].get("post_process", 0.0)) / e2e_ms, 2)
+        can["over_device_e2e"] = round(can["scene_ms"] / e2e_ms, 2)
+        secondary["c2_api"] = api
+        secondary["c2_api_canonical"] = can
+        secondary["c2_pp"] = {"scene_ms": api["part_ms"].get("post_process"),
+                              "note": "post_process_objects (utils/post_process.py:180-194: DBSCAN split, point "
+                                      "filter, overlap merge; host packing included) on the c2_api run's objects"}
 
     if rank == 0:
         line = {
@@ -932,6 +961,10 @@ def main():
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
                        "stage_ms": {k: round(v[0], 4) for k, v in calib.items()},
                        "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}"},
+            # SURVEY.md §8(d)'s own definition of the pair metric: the same pairs over S6's time only
+            "pairs_per_s_s6": round(pairs_per_step / max(s6_ms / 1e3, 1e-12), 1),
+            "pairs_per_s_s6_def": "sum_t N_t^2 / sum_t (S6 iteration t's device time: s6_columns + s6_pairs + "
+                                  "s6_components + s6_merge of the calibration step, HIP events)",
             "roofline": roof,
             "stage_roofline": stages,
             "cpu_baseline": cpu,
