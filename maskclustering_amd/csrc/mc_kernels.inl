@@ -1317,6 +1317,24 @@ __device__ __forceinline__ void edge_capture(EdgeCap ec, int t, int a, int b)
                       static_cast<unsigned long long>(b);
 }
 
+// the same from a converged wave, one counter add per wave (every lane calls it; `e` = this lane
+// has the edge (a, b))
+__device__ __forceinline__ void edge_capture_wave(EdgeCap ec, int t, int a, int b, bool e)
+{
+    if (!ec.buf) return;
+    const unsigned long long bal = __ballot(e);
+    if (!bal) return;
+    const int lane = static_cast<int>(threadIdx.x & 63);
+    const int leader = __ffsll(static_cast<long long>(bal)) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(ec.cnt, static_cast<unsigned long long>(__popcll(bal)));
+    base = __shfl(base, leader, 64);
+    const unsigned long long pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+    if (e && pos < static_cast<unsigned long long>(ec.cap))
+        ec.buf[pos] = (static_cast<unsigned long long>(t) << 48) | (static_cast<unsigned long long>(a) << 24) |
+                      static_cast<unsigned long long>(b);
+}
+
 struct OvfWork {
     int *scratch, *touched;  // kOvfSlots dense counters / touched lists of N0 ints (zero at rest)
     int N0;
@@ -1476,9 +1494,10 @@ __global__ __launch_bounds__(256) void k6_pairs(const int *__restrict__ dN, cons
                 }
 #pragma unroll
                 for (int r = 0; r < kTestBatch; r++) {
-                    if (bn[r] >= 0 && edge_ok(ob[r], sc[r], er)) {
+                    const bool e = bn[r] >= 0 && edge_ok(ob[r], sc[r], er);
+                    edge_capture_wave(ec, t, a, bn[r], e);
+                    if (e) {
                         nedges++;
-                        edge_capture(ec, t, a, bn[r]);
                         if (MC_ABLATE_PAIRS != 1 && MC_ABLATE_PAIRS != 5) uf_unite(parent, a, bn[r]);
                     }
                 }
