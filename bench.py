@@ -392,7 +392,10 @@ class ShardedEndToEndStep(EndToEndStep):
         self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
         # one device per rank; the one-GPU rehearsal (MC_BENCH_DEVICE) splits it between the ranks
         own_device_budget(self.ctx, 0.65 / (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
-        self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs)
+        # MC_BENCH_NATIVE_COMM=1: the sharded graph stages exchange over the library's own RCCL
+        # communicator (mc_ctx_comm_init) instead of torch.distributed between calls
+        native = os.environ.get("MC_BENCH_NATIVE_COMM", "0") == "1" and world > 1
+        self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs, native_comm=native)
         assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.t_depth, self.t_seg = fr.depth, fr.seg

@@ -203,7 +203,7 @@ class FrameShardedScene:
     """
 
     def __init__(self, run, num_points: int, num_frames: int, group=None, shard_graph: bool = True,
-                 costs=None):
+                 costs=None, native_comm: bool = False):
         from .graph_shard import ShardedGraph
         self.run = run
         self.ctx = run.ctx
@@ -227,7 +227,9 @@ class FrameShardedScene:
         self.max_masks = 255 * max(1, max(hi - lo for lo, hi in self.slices))
         self._pts = None  # global point ids (kept alive until the graph input copy is done)
         # the graph stages row-block sharded over the same ranks (shard_graph=False: replicated)
-        self.graph = ShardedGraph(run, group) if shard_graph else None
+        # (native_comm: the graph stages' exchanges run inside the library over its own RCCL
+        # communicator, mc_ctx_comm_init, instead of torch.distributed collectives between calls)
+        self.graph = ShardedGraph(run, group, native_comm=native_comm) if shard_graph else None
 
     @property
     def pts(self) -> torch.Tensor:
