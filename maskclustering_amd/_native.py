@@ -184,7 +184,11 @@ def load():
         "mc_ctx_comm_init": (ctypes.c_int, [vp, vp, i32, i32]),
         "mc_ctx_attach_comm": (ctypes.c_int, [vp, vp]),
     }
+    # MCGRAPH_LIB_PARTIAL=1 (A/B scripts only): an older variant library may lack newer entry points
+    partial = os.environ.get("MCGRAPH_LIB_PARTIAL") == "1"
     for name, (res, args) in sig.items():
+        if partial and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

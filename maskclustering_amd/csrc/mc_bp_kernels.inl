@@ -569,6 +569,10 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
+#ifndef MC_VX_RECOMPUTE
+#define MC_VX_RECOMPUTE 0  // 1: no staged world points; 1. re-derives them in pixel order, 3. lists pixel
+                           //    indices and 4. re-derives its points from one depth gather each (A/B knob)
+#endif
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
 // (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
@@ -643,7 +647,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                     bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
-                        pp[3 * k + c] = p[c];
+                        if (!MC_VX_RECOMPUTE) pp[3 * k + c] = p[c];
                         mn[c] = fmin(mn[c], p[c]);
                     }
                 }
@@ -660,7 +664,14 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int k = c0 + t;
             int h = -1;
             if (k < n) {
-                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
+                double p[3];
+                if (MC_VX_RECOMPUTE) {
+                    vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
+                } else {
+                    p[0] = pp[3 * k];
+                    p[1] = pp[3 * k + 1];
+                    p[2] = pp[3 * k + 2];
+                }
                 unsigned key = 0;
                 bool fits = true;
 #pragma unroll
@@ -755,7 +766,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 }
                 lds_barrier();
             }
-            if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
+            if (v >= 0) vlist[base + gb[wv][leader] + rank] = MC_VX_RECOMPUTE ? static_cast<int>(pl[k]) : k;
         }
         sync_global();  // 4. reads the lists other waves wrote
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
@@ -764,6 +775,33 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
+            if (MC_VX_RECOMPUTE) {  // the list holds pixel indices: one depth gather per point
+                for (; j + 4 <= b1; j += 4) {
+                    unsigned iv[4];
+                    float dv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) iv[u] = static_cast<unsigned>(vl[j + u]);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) dv[u] = dep[iv[u]];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        double x, y, z;
+                        bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], x, y, z);
+                        ax = ax + x;
+                        ay = ay + y;
+                        az = az + z;
+                    }
+                }
+                for (; j < b1; j++) {
+                    const unsigned i = static_cast<unsigned>(vl[j]);
+                    double x, y, z;
+                    bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], x, y, z);
+                    ax = ax + x;
+                    ay = ay + y;
+                    az = az + z;
+                }
+                j = b1;
+            }
             for (; j + 4 <= b1; j += 4) {
                 const double *q[4];
 #pragma unroll
