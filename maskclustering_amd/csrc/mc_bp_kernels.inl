@@ -1435,9 +1435,10 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 // counter returns (sflag[] holds the counts, self entries already in slot 0).  Half the candidate
 // records of lds_eps_list; the slot order within a list is arbitrary, which no consumer depends on
 // (the union and the border labels are order-free, the k-NN sorts).
-template <int N>
+template <int N, bool kUnite>
 __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag)
+                                              const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag,
+                                              int *spar)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
@@ -1447,6 +1448,7 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
     };
     const double eps2 = pr.eps2;
+    int ra = kUnite ? uf_find_s(spar, q) : 0;
     auto visit = [&](const double4 &p, int q2, unsigned long long key) {
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
@@ -1455,6 +1457,16 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
             const int o1 = atomicAdd(&sflag[q], 1), o2 = atomicAdd(&sflag[q2], 1);
             if (o1 < kBpNbCap) nb_put<N>(nbw, q, o1, static_cast<unsigned>(q2) | c);
             if (o2 < kBpNbCap) nb_put<N>(nbw, q2, o2, static_cast<unsigned>(q) | c);
+            if constexpr (kUnite) {  // speculative: every pair, as if both points were core
+                const int p2 = ld_wg(spar + q2);
+                if (p2 != ra) {
+                    const int rb = uf_find_s(spar, p2);
+                    if (rb != ra) {
+                        uf_unite_s(spar, ra, rb);
+                        ra = uf_find_s(spar, ra);
+                    }
+                }
+            }
         }
     };
     unsigned long long nkey = 0;
@@ -1669,6 +1681,10 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 #ifndef MC_ABLATE_BP
 #define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union
 #endif
+#ifndef MC_BP_FUSED_UNION
+#define MC_BP_FUSED_UNION 1  // union every pair while the lists are built; the separate union pass only for
+                             // slots with a non-core point that has neighbours (0: A/B baseline)
+#endif
 
 template <int N>
 __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsClass<N>::T / 256) void k_bp_denoise_lds(
@@ -1817,7 +1833,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) {
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
-                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag);
+                lds_eps_pairs<N, MC_BP_FUSED_UNION != 0>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
+                                                          spar);
             }
             sync_global();  // the lists hold other waves' stores
         } else {
@@ -1832,8 +1849,27 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         bar();
         BP_STAMP(21);
         if constexpr (MC_DBG_CHECK) bp_dbg_lists<N>(g, sflag, nbw, n, pr, s);
-        // 6. connected core points: list points first; points with more than kBpNbCap neighbours
-        //    are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
+        // 6. connected core points.  Where the pair pass already united every pair (MC_BP_FUSED_UNION)
+        //    that union is the core-point union unless a non-core point has neighbours (every pair then
+        //    joins two core points; an isolated point joins nothing), so only such slots run the pass
+        //    below, from a fresh forest.  The pass: list points first; points with more than nbcap
+        //    neighbours are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
+        bool need_union = true;
+        if constexpr (!kBpLean2<N> && MC_BP_FUSED_UNION != 0) {
+            if (t == 0) s_ndef = 0;
+            bar();
+            for (int q = t; q < n; q += T) {
+                const int cnt = nb_cnt(sflag[q]);
+                if (cnt >= 2 && cnt < pr.minpts) s_ndef = 1;
+            }
+            bar();
+            need_union = s_ndef != 0;
+            if (need_union) {
+                for (int q = t; q < n; q += T) spar[q] = q;
+                bar();
+            }
+        }
+        if (need_union) {
         if (t == 0) s_ndef = 0;
         bar();
         for (int q = t; q < n; q += T) {
@@ -1881,6 +1917,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             });
         }
         bar();
+        }  // need_union
         BP_STAMP(22);
         // 7. roots; every component keyed by its smallest original index; clusters ranked by it
         {
