@@ -130,7 +130,7 @@ struct mc_ctx {
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
     DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt, d_bppack;
-    DevBuf d_dq, d_slot_grid;  // denoise: deferred k-NN slots (slot, count) and their grid origin / extent
+    DevBuf d_slot_grid;  // denoise: grid origin / extent of the slots with points queued for the k-NN ring search
     int num_cu = 256;
     int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
     size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
@@ -383,7 +383,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
                          &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid,
-                         &ctx->d_dq, &ctx->d_slot_grid};
+                         &ctx->d_slot_grid};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy), (void)hipStreamDestroy(ctx->copy);
     if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
@@ -1754,7 +1754,7 @@ enum BpStat : int {
     BS_TK = BS_CLS + mc::kBpClasses + 1,  // ticket counters of the LDS classes
     BS_VXFB = BS_TK + mc::kBpClasses,     // slots the first voxel tier hands to the second
     BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
-    BS_DQ,                                // slots with points deferred to the k-NN ring search
+    BS_DQ,                                // points queued for the k-NN ring search
     BS_COUNT
 };
 
@@ -1821,7 +1821,6 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
     ctx->d_cls_list.reserve((mc::kBpClasses + 1) * slots * 4);
     ctx->d_vox_order.reserve(slots * 4);
     ctx->d_vx_fb.reserve(2 * slots * 4);  // the two tiers' overflow lists
-    ctx->d_dq.reserve(2 * slots * 4);
     ctx->d_slot_grid.reserve(8 * slots * 8);
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
     ctx->d_nbl.reserve(nbl_offset(ctx, mc::kBpClasses) * 2);
@@ -1903,8 +1902,8 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
                        ctx->d_slot_m.as<int>(), ctx->d_avg.as<double>(), ctx->d_ssidx.as<int>(),
-                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_pbkt.as<int>(), ctx->d_dq.as<int>(),
-                       st + BS_DQ, ctx->d_slot_grid.as<double>());
+                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
+                       ctx->d_vx_pvid.as<int>(), st + BS_DQ, ctx->d_slot_grid.as<double>());
 }
 // MC_BP_DEBUG_SYNC=1: synchronise and report after every S1 group (diagnostics of a stalled batch)
 void bp_debug_sync(hipStream_t s, const char *what)
@@ -2333,9 +2332,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 }
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
                 // the deferred points' ring search, then every LDS-class slot's statistics and survivors
-                hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 4), dim3(256), 0, s, st + BS_DQ,
-                                   ctx->d_dq.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
-                                   ctx->d_bstart.as<int>(), ctx->d_pbkt.as<int>(), ctx->d_slot_grid.as<double>(),
+                hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ,
+                                   ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
+                                   ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_slot_grid.as<double>(),
                                    ctx->d_avg.as<double>());
                 hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * 4), dim3(256), 0, s, st + BS_CLS,
                                    ctx->d_cls_list.as<int>(), ncap, ctx->d_slot_pix.as<int>(), ctx->d_slot_m.as<int>(),

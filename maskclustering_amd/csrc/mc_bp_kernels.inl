@@ -2116,22 +2116,23 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             if (lane == 0) mavg[r] = mean;
         }
         // the deferred points: the slot's grid (cell-sorted records with kept bits, bucket starts,
-        // origin and extent) and its items (position | rank << 14) to its own ranges, the slot to the
-        // ring-search queue
+        // origin and extent) to its own ranges, its points to the batch's ring-search queue (slot,
+        // position | rank << 14; at most one entry per voxel of the batch, so a pixel-sized array holds it)
         const int nd = s_ndef;
         if (nd > 0) {
             double4 *gr = grec + base;
             for (int i = t; i < n; i += T) gr[i] = spt[i];
             int *gb = gbs + 2 * static_cast<size_t>(base) + s;
             for (int b = t; b <= NBK * n; b += T) gb[b] = sA[b];
+            if (t == 0) s_slot = atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
+            bar();
+            const int e0 = s_slot;
             for (int f = t; f < nd; f += T) {
                 const int q = sring[f];
-                gitem[base + f] = q | (spar[q] << 14);
+                dq[e0 + f] = s;
+                gitem[e0 + f] = q | (spar[q] << 14);
             }
             if (t == 0) {
-                const int e = atomicAdd(dq_cnt, 1);
-                dq[2 * e] = s;
-                dq[2 * e + 1] = nd;
                 double *gm = slot_grid + 8 * static_cast<size_t>(s);
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
@@ -2151,8 +2152,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 }
 
 // (a4) k-NN of the deferred points of every LDS-class slot of a batch (k_bp_denoise_lds's list pass
-// could not serve them): a wave per deferred slot, a lane per point, over the slot's grid in global
-// memory.  Grid rings up to R = 2 (cells whose nearest face is no nearer than the current k-th
+// could not serve them): a thread per queued point, over its slot's grid in global memory.  Grid rings up to R = 2 (cells whose nearest face is no nearer than the current k-th
 // distance skipped: a's offsets in its cell, gaps shrunk by 1e-9 ce so the bound stays below every
 // point's computed distance); a point the rings cannot settle (sparse) scans every kept point.
 __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_cnt, const int *__restrict__ dq,
@@ -2162,10 +2162,8 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                                                      double *__restrict__ gavg)
 {
     const int ne = *dq_cnt;
-    const int lane = lane_id();
-    const int nwaves = gridDim.x * 4;
-    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < ne; e += nwaves) {
-        const int s = dq[2 * e], nd = dq[2 * e + 1];
+    for (int f = blockIdx.x * 256 + threadIdx.x; f < ne; f += gridDim.x * 256) {
+        const int s = dq[f];
         const int base = slot_pix[s];
         const double *gm = slot_grid + 8 * static_cast<size_t>(s);
         const double mn[3] = {gm[0], gm[1], gm[2]};
@@ -2176,8 +2174,8 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
         const int n = static_cast<int>(gm[7]);
 #pragma unroll
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(gm[3 + c]);
-        for (int f = lane; f < nd; f += 64) {
-            const int item = gitem[base + f];
+        {
+            const int item = gitem[f];
             const int q = item & 0x3FFF, r = item >> 14;
             const double4 a = g.pt[q];
             double best[kBpKnnMax];
