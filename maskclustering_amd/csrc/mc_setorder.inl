@@ -23,6 +23,9 @@
 // dummy.  Pinned against the running interpreter (tests/test_setorder_cpu.py: random histories and the
 // reference's own exports, tests/golden/e2e_pp_small_*).
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -130,8 +133,48 @@ inline void merge(PySet &s, const PySet &o)
         if (k >= 0) add(s, k);
 }
 
+// merge() of a set the caller no longer needs: into an empty set whose mask (after the up-front
+// resize) is the other's, the verbatim copy is the other's table itself
+inline void merge_consume(PySet &s, PySet &&o)
+{
+    if (s.used == 0 && o.used != 0) {
+        size_t ns = s.mask + 1;
+        if ((s.used + o.used) * 5 >= s.mask * 3) {
+            ns = kMinSize;
+            while (ns <= (s.used + o.used) * 2) ns <<= 1;
+            if (ns == kMinSize && s.mask == kMinSize - 1) ns = s.mask + 1;
+        }
+        if (ns - 1 == o.mask) {
+            s = std::move(o);
+            return;
+        }
+    }
+    merge(s, o);
+}
+
 // a.union(b) when the caller no longer needs a: the copy step (make_new_set + set_merge into the
 // empty set) keeps a's table when its mask is what the copy would size, else re-inserts in slot order
+inline PySet union_consume(PySet &&a, PySet &&b)
+{
+    PySet r;
+    if (a.used) {
+        size_t ns = kMinSize;
+        if (a.used * 5 >= (kMinSize - 1) * 3)
+            while (ns <= a.used * 2) ns <<= 1;
+        if (ns - 1 == a.mask) {
+            r = std::move(a);
+        } else {
+            r.t.assign(ns, -1);
+            r.mask = ns - 1;
+            for (int32_t k : a.t)
+                if (k >= 0) insert_clean(r.t.data(), r.mask, k);
+            r.used = a.used;
+        }
+    }
+    merge_consume(r, std::move(b));
+    return r;
+}
+
 inline PySet union_consume(PySet &&a, const PySet &b)
 {
     PySet r;
@@ -161,6 +204,67 @@ inline PySet from_sequence(const int32_t *v, int64_t n)
     return s;
 }
 
+// Workers kept for the whole replay (one set of threads instead of a spawn per level): run(fn) runs fn
+// on every worker and the calling thread and returns when all are done.
+class Pool {
+  public:
+    explicit Pool(int n) : n_(n)
+    {
+        for (int i = 1; i < n_; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void run(const std::function<void()> &fn)
+    {
+        if (n_ == 1) return fn();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            busy_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        fn();
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [this] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop()
+    {
+        unsigned seen = 0;
+        while (true) {
+            const std::function<void()> *job;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+            }
+            (*job)();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void()> *job_ = nullptr;
+    unsigned gen_ = 0;
+    int busy_ = 0;
+    bool quit_ = false;
+};
+
 }  // namespace mcso
 
 extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
@@ -185,8 +289,15 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
         if (pt_off[N0] && !pts) return MC_ERR_INVALID;
         for (int64_t k = 0; k < pt_off[N0]; k++)
             if (pts[k] < 0) return MC_ERR_INVALID;
-        int nth = num_threads > 0 ? num_threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        // threads: the caller's count, else the host's, capped by OMP_NUM_THREADS (a process's CPU share:
+        // hardware_concurrency reports the whole machine)
+        int nth = num_threads;
+        if (nth <= 0) {
+            nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+            if (const char *e = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(e)));
+        }
         nth = std::max(1, std::min(nth, 64));
+        mcso::Pool pool(nth);
 
         // per node of the current level: its mask order (level-0 indices) and point set; level 0's
         // sets are made by the worker that consumes them (each is read by exactly one component)
@@ -216,7 +327,14 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
                     adj[cur[edge_b[e]]++] = edge_a[e];
                 }
             }
-            for (int v = 0; v < N; v++) std::sort(adj.begin() + aoff[v], adj.begin() + aoff[v + 1]);
+            {  // edges sorted by (a, b) already give every list in ascending order
+                bool sorted = true;
+                for (int64_t e = e0 + 1; e < e1 && sorted; e++)
+                    sorted = edge_a[e - 1] < edge_a[e] || (edge_a[e - 1] == edge_a[e] && edge_b[e - 1] < edge_b[e]);
+                for (int64_t e = e0; e < e1 && sorted; e++) sorted = edge_a[e] < edge_b[e];
+                if (!sorted)
+                    for (int v = 0; v < N; v++) std::sort(adj.begin() + aoff[v], adj.begin() + aoff[v + 1]);
+            }
             // components: _plain_bfs from every unseen node in order; `seen` is a set of node ints
             std::vector<int32_t> lab(static_cast<size_t>(N), -1);
             comp_off.assign(1, 0);
@@ -263,20 +381,16 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
                         const int32_t m = comp_mem[j];
                         mo.insert(mo.end(), morder[m].begin(), morder[m].end());
                         if (t == 0) {
-                            const PySet s0 = mcso::from_sequence(pts + pt_off[m], pt_off[m + 1] - pt_off[m]);
-                            acc = mcso::union_consume(std::move(acc), s0);
-                        } else {
-                            acc = mcso::union_consume(std::move(acc), sets[m]);
+                            acc = mcso::union_consume(std::move(acc),
+                                                      mcso::from_sequence(pts + pt_off[m], pt_off[m + 1] - pt_off[m]));
+                        } else {  // every level-t set is read by exactly one component
+                            acc = mcso::union_consume(std::move(acc), std::move(sets[m]));
                         }
                     }
                     nsets[k] = std::move(acc);
                 }
             };
-            const int nw = std::min(nth, std::max(1, K / 4));
-            std::vector<std::thread> th;
-            for (int w = 1; w < nw; w++) th.emplace_back(work);
-            work();
-            for (auto &x : th) x.join();
+            pool.run(work);
             morder.swap(nmorder);
             sets.swap(nsets);
         }
