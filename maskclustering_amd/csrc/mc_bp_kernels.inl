@@ -569,6 +569,10 @@ __device__ __forceinline__ void lds_barrier()
 #ifndef MC_ABLATE_VX
 #define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
 #endif
+#ifndef MC_VX_FUSED_RANK
+#define MC_VX_FUSED_RANK 0  // 1: every pixel's stable rank within its voxel taken in 1. (ballot groups, waves in
+                            //    order, beside the first-occurrence numbering), so 3. is a plain scatter (A/B knob)
+#endif
 #ifndef MC_VX_RECOMPUTE
 #define MC_VX_RECOMPUTE 0  // 1: no staged world points; 1. re-derives them in pixel order, 3. lists pixel
                            //    indices and 4. re-derives its points from one depth gather each (A/B knob)
@@ -710,7 +714,41 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 else s_flag = 1;
             }
             __syncthreads();
-            if (h >= 0) {
+            if (MC_VX_FUSED_RANK) {
+                // the pixel's rank within its voxel: lanes grouped by voxel, the groups' cursors advanced
+                // wave by wave (pixel order), packed with the voxel id (13 bits) for the scatter in 3.
+                int v = -1;
+                if (h >= 0) {
+                    const unsigned vv = hval[h] >> 16;
+                    if (vv < static_cast<unsigned>(kVxV)) v = static_cast<int>(vv);
+                }
+                int rank = 0, leader = 0, cnt = 0;
+                unsigned long long act = __ballot(v >= 0);
+                while (act) {
+                    const int L = __ffsll(static_cast<long long>(act)) - 1;
+                    const int vv = __shfl(v, L, 64);
+                    const unsigned long long m = __ballot(v == vv);
+                    if (v == vv) {
+                        rank = __popcll(m & ((1ull << lane) - 1ull));
+                        leader = L;
+                        cnt = __popcll(m);
+                    }
+                    act &= ~m;
+                }
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    if (wv == w && v >= 0 && lane == leader) {
+                        gb[w][lane] = vcur[v];
+                        vcur[v] += cnt;
+                    }
+                    lds_barrier();
+                }
+                if (v >= 0) {
+                    const int rk = gb[wv][leader] + rank;
+                    if (rk >= (1 << 19)) s_flag = 1;
+                    else pvid[base + k] = v | (rk << 13);
+                }
+            } else if (h >= 0) {
                 const unsigned v = hval[h] >> 16;
                 if (v < static_cast<unsigned>(kVxV)) {
                     pvid[base + k] = static_cast<int>(v);
@@ -739,9 +777,15 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
-        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the
-                                                  // LDS-only barriers below
-        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 ? 0 : n); c0 += kVxT) {
+        if (MC_VX_FUSED_RANK) {  // the ranks are known: a plain scatter
+            for (int k = t; k < (MC_ABLATE_VX == 1 ? 0 : n); k += kVxT) {
+                const int pv = pvid[base + k];
+                vlist[base + vcur[pv & 0x1FFF] + (pv >> 13)] = MC_VX_RECOMPUTE ? static_cast<int>(pl[k]) : k;
+            }
+        }
+        int vnext = (!MC_VX_FUSED_RANK && t < n) ? pvid[base + t] : -1;  // the next chunk's ids stay in
+                                                                          // flight across the LDS-only barriers
+        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 || MC_VX_FUSED_RANK ? 0 : n); c0 += kVxT) {
             const int k = c0 + t;
             const int v = vnext;
             vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
@@ -771,7 +815,9 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         sync_global();  // 4. reads the lists other waves wrote
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
         for (int v = t; v < (MC_ABLATE_VX ? 0 : nv); v += kVxT) {
-            const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
+            // (vcur = list ends after the ordered scatter, list starts after the fused ranks)
+            const int b0 = MC_VX_FUSED_RANK ? vcur[v] : (v ? vcur[v - 1] : 0);
+            const int b1 = MC_VX_FUSED_RANK ? (v + 1 < nv ? vcur[v + 1] : n) : vcur[v];
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
