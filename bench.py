@@ -134,7 +134,10 @@ def roofline_entry(w, avg_s, pmc_group=None):
     return e
 
 
-SQ_DENOISE = os.path.join(REPO, "profiles", "r03", "denoise_sq_counters_c3_v13.json")
+# the SQ counter passes of the benched build (scripts/gpu_r4final.sh); the round-3 file only as a fallback
+SQ_DENOISE = next((p for p in (os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"),
+                               os.path.join(REPO, "profiles", "r03", "denoise_sq_counters_c3_v13.json"))
+                   if os.path.exists(p)), os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"))
 SQ_DENOISE_FRAMES = 100     # the counter pass: C3 frames 600-699 (scripts/pmc_kernel.py over scripts/bp_profile.py)
 CLOCK_GHZ = 2.4             # MI355X engine clock (MI355X_MICROARCH.md)
 
@@ -146,15 +149,28 @@ def denoise_valu(frames, launches, avg_s):
     if not os.path.exists(SQ_DENOISE):
         return None
     sq = json.load(open(SQ_DENOISE))
-    insts = sum(v.get("SQ_INSTS_VALU", 0.0) for k, v in sq.items() if "denoise" in k)
+    ks = {k: v for k, v in sq.items() if "k_bp_denoise" in k or "k_bp_knn_ring" in k}
+    insts = sum(v.get("SQ_INSTS_VALU", 0.0) for v in ks.values())
     simds = 4 * _torch_cu_count()
     per_launch = insts / SQ_DENOISE_FRAMES * frames / max(launches, 1)
     frac = per_launch * 4 / (simds * CLOCK_GHZ * 1e9 * avg_s)
-    return {"bound": "valu-issue", "insts_per_launch": round(per_launch, 0), "frac": round(frac, 4),
-            "simds": simds, "clock_ghz": CLOCK_GHZ, "source": os.path.relpath(SQ_DENOISE, REPO),
-            "note": "VALU instructions of the size classes per frame from the committed SQ counter pass, x the "
-                    "launch's frames, 4 cycles per wave64 instruction; the rest of the cycles the waves wait on "
-                    "memory or barriers (SQ_WAIT_ANY 67-73 %, DESIGN.md)"}
+    out = {"bound": "valu-issue", "insts_per_launch": round(per_launch, 0), "frac": round(frac, 4),
+           "simds": simds, "clock_ghz": CLOCK_GHZ, "source": os.path.relpath(SQ_DENOISE, REPO),
+           "note": "VALU instructions of the group's kernels per frame from the committed SQ counter pass of the "
+                   "benched build, x the launch's frames, 4 cycles per wave64 instruction; the rest of the cycles "
+                   "the waves wait on memory or barriers (SQ_WAIT_ANY / SQ_WAVE_CYCLES per kernel below)"}
+    per = {}
+    for k, v in ks.items():
+        e = {}
+        if v.get("SQ_WAVE_CYCLES"):
+            e["wait_frac"] = round(v.get("SQ_WAIT_ANY", 0.0) / v["SQ_WAVE_CYCLES"], 3)
+        if v.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_bank_conflict_frac"] = round(v.get("SQ_LDS_BANK_CONFLICT", 0.0) / v["SQ_LDS_IDX_ACTIVE"], 3)
+        if e:
+            per[k.replace("mc::", "")] = e
+    if per:
+        out["per_kernel"] = per
+    return out
 
 
 def _torch_cu_count():
