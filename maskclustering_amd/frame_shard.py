@@ -119,7 +119,7 @@ def _comm_device(group, like: torch.device) -> torch.device:
 
 
 def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
-                 max_masks: int | None = None):
+                 max_masks: int | None = None, points_ready=None):
     """All-gather per-rank mask CSRs into the global one.
 
     mask_col / mask_label / mask_off: this rank's masks (numpy; mask_col relative to
@@ -133,7 +133,9 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
     Two collectives, one host read: (1) one packed int32 block per rank, [M, nnz, col[M],
     label[M], len[M]] at a fixed stride, whose copy to the host the caller needs anyway (the
     graph input's mask index is host metadata); (2) the point ids at the largest rank's nnz,
-    gathered on the device into one tensor and compacted there.
+    gathered on the device into one tensor and compacted there.  points_ready (optional) is
+    called between the two: the metadata exchange runs while mask_pts is still being written
+    (e.g. by a copy on another stream that points_ready then orders torch's stream behind).
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     out_dev = mask_pts.device
@@ -145,6 +147,8 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
     if len(off) != M + 1 or len(lab) != M or mask_pts.numel() < nnz:
         raise ValueError("inconsistent mask CSR")
     if world == 1:
+        if points_ready is not None:
+            points_ready()
         return col, lab, off.copy(), mask_pts[:nnz].clone()
     if nnz >= 2 ** 31:
         raise ValueError("a rank's mask point ids exceed the int32 block")
@@ -169,6 +173,8 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
     g_off = np.zeros(len(g_len) + 1, np.int64)
     np.cumsum(g_len, out=g_off[1:])
     nmax = max(1, int(Ns.max()))
+    if points_ready is not None:
+        points_ready()
     buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
     buf[:nnz] = mask_pts[:nnz].to(dev)
     allp = torch.empty(world * nmax, dtype=torch.int32, device=dev)
@@ -281,16 +287,34 @@ class FrameShardedScene:
                                               poses.data_ptr()))
             col, lab, off = self.ctx.bp_mask_index()
             local = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=depth.device)
+            # the copy of the point ids runs on the context's stream while the metadata block is
+            # exchanged; torch's stream (the collectives') is ordered behind it without a host wait
             self.ctx.bp_points_to_device(local.data_ptr())
-            self.ctx.synchronize()
+            ready = lambda: self._order_streams(torch_after_ctx=True, device=depth.device)
         else:  # more ranks than frames
             col, lab, off = np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64)
             local = torch.zeros(1, dtype=torch.int32, device=depth.device)
-        g_col, g_lab, g_off, self.pts = gather_masks(col, lab, off, local, self.lo, self.group, self.max_masks)
+            ready = None
+        g_col, g_lab, g_off, self.pts = gather_masks(col, lab, off, local, self.lo, self.group, self.max_masks,
+                                                     points_ready=ready)
         self.mask_index = (g_col, g_lab, g_off)
-        torch.cuda.current_stream(self.pts.device).synchronize()  # the context stream reads them next
+        # the context's stream reads the gathered ids next: ordered behind torch's stream on the device
+        self._order_streams(torch_after_ctx=False, device=self.pts.device)
         self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, pts_device_ptr=self.pts.data_ptr())
         return g_col, g_lab, g_off
+
+    def _order_streams(self, torch_after_ctx: bool, device):
+        """Device-side ordering between the context's stream and torch's current stream (an event
+        recorded on one, waited on by the other); nothing when they are the same stream."""
+        cur = torch.cuda.current_stream(device)
+        s = int(self.ctx.stream() or 0)
+        if s == int(cur.cuda_stream):
+            return
+        if s == 0:  # the context runs on the null stream: a host-side join is the safe order
+            (self.ctx.synchronize if torch_after_ctx else cur.synchronize)()
+            return
+        ext = torch.cuda.ExternalStream(s, device=device)
+        (cur.wait_stream(ext) if torch_after_ctx else ext.wait_stream(cur))
 
     def step(self, mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
              contained_threshold):
