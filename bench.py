@@ -527,10 +527,25 @@ class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic
 
 
 class FrameDataset:  # dataset/scannet.py:34-73 over arrays
-    def __init__(self, fr, frame_ids):
+    depth_scale = 1000.0  # dataset/scannet.py:21
+
+    def __init__(self, fr, frame_ids, raw_depth=True):
         self.fr, self.col = fr, {f: c for c, f in enumerate(frame_ids)}
         for x in (fr.depth, fr.seg, fr.poses):
             x.flags.writeable = False
+        if raw_depth:
+            # the depth PNGs' uint16 values (the synthetic depth is quantised to millimetres), served
+            # by the optional get_depth_raw hook (construction._raw_depth_scale); checked to decode
+            # to exactly the float32 frames get_depth returns
+            u16 = getattr(fr, "_depth_u16", None)
+            if u16 is None:
+                u16 = np.rint(fr.depth * np.float32(1000.0)).astype(np.uint16)
+                if not np.array_equal((u16 / self.depth_scale).astype(np.float32).view(np.uint32),
+                                      fr.depth.view(np.uint32)):
+                    raise ValueError("synthetic depth is not uint16 / 1000")
+                u16.flags.writeable = False
+                fr._depth_u16 = u16
+            self.get_depth_raw = lambda f: u16[self.col[f]]
 
     def get_intrinsics(self, f):
         return PinholeIntrinsic(*self.fr.intrinsics[self.col[f]])
@@ -547,13 +562,15 @@ class FrameDataset:  # dataset/scannet.py:34-73 over arrays
         return self.fr.seg[self.col[f]]
 
 
-def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=False, fr=None):
+def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=False, fr=None, raw_depth=True):
     """The reference-API boundary exactly as main.py:17-21 calls it, on the synthetic RGB-D scene
     whose dataset object serves decoded frames from host memory (dataset/scannet.py: get_depth /
     get_segmentation / get_intrinsics / get_extrinsic): one step = mask_graph_construction +
     iterative_clustering (replay=None: the default, the reference's container orders; False:
     canonical) (+ post_process's compute, without the file export).  Wall time of that Python call
-    sequence, host packing and PCIe included, per part.  Returns (record, frames)."""
+    sequence, host packing and PCIe included, per part.  raw_depth: the dataset also offers
+    get_depth_raw (uint16 frames, decoded on the device); False: float32 get_depth only.
+    Returns (record, frames)."""
     import cProfile
     import pstats
 
@@ -568,7 +585,7 @@ def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=F
         log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
     fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
     args = SimpleNamespace(debug=False, point_filter_threshold=0.5, **CFG)
-    ds = FrameDataset(fr, fids)
+    ds = FrameDataset(fr, fids, raw_depth=raw_depth)
     parts = {"graph": [], "cluster": [], "post_process": []}
 
     def step():
@@ -606,6 +623,7 @@ def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=F
     ms = 1e3 * float(np.mean(walls))
     mode = "reference" if replay is None or replay else "canonical"
     rec = {"scene_ms": round(ms, 3), "set_order": mode, "with_post_process": bool(with_pp),
+           "depth_frames": "uint16 (get_depth_raw, decoded on the device)" if raw_depth else "float32 (get_depth)",
            "part_ms": {k: round(1e3 * float(np.mean(v)), 3) for k, v in parts.items() if v and (k != "post_process"
                                                                                               or with_pp)},
            "workload": f"{shape}: synthetic RGB-D scene, {fr.num_frames} frames {fr.depth.shape[2]}x{fr.depth.shape[1]}, "
@@ -619,7 +637,7 @@ def run_api(a):
     wall time of main.py:17-21's calls, host packing and PCIe included (the device part is the
     e2e variant's S1-S6)."""
     rec, _ = api_timing(a.shape, a.seed, a.steps, a.warmup, replay=False if a.canonical else None,
-                        with_pp=a.with_pp, profile=a.profile)
+                        with_pp=a.with_pp, profile=a.profile, raw_depth=not a.f32_depth)
     ms = rec["scene_ms"]
     res = {"metric": "reference-API graph path ms per scene (main.py:17-21 through the drop-in modules)",
            "value": ms, "unit": "ms", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
@@ -810,6 +828,8 @@ def main():
     ap.add_argument("--canonical", action="store_true", help="api: iterative_clustering(replay=False), contents "
                                                              "only (the default is the reference's set orders, "
                                                              "INTEGRATION.md §4)")
+    ap.add_argument("--f32-depth", action="store_true", help="api: the dataset hands out float32 get_depth only "
+                                                             "(default: also get_depth_raw, uint16 frames)")
     ap.add_argument("--shape", default=None, help="default: c3 (g, e2e), c2 (api, pp, sweep)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -952,11 +972,14 @@ def main():
         n_api = max(3, min(args.steps, 5))
         api, fr_c2 = api_timing("c2", 0, n_api, 2, replay=None, with_pp=True)
         can, _ = api_timing("c2", 0, n_api, 2, replay=False, fr=fr_c2)
+        f32, _ = api_timing("c2", 0, n_api, 2, replay=None, fr=fr_c2, raw_depth=False)
         e2e_ms = secondary["c2_e2e"]["scene_ms"]
         api["over_device_e2e"] = round((api["scene_ms"] - api["part_ms"].get("post_process", 0.0)) / e2e_ms, 2)
         can["over_device_e2e"] = round(can["scene_ms"] / e2e_ms, 2)
+        f32["over_device_e2e"] = round(f32["scene_ms"] / e2e_ms, 2)
         secondary["c2_api"] = api
         secondary["c2_api_canonical"] = can
+        secondary["c2_api_f32_depth"] = f32
         secondary["c2_pp"] = {"scene_ms": api["part_ms"].get("post_process"),
                               "note": "post_process_objects (utils/post_process.py:180-194: DBSCAN split, point "
                                       "filter, overlap merge; host packing included) on the c2_api run's objects"}

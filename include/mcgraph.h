@@ -157,6 +157,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
 int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
                           const float *const *depth_frames, const uint8_t *const *seg_frames,
                           const double *intrinsics, const double *poses, const mc_bp_params *params);
+/* the same from the depth PNGs' raw values (depth_frames[f]: uint16 [H,W]; dataset/scannet.py:51-53,
+ * scannetpp.py:168-170, matterport.py:91-93): staged as 2 bytes per pixel instead of 4 and decoded on
+ * the device to float32(uint16 / depth_scale) computed in float64 -- the array get_depth returns.  */
+int mc_backproject_frames_raw(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                              const uint16_t *const *depth_frames, double depth_scale,
+                              const uint8_t *const *seg_frames, const double *intrinsics, const double *poses,
+                              const mc_bp_params *params);
 int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info);
 /* kept masks in frame order then id order: mask_col (frame index), mask_label
  * (id), mask_off [M+1], mask_pts = sorted unique scene ids (mask_info[id], :148) */

@@ -32,7 +32,8 @@ EXPORTED = [
     "mc_nodes_set",
     "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_level_caps", "mc_cluster_get_partition",
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
-    "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_frames", "mc_backproject_get_info",
+    "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_frames", "mc_backproject_frames_raw",
+    "mc_backproject_get_info",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
@@ -161,6 +162,7 @@ def load():
         "mc_scene_set_points": (ctypes.c_int, [vp, i64, vp, ctypes.c_int]),
         "mc_backproject": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, ctypes.c_int, P(BpParams)]),
         "mc_backproject_frames": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, P(BpParams)]),
+        "mc_backproject_frames_raw": (ctypes.c_int, [vp, i32, i32, i32, vp, ctypes.c_double, vp, vp, vp, P(BpParams)]),
         "mc_backproject_get_info": (ctypes.c_int, [vp, P(BpInfo)]),
         "mc_backproject_get_masks": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "mc_backproject_copy_points_device": (ctypes.c_int, [vp, vp]),
@@ -543,22 +545,30 @@ def _bp_methods():
         self._check(self.L.mc_backproject(self.h, F, H, W, _ptr(depth), _ptr(seg), _ptr(K), _ptr(T), 0,
                                           ctypes.byref(prm)))
 
-    def backproject_frames(self, depth_frames, seg_frames, intrinsics, poses, params: BpParams | None = None):
+    def backproject_frames(self, depth_frames, seg_frames, intrinsics, poses, params: BpParams | None = None,
+                           depth_scale=None):
         """S1 from per-frame host arrays (depth float32 [H,W], seg uint8 [H,W] each, C-contiguous),
-        staged to the device without an [F,H,W] host copy (mc_backproject_frames)."""
+        staged to the device without an [F,H,W] host copy (mc_backproject_frames).  With
+        depth_scale, the depth frames are the PNGs' uint16 values, decoded on the device
+        (mc_backproject_frames_raw)."""
         prm = params or bp_params()
         F = len(depth_frames)
         assert len(seg_frames) == F and F > 0
         H, W = depth_frames[0].shape
+        dt = np.float32 if depth_scale is None else np.uint16
         for d, sg in zip(depth_frames, seg_frames):
-            if d.shape != (H, W) or sg.shape != (H, W) or d.dtype != np.float32 or sg.dtype != np.uint8 \
+            if d.shape != (H, W) or sg.shape != (H, W) or d.dtype != dt or sg.dtype != np.uint8 \
                     or not d.flags.c_contiguous or not sg.flags.c_contiguous:
-                raise ValueError("frames must be C-contiguous float32 depth / uint8 seg arrays of one shape")
+                raise ValueError(f"frames must be C-contiguous {np.dtype(dt).name} depth / uint8 seg arrays of one shape")
         dp = (ctypes.c_void_p * F)(*[d.ctypes.data for d in depth_frames])
         sp = (ctypes.c_void_p * F)(*[sg.ctypes.data for sg in seg_frames])
         K = np.ascontiguousarray(intrinsics, np.float64).reshape(F, 4)
         T = np.ascontiguousarray(poses, np.float64).reshape(F, 16)
-        self._check(self.L.mc_backproject_frames(self.h, F, H, W, dp, sp, _ptr(K), _ptr(T), ctypes.byref(prm)))
+        if depth_scale is None:
+            self._check(self.L.mc_backproject_frames(self.h, F, H, W, dp, sp, _ptr(K), _ptr(T), ctypes.byref(prm)))
+        else:
+            self._check(self.L.mc_backproject_frames_raw(self.h, F, H, W, dp, float(depth_scale), sp, _ptr(K), _ptr(T),
+                                                         ctypes.byref(prm)))
 
     def bp_info(self) -> BpInfo:
         info = BpInfo()

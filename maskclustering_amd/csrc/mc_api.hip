@@ -119,7 +119,7 @@ struct mc_ctx {
     float grid_radius = -1.f;  // scene grid built for this ball radius
     unsigned gnb = 0;
     DevBuf d_scene, d_gcnt, d_gstart, d_gbkt, d_gcellk, d_gpts, d_gidx, d_gcell, d_gscan_tmp;
-    DevBuf d_in_depth, d_in_seg, d_in_intr, d_in_pose;
+    DevBuf d_in_depth, d_in_seg, d_in_intr, d_in_pose, d_in_raw;
     DevBuf d_band, d_present, d_fflags, d_cand, d_npix, d_csidx, d_poff, d_slot_of, d_bpstat;
     DevBuf d_bpvid;  // per-batch valid-id map (k_bp_count -> k_bp_compact), 1 byte per pixel
     DevBuf d_slot_frame, d_slot_id, d_slot_np, d_slot_pix, d_slot_nv, d_slot_m, d_slot_ns, d_slot_box, d_slot_nn,
@@ -370,7 +370,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                       &ctx->d_cap_buf, &ctx->d_cap_cnt};
     for (DevBuf *b : bufs) b->release();
     DevBuf *bp_bufs[] = {&ctx->d_scene, &ctx->d_gcnt, &ctx->d_gstart, &ctx->d_gbkt, &ctx->d_gcellk, &ctx->d_gpts,
-                         &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg,
+                         &ctx->d_gidx, &ctx->d_gcell, &ctx->d_gscan_tmp, &ctx->d_in_depth, &ctx->d_in_seg, &ctx->d_in_raw,
                          &ctx->d_in_intr, &ctx->d_in_pose, &ctx->d_band, &ctx->d_bpvid, &ctx->d_present, &ctx->d_fflags,
                          &ctx->d_cand, &ctx->d_npix, &ctx->d_csidx, &ctx->d_poff, &ctx->d_slot_of, &ctx->d_bpstat,
                          &ctx->d_slot_frame, &ctx->d_slot_id, &ctx->d_slot_np, &ctx->d_slot_pix, &ctx->d_slot_nv,
@@ -1963,6 +1963,7 @@ struct BpUpload {
     const void *const *depth;
     const void *const *seg;
     int staged;
+    double raw_scale;  // > 0: depth frames are the PNGs' uint16 values, decoded on the copy stream
 };
 
 // frames [f_lo, f_hi) (frames[f] = host pointer of frame f) -> dst + f * frame_bytes, through the
@@ -2019,11 +2020,12 @@ static void stage_frames(mc_ctx *ctx, const void *const *frames, size_t frame_by
     }
 }
 
-int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
-                          const float *const *depth_frames, const uint8_t *const *seg_frames,
-                          const double *intrinsics, const double *poses, const mc_bp_params *params)
+static int backproject_frames_impl(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                                   const void *const *depth_frames, double raw_scale, const uint8_t *const *seg_frames,
+                                   const double *intrinsics, const double *poses, const mc_bp_params *params)
 {
     const int rc = guarded(ctx, [&] {
+        MC_REQUIRE(raw_scale >= 0.0 && std::isfinite(raw_scale), MC_ERR_INVALID, "bad depth_scale");
         MC_REQUIRE(num_frames >= 0 && height > 0 && width > 0, MC_ERR_INVALID, "bad frame sizes");
         MC_REQUIRE(num_frames == 0 || (depth_frames && seg_frames && intrinsics && poses), MC_ERR_INVALID,
                    "null frame arrays");
@@ -2035,6 +2037,7 @@ int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32
         hipStream_t s = ctx->stream;
         ctx->d_in_depth.reserve(F * HW * 4);
         ctx->d_in_seg.reserve(F * HW);
+        if (raw_scale > 0.0) ctx->d_in_raw.reserve(F * HW * 2);
         ctx->d_in_intr.reserve(F * 4 * 8ull);
         ctx->d_in_pose.reserve(F * 16 * 8ull);
         MC_HIP(hipMemcpyAsync(ctx->d_in_intr.ptr, intrinsics, F * 4 * 8ull, hipMemcpyHostToDevice, s));
@@ -2052,7 +2055,7 @@ int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32
         return mc_backproject(ctx, 0, height, width, &zf, &zs, zd, zd, 0, params);
     }
     // the frames are staged by the S1 batch loop itself: batch b + 1's while batch b computes
-    BpUpload up{reinterpret_cast<const void *const *>(depth_frames), reinterpret_cast<const void *const *>(seg_frames), 0};
+    BpUpload up{depth_frames, reinterpret_cast<const void *const *>(seg_frames), 0, raw_scale};
     ctx->bp_up = &up;
     const int rc2 = mc_backproject(ctx, num_frames, height, width, ctx->d_in_depth.as<float>(),
                                    ctx->d_in_seg.as<uint8_t>(), ctx->d_in_intr.as<double>(),
@@ -2060,6 +2063,24 @@ int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32
     ctx->bp_up = nullptr;
     (void)hipStreamSynchronize(ctx->copy);  // no DMA into d_in_* outlives the call (error paths)
     return rc2;
+}
+
+int mc_backproject_frames(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                          const float *const *depth_frames, const uint8_t *const *seg_frames,
+                          const double *intrinsics, const double *poses, const mc_bp_params *params)
+{
+    return backproject_frames_impl(ctx, num_frames, height, width, reinterpret_cast<const void *const *>(depth_frames),
+                                   0.0, seg_frames, intrinsics, poses, params);
+}
+
+int mc_backproject_frames_raw(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width,
+                              const uint16_t *const *depth_frames, double depth_scale,
+                              const uint8_t *const *seg_frames, const double *intrinsics, const double *poses,
+                              const mc_bp_params *params)
+{
+    if (!(depth_scale > 0.0)) return guarded(ctx, [&] { MC_REQUIRE(false, MC_ERR_INVALID, "depth_scale must be > 0"); });
+    return backproject_frames_impl(ctx, num_frames, height, width, reinterpret_cast<const void *const *>(depth_frames),
+                                   depth_scale, seg_frames, intrinsics, poses, params);
 }
 
 int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t width, const float *depth,
@@ -2159,7 +2180,19 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // stage the host frames [up->staged, f_hi) on the copy stream
         auto upload_to = [&](int f_hi) {
             if (!up || f_hi <= up->staged) return;
-            stage_frames(ctx, up->depth, HW * 4, up->staged, f_hi, static_cast<char *>(ctx->d_in_depth.ptr), ctx->copy);
+            if (up->raw_scale > 0.0) {  // 2-byte frames, then float32(u16 / scale) on the copy stream
+                stage_frames(ctx, up->depth, HW * 2, up->staged, f_hi, static_cast<char *>(ctx->d_in_raw.ptr), ctx->copy);
+                const int64_t total = static_cast<int64_t>(f_hi - up->staged) * static_cast<int64_t>(HW);
+                hipLaunchKernelGGL(mc::k_frames_decode, grid_for(total, 256, 16384), dim3(256), 0, ctx->copy, total, H, W,
+                                   1, 1, ctx->d_in_raw.as<unsigned short>() + static_cast<size_t>(up->staged) * HW,
+                                   up->raw_scale, static_cast<const unsigned char *>(nullptr),
+                                   static_cast<const int *>(nullptr), static_cast<const int *>(nullptr),
+                                   ctx->d_in_depth.as<float>() + static_cast<size_t>(up->staged) * HW,
+                                   static_cast<unsigned char *>(nullptr));
+                MC_HIP(hipGetLastError());
+            } else {
+                stage_frames(ctx, up->depth, HW * 4, up->staged, f_hi, static_cast<char *>(ctx->d_in_depth.ptr), ctx->copy);
+            }
             stage_frames(ctx, up->seg, HW, up->staged, f_hi, static_cast<char *>(ctx->d_in_seg.ptr), ctx->copy);
             MC_HIP(hipEventRecord(ctx->ev_up, ctx->copy));
             up->staged = f_hi;

@@ -24,6 +24,8 @@ from __future__ import annotations
 
 import itertools
 
+import os
+
 import numpy as np
 
 from .. import _device
@@ -69,12 +71,32 @@ class GraphHandle:
 _current = {"token": None}
 
 
-def _read_frames(frame_list, dataset):
+def _raw_depth_scale(dataset):
+    """depth_scale when the dataset hands out its depth PNGs' raw values: an optional
+    ``get_depth_raw(frame_id)`` returning the uint16 array that the reference's datasets divide by
+    ``depth_scale`` in get_depth (dataset/scannet.py:49-54, scannetpp.py:166-171,
+    matterport.py:89-94).  The frames then cross PCIe at 2 bytes per pixel and are divided on the
+    device, bit-identical to get_depth's float32.  MASKCLUSTERING_RAW_DEPTH=0:
+    always get_depth."""
+    if os.environ.get("MASKCLUSTERING_RAW_DEPTH", "1") == "0" or not callable(getattr(dataset, "get_depth_raw", None)):
+        return None
+    scale = getattr(dataset, "depth_scale", None)
+    return float(scale) if scale is not None and float(scale) > 0 else None
+
+
+def _read_frames(frame_list, dataset, raw_scale=None):
     """the dataset calls of construction.py:47-48 / mask_backprojection.py:71-80, per frame (the
-    arrays are handed to the device as they are, no [F,H,W] host stack)"""
+    arrays are handed to the device as they are, no [F,H,W] host stack); raw_scale: the depth
+    frames are get_depth_raw's uint16 values"""
     depth, seg, K, T = [], [], [], []
     for frame_id in frame_list:
-        depth.append(np.ascontiguousarray(dataset.get_depth(frame_id), np.float32))
+        if raw_scale is not None:
+            d = np.asarray(dataset.get_depth_raw(frame_id))
+            if d.dtype != np.uint16:
+                raise TypeError("get_depth_raw must return the depth PNG's uint16 values")
+            depth.append(np.ascontiguousarray(d))
+        else:
+            depth.append(np.ascontiguousarray(dataset.get_depth(frame_id), np.float32))
         seg.append(np.ascontiguousarray(_device.seg_u8(dataset.get_segmentation(frame_id, align_with_depth=True))))
         K.append(_device.intrinsics_tuple(dataset.get_intrinsics(frame_id)))
         T.append(np.asarray(dataset.get_extrinsic(frame_id), np.float64).reshape(4, 4))
@@ -90,9 +112,10 @@ def _backproject_all(scene_points, frame_list, dataset):
         ctx.backproject(np.zeros((0, 1, 1), np.float32), np.zeros((0, 1, 1), np.uint8), np.zeros((0, 4)),
                         np.zeros((0, 4, 4)), _mb.params())
         return ctx
-    depth, seg, K, T = _read_frames(frame_list, dataset)
+    raw_scale = _raw_depth_scale(dataset)
+    depth, seg, K, T = _read_frames(frame_list, dataset, raw_scale)
     try:
-        ctx.backproject_frames(depth, seg, K, T, _mb.params())
+        ctx.backproject_frames(depth, seg, K, T, _mb.params(), depth_scale=raw_scale)
     except McError as e:
         if e.code == MC_ERR_INVALID and "depth_trunc" in str(e):
             raise IndexError(str(e)) from e

@@ -125,6 +125,24 @@ def test_backproject_frames_staged_per_batch(ctx, monkeypatch, nb):
     np.testing.assert_array_equal(sa, ctx.bp_candidates())
 
 
+@pytest.mark.parametrize("nb", ["1", "3"])
+def test_backproject_frames_raw_depth(ctx, monkeypatch, nb):
+    """mc_backproject_frames_raw (uint16 frames staged at 2 bytes per pixel, decoded on the copy
+    stream, dataset/scannet.py:51-53) == mc_backproject over the float32 frames get_depth returns."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=4)
+    u16 = np.rint(fr.depth * np.float32(1000.0)).astype(np.uint16)
+    assert np.array_equal((u16 / 1000.0).astype(np.float32).view(np.uint32), fr.depth.view(np.uint32))
+    a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    sa = ctx.bp_candidates()
+    monkeypatch.setenv("MC_BP_UPLOAD_BATCHES", nb)
+    ctx.backproject_frames([np.ascontiguousarray(d) for d in u16], [np.ascontiguousarray(s) for s in fr.seg],
+                           fr.intrinsics, fr.poses, depth_scale=1000.0)
+    for x, y in zip(a, ctx.bp_masks()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(sa, ctx.bp_candidates())
+
+
 def test_end_to_end_matches_oracle(ctx):
     """S1 on the device feeding S2-S6 on the device == the oracle's S1 feeding its S2-S6."""
     from maskclustering_amd.pipeline import GraphRun
