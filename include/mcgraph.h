@@ -365,6 +365,21 @@ int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int
                        int64_t *obj_pt_off, int32_t *obj_pts, int64_t *son_off, int32_t *son_order,
                        int32_t *labels);
 
+/* The same in two calls, so that the level-0 sets are built while the device clusters: begin takes
+ * level-0 node i's points as pts[node_start[i] .. node_start[i] + node_len[i]) (rows of the caller's
+ * mask CSR, no flattened copy) and, with async_build != 0, builds the sets on a background thread
+ * (the caller keeps node_start / node_len / pts alive until finish or free); finish waits for it and
+ * replays the iterations exactly as mc_setorder_replay (outputs as there; obj_pts holds at most
+ * sum(node_len)).  finish is called at most once; free joins and releases (also after an error). */
+typedef struct mc_setorder mc_setorder;
+int mc_setorder_begin(int32_t num_nodes, const int64_t *node_start, const int64_t *node_len, const int32_t *pts,
+                      int32_t num_threads, int async_build, mc_setorder **out);
+int mc_setorder_finish(mc_setorder *h, int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
+                       const int32_t *edge_a, const int32_t *edge_b, int32_t *num_objects, int64_t *obj_mask_off,
+                       int32_t *mask_order, int64_t *obj_pt_off, int32_t *obj_pts, int64_t *son_off,
+                       int32_t *son_order, int32_t *labels);
+void mc_setorder_free(mc_setorder *h);
+
 #ifdef __cplusplus
 }
 #endif

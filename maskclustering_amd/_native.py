@@ -39,6 +39,7 @@ EXPORTED = [
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
     "mc_shard_set", "mc_shard_pending", "mc_shard_export", "mc_shard_import",
     "mc_cluster_set_edge_capture", "mc_cluster_get_edges", "mc_openvoc_query", "mc_bits_unpack", "mc_setorder_replay",
+    "mc_setorder_begin", "mc_setorder_finish", "mc_setorder_free",
     "mc_comm_unique_id", "mc_ctx_comm_init", "mc_ctx_attach_comm",
 ]
 MC_COMM_ID_BYTES = 128
@@ -178,6 +179,9 @@ def load():
         "mc_openvoc_query": (ctypes.c_int, [vp, i32, vp, vp, i32, i32, vp, i32, vp, ctypes.c_float, vp]),
         "mc_bits_unpack": (ctypes.c_int, [vp, ctypes.c_int64, i32, i32, vp]),
         "mc_setorder_replay": (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, i32, P(i32), vp, vp, vp, vp, vp, vp, vp]),
+        "mc_setorder_begin": (ctypes.c_int, [i32, vp, vp, vp, i32, ctypes.c_int, P(vp)]),
+        "mc_setorder_finish": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, P(i32), vp, vp, vp, vp, vp, vp, vp]),
+        "mc_setorder_free": (None, [vp]),
         "mc_cluster_get_edges": (ctypes.c_int, [vp, vp, P(i64)]),
         "mc_shard_pending": (ctypes.c_int, [vp, P(i32)]),
         "mc_shard_export": (ctypes.c_int, [vp, i32, vp, P(i64)]),
@@ -239,6 +243,65 @@ def setorder_replay(level_sizes, edge_off, edge_a, edge_b, pt_off, pts, threads=
     if labels:
         out["labels"] = lab[:int(sz.sum())]
     return out
+
+
+class SetOrder:
+    """mc_setorder_begin / mc_setorder_finish: the level-0 point sets (node i: pts[node_start[i] :
+    node_start[i] + node_len[i]], added in order) built on a native background thread from
+    construction on, the iterations replayed by finish (the result of setorder_replay)."""
+
+    def __init__(self, node_start, node_len, pts, threads=0, async_build=True):
+        self.L = load()
+        st = np.ascontiguousarray(node_start, np.int64)
+        ln = np.ascontiguousarray(node_len, np.int64)
+        pp = np.ascontiguousarray(pts, np.int32)
+        if len(st) != len(ln) or (len(ln) and int((st + ln).max()) > len(pp)):
+            raise ValueError("node ranges outside pts")
+        self._keep = (st, ln, pp)  # read by the background thread until finish / close
+        self.n0, self.total = len(st), int(ln.sum())
+        h = ctypes.c_void_p()
+        rc = self.L.mc_setorder_begin(self.n0, _ptr(st), _ptr(ln), _ptr(pp), int(threads), 1 if async_build else 0,
+                                      ctypes.byref(h))
+        if rc != MC_OK:
+            raise McError(rc, "mc_setorder_begin: invalid node ranges / point ids")
+        self.h = h
+
+    def finish(self, level_sizes, edge_off, edge_a, edge_b, labels=False):
+        if not getattr(self, "h", None):
+            raise RuntimeError("SetOrder already finished")
+        T = len(level_sizes)
+        sz = np.ascontiguousarray(level_sizes, np.int32)
+        eo = np.ascontiguousarray(edge_off, np.int64)
+        ea = np.ascontiguousarray(edge_a, np.int32)
+        eb = np.ascontiguousarray(edge_b, np.int32)
+        N0, NL = int(sz[0]), int(sz[T - 1])
+        K = ctypes.c_int32()
+        mo, mord = np.zeros(NL + 1, np.int64), np.zeros(max(N0, 1), np.int32)
+        oo, opts = np.zeros(NL + 1, np.int64), np.zeros(max(self.total, 1), np.int32)
+        so, sord = np.zeros(NL + 1, np.int64), np.zeros(max(NL, 1), np.int32)
+        lab = np.zeros(max(int(sz.sum()), 1), np.int32) if labels else None
+        try:
+            rc = self.L.mc_setorder_finish(self.h, T, _ptr(sz), _ptr(eo), _ptr(ea), _ptr(eb), ctypes.byref(K), _ptr(mo),
+                                           _ptr(mord), _ptr(oo), _ptr(opts), _ptr(so), _ptr(sord), _ptr(lab))
+        finally:
+            self.close()
+        if rc != MC_OK:
+            raise McError(rc, "mc_setorder_finish: inconsistent levels / edges")
+        k = K.value
+        out = dict(mask_off=mo[:k + 1], mask_order=mord[:N0], pt_off=oo[:k + 1], pts=opts[:int(oo[k])],
+                   son_off=so[:k + 1], son_order=sord[:NL])
+        if labels:
+            out["labels"] = lab[:int(sz.sum())]
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mc_setorder_free(self.h)
+            self.h = None
+        self._keep = None
+
+    def __del__(self):
+        self.close()
 
 
 class Context:

@@ -22,10 +22,12 @@
 // re-inserts in slot order.  The reference never removes from these sets, so no table ever holds a
 // dummy.  Pinned against the running interpreter (tests/test_setorder_cpu.py: random histories and the
 // reference's own exports, tests/golden/e2e_pp_small_*).
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -267,43 +269,113 @@ class Pool {
 
 }  // namespace mcso
 
-extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
-                                  const int32_t *edge_a, const int32_t *edge_b, const int64_t *pt_off,
-                                  const int32_t *pts, int32_t num_threads, int32_t *num_objects,
-                                  int64_t *obj_mask_off, int32_t *mask_order, int64_t *obj_pt_off, int32_t *obj_pts,
-                                  int64_t *son_off, int32_t *son_order, int32_t *labels)
+// Level-0 sets built ahead (mc_setorder_begin): a background thread makes every set(ascending ids)
+// while the caller's device clustering runs; mc_setorder_finish replays the levels on them.
+struct mc_setorder {
+    int32_t n0 = 0;
+    int nth = 1;
+    std::vector<mcso::PySet> sets;
+    std::thread th;
+    int rc = MC_OK;
+    bool consumed = false;
+};
+
+namespace mcso {
+
+inline int threads_for(int32_t num_threads)
+{
+    // the caller's count, else the host's, capped by OMP_NUM_THREADS (a process's CPU share:
+    // hardware_concurrency reports the whole machine)
+    int nth = num_threads;
+    if (nth <= 0) {
+        nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        if (const char *e = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(e)));
+    }
+    return std::max(1, std::min(nth, 64));
+}
+
+inline void build_level0(mc_setorder *h, const int64_t *node_start, const int64_t *node_len, const int32_t *pts)
+{
+    try {
+        const int N0 = h->n0;
+        std::atomic<int> next{0};
+        auto work = [&]() {
+            // chunks of 64 nodes: fewer shared-counter round trips than one node at a time
+            for (int c = next.fetch_add(64); c < N0; c = next.fetch_add(64))
+                for (int i = c; i < std::min(N0, c + 64); i++) h->sets[i] = from_sequence(pts + node_start[i], node_len[i]);
+        };
+        Pool pool(h->nth);
+        pool.run(work);
+    } catch (const std::bad_alloc &) {
+        h->rc = MC_ERR_HIP;
+    }
+}
+
+}  // namespace mcso
+
+extern "C" int mc_setorder_begin(int32_t num_nodes, const int64_t *node_start, const int64_t *node_len,
+                                 const int32_t *pts, int32_t num_threads, int async_build, mc_setorder **out)
+{
+    if (!out || num_nodes < 0 || (num_nodes && (!node_start || !node_len))) return MC_ERR_INVALID;
+    *out = nullptr;
+    for (int i = 0; i < num_nodes; i++) {
+        if (node_start[i] < 0 || node_len[i] < 0 || (node_len[i] && !pts)) return MC_ERR_INVALID;
+        for (int64_t k = 0; k < node_len[i]; k++)
+            if (pts[node_start[i] + k] < 0) return MC_ERR_INVALID;
+    }
+    try {
+        auto *h = new mc_setorder;
+        h->n0 = num_nodes;
+        h->nth = mcso::threads_for(num_threads);
+        h->sets.resize(static_cast<size_t>(num_nodes));
+        if (async_build)
+            h->th = std::thread(mcso::build_level0, h, node_start, node_len, pts);
+        else
+            mcso::build_level0(h, node_start, node_len, pts);
+        *out = h;
+        return MC_OK;
+    } catch (const std::bad_alloc &) {
+        return MC_ERR_HIP;
+    } catch (const std::system_error &) {
+        return MC_ERR_HIP;
+    }
+}
+
+extern "C" void mc_setorder_free(mc_setorder *h)
+{
+    if (!h) return;
+    if (h->th.joinable()) h->th.join();
+    delete h;
+}
+
+extern "C" int mc_setorder_finish(mc_setorder *h, int32_t num_levels, const int32_t *level_sizes,
+                                  const int64_t *edge_off, const int32_t *edge_a, const int32_t *edge_b,
+                                  int32_t *num_objects, int64_t *obj_mask_off, int32_t *mask_order,
+                                  int64_t *obj_pt_off, int32_t *obj_pts, int64_t *son_off, int32_t *son_order,
+                                  int32_t *labels)
 {
     using mcso::PySet;
+    if (!h) return MC_ERR_INVALID;
+    if (h->th.joinable()) h->th.join();
+    if (h->rc != MC_OK) return h->rc;
     try {
-        if (num_levels < 1 || !level_sizes || !edge_off || !pt_off || !num_objects || !obj_mask_off || !mask_order ||
-            !obj_pt_off || !obj_pts || !son_off || !son_order)
+        if (h->consumed || num_levels < 1 || !level_sizes || !edge_off || !num_objects || !obj_mask_off ||
+            !mask_order || !obj_pt_off || !obj_pts || !son_off || !son_order)
             return MC_ERR_INVALID;
         const int T = num_levels;
         for (int t = 0; t < T; t++)
             if (level_sizes[t] < 0 || edge_off[t + 1] < edge_off[t]) return MC_ERR_INVALID;
         if (edge_off[0] != 0 || (edge_off[T] && (!edge_a || !edge_b))) return MC_ERR_INVALID;
         const int N0 = level_sizes[0];
-        if (pt_off[0] != 0) return MC_ERR_INVALID;
-        for (int i = 0; i < N0; i++)
-            if (pt_off[i + 1] < pt_off[i]) return MC_ERR_INVALID;
-        if (pt_off[N0] && !pts) return MC_ERR_INVALID;
-        for (int64_t k = 0; k < pt_off[N0]; k++)
-            if (pts[k] < 0) return MC_ERR_INVALID;
-        // threads: the caller's count, else the host's, capped by OMP_NUM_THREADS (a process's CPU share:
-        // hardware_concurrency reports the whole machine)
-        int nth = num_threads;
-        if (nth <= 0) {
-            nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-            if (const char *e = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(e)));
-        }
-        nth = std::max(1, std::min(nth, 64));
-        mcso::Pool pool(nth);
+        if (N0 != h->n0) return MC_ERR_INVALID;
+        h->consumed = true;
+        mcso::Pool pool(h->nth);
 
-        // per node of the current level: its mask order (level-0 indices) and point set; level 0's
-        // sets are made by the worker that consumes them (each is read by exactly one component)
+        // per node of the current level: its mask order (level-0 indices) and point set
         std::vector<std::vector<int32_t>> morder(N0);
         for (int i = 0; i < N0; i++) morder[i].assign(1, i);
         std::vector<PySet> sets;
+        sets.swap(h->sets);
         std::vector<int32_t> comp_off, comp_mem;  // the last level's components (member order)
         int64_t lab_base = 0;
         for (int t = 0; t < T; t++) {
@@ -343,6 +415,12 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
             for (int v = 0; v < N; v++) {
                 if (lab[v] >= 0) continue;
                 const int k = static_cast<int>(comp_off.size()) - 1;
+                if (aoff[v + 1] == aoff[v]) {  // an isolated node: {v}
+                    lab[v] = k;
+                    comp_mem.push_back(v);
+                    comp_off.push_back(static_cast<int32_t>(comp_mem.size()));
+                    continue;
+                }
                 PySet seen;
                 mcso::add(seen, v);
                 lab[v] = k;
@@ -369,7 +447,8 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
             if (labels) std::copy(lab.begin(), lab.end(), labels + lab_base);
             lab_base += N;
             const int K = static_cast<int>(comp_off.size()) - 1;
-            // create_node_from_list per component, in parallel over components
+            // create_node_from_list per component, in parallel over components; every set of this
+            // level is read by exactly one component
             std::vector<std::vector<int32_t>> nmorder(K);
             std::vector<PySet> nsets(K);
             std::atomic<int> next_k{0};
@@ -380,12 +459,7 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
                     for (int32_t j = comp_off[k]; j < comp_off[k + 1]; j++) {
                         const int32_t m = comp_mem[j];
                         mo.insert(mo.end(), morder[m].begin(), morder[m].end());
-                        if (t == 0) {
-                            acc = mcso::union_consume(std::move(acc),
-                                                      mcso::from_sequence(pts + pt_off[m], pt_off[m + 1] - pt_off[m]));
-                        } else {  // every level-t set is read by exactly one component
-                            acc = mcso::union_consume(std::move(acc), std::move(sets[m]));
-                        }
+                        acc = mcso::union_consume(std::move(acc), std::move(sets[m]));
                     }
                     nsets[k] = std::move(acc);
                 }
@@ -412,4 +486,27 @@ extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes
     } catch (const std::bad_alloc &) {
         return MC_ERR_HIP;
     }
+}
+
+extern "C" int mc_setorder_replay(int32_t num_levels, const int32_t *level_sizes, const int64_t *edge_off,
+                                  const int32_t *edge_a, const int32_t *edge_b, const int64_t *pt_off,
+                                  const int32_t *pts, int32_t num_threads, int32_t *num_objects,
+                                  int64_t *obj_mask_off, int32_t *mask_order, int64_t *obj_pt_off, int32_t *obj_pts,
+                                  int64_t *son_off, int32_t *son_order, int32_t *labels)
+{
+    if (num_levels < 1 || !level_sizes || !pt_off || level_sizes[0] < 0 || pt_off[0] != 0) return MC_ERR_INVALID;
+    const int N0 = level_sizes[0];
+    std::vector<int64_t> start(static_cast<size_t>(N0)), len(static_cast<size_t>(N0));
+    for (int i = 0; i < N0; i++) {
+        if (pt_off[i + 1] < pt_off[i]) return MC_ERR_INVALID;
+        start[i] = pt_off[i];
+        len[i] = pt_off[i + 1] - pt_off[i];
+    }
+    mc_setorder *h = nullptr;
+    int rc = mc_setorder_begin(N0, start.data(), len.data(), pts, num_threads, 0, &h);
+    if (rc != MC_OK) return rc;
+    rc = mc_setorder_finish(h, num_levels, level_sizes, edge_off, edge_a, edge_b, num_objects, obj_mask_off, mask_order,
+                            obj_pt_off, obj_pts, son_off, son_order, labels);
+    mc_setorder_free(h);
+    return rc;
 }

@@ -139,9 +139,11 @@ def _replay(nodes, T, sizes, edges, parts):
 
 
 def _level0_sequences(h):
-    """(pt_off, pts) of the level-0 nodes of device graph h: each node's point set as the reference
-    made it, set(ascending scene ids) (utils/mask_backprojection.py:147, aliased by init_nodes); None
-    when the mapping or a materialised set changed since construction (unknown history)."""
+    """(node_start, node_len, pts) of the level-0 nodes of device graph h: node i's point set as the
+    reference made it, set(ascending scene ids) (utils/mask_backprojection.py:147, aliased by
+    init_nodes), is pts[node_start[i] : node_start[i] + node_len[i]] (rows of the mask CSR, not
+    copied); None when the mapping or a materialised set changed since construction (unknown
+    history)."""
     src, node0 = h.src, h.node0
     mpc = src.mpc
     csr = getattr(mpc, "csr", None)
@@ -154,10 +156,7 @@ def _level0_sequences(h):
     for k, v in made.items():                     # a set read and changed in place by the caller
         if len(v) != off[row_of[k] + 1] - off[row_of[k]]:
             return None
-    pt_off = np.zeros(len(rows) + 1, np.int64)
-    np.cumsum(lens, out=pt_off[1:])
-    idx = np.repeat(off[rows] - pt_off[:-1], lens) + np.arange(int(pt_off[-1]), dtype=np.int64)
-    return pt_off, np.asarray(pts)[idx].astype(np.int32)
+    return off[rows], lens, np.asarray(pts)
 
 
 def _edge_levels(edges, T):
@@ -188,6 +187,8 @@ def _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, deb
         F, M = _pack(ctx, nodes)
     thr = np.array([float(t) for t in observer_num_thresholds], np.float32)
     seqs = _level0_sequences(h) if (replay and h is not None) else None
+    # the level-0 sets are built on a native background thread while the device clusters
+    sorder = _native.SetOrder(*seqs) if seqs is not None else None
     if replay:
         cap = _EDGE_CAP0
         while True:
@@ -210,10 +211,10 @@ def _iterative_clustering(nodes, observer_num_thresholds, connect_threshold, deb
     obj = ctx.objects(ci, F)
     last = ctx.partition(T - 1, int(sizes[T - 1]))
     vf = bits_to_bool(obj["vf_bits"], F)
-    if replay and seqs is not None:
-        # native restatement of the reference's container building (mc_setorder_replay)
+    if sorder is not None:
+        # native restatement of the reference's container building (mc_setorder_begin / finish)
         eo, ea, eb = _edge_levels(edges, T)
-        so = _native.setorder_replay(sizes[:T], eo, ea, eb, seqs[0], seqs[1], labels=True)
+        so = sorder.finish(sizes[:T], eo, ea, eb, labels=True)
         lab = so["labels"]
         base = 0
         for t in range(T):

@@ -172,3 +172,40 @@ def test_reference_run_orders(cfg):
                                       err_msg=f"node {k}: list(point_ids)")
         ml = [node0[i] for i in got["mask_order"][got["mask_off"][k]:got["mask_off"][k + 1]]]
         assert ";".join(f"{fids[col[m]]}_{lab[m]}" for m in ml) == str(g["node_mask_lists"][k]), f"node {k} mask_list"
+
+
+@pytest.mark.parametrize("async_build", [True, False])
+def test_begin_finish_on_csr_rows(async_build):
+    """mc_setorder_begin / finish (the level-0 sets built on a background thread, read straight from
+    rows of a CSR in any order, with rows shared by no node) == mc_setorder_replay on the flattened
+    sequences."""
+    rng = np.random.default_rng(5)
+    rows = [np.unique(rng.choice(800_000, int(rng.integers(0, 700)), replace=False)).astype(np.int32)
+            for _ in range(900)]
+    off = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum([len(r) for r in rows], out=off[1:])
+    pts = np.concatenate(rows)
+    node_rows = rng.permutation(len(rows))[:700]           # level-0 node i reads CSR row node_rows[i]
+    seqs = [rows[r] for r in node_rows]
+    levels = _levels(rng, len(seqs), 4, 0.9)
+    want = _native_run(levels, seqs)
+    so = _native.SetOrder(off[node_rows], off[node_rows + 1] - off[node_rows], pts, async_build=async_build)
+    sizes = [n for n, _ in levels]
+    eo = np.zeros(len(levels) + 1, np.int64)
+    np.cumsum([len(e) for _, e in levels], out=eo[1:])
+    ea = np.array([a for _, e in levels for a, _ in e], np.int32)
+    eb = np.array([b for _, e in levels for _, b in e], np.int32)
+    got = so.finish(sizes, eo, ea, eb, labels=True)
+    for k in want:
+        np.testing.assert_array_equal(want[k], got[k], err_msg=k)
+    with pytest.raises(RuntimeError):
+        so.finish(sizes, eo, ea, eb)
+
+
+def test_begin_rejects_bad_ranges_and_frees_unfinished():
+    with pytest.raises(ValueError):
+        _native.SetOrder([0], [5], np.arange(3, dtype=np.int32))
+    with pytest.raises(_native.McError):
+        _native.SetOrder([0], [2], np.array([1, -1], np.int32))
+    so = _native.SetOrder([0, 2], [2, 1], np.arange(3, dtype=np.int32))
+    so.close()  # never finished: the background build is joined and released
