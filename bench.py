@@ -527,10 +527,9 @@ class PinholeIntrinsic:  # the accessors of open3d.camera.PinholeCameraIntrinsic
 
 
 class FrameDataset:  # dataset/scannet.py:34-73 over arrays
-    depth_scale = 1000.0  # dataset/scannet.py:21
-
     def __init__(self, fr, frame_ids, raw_depth=True):
         self.fr, self.col = fr, {f: c for c, f in enumerate(frame_ids)}
+        self.depth_scale = float(fr.meta.get("depth_scale", 1000.0))  # dataset/scannet.py:21, matterport.py:23
         for x in (fr.depth, fr.seg, fr.poses):
             x.flags.writeable = False
         if raw_depth:
@@ -539,10 +538,10 @@ class FrameDataset:  # dataset/scannet.py:34-73 over arrays
             # to exactly the float32 frames get_depth returns
             u16 = getattr(fr, "_depth_u16", None)
             if u16 is None:
-                u16 = np.rint(fr.depth * np.float32(1000.0)).astype(np.uint16)
+                u16 = np.rint(fr.depth.astype(np.float64) * self.depth_scale).astype(np.uint16)
                 if not np.array_equal((u16 / self.depth_scale).astype(np.float32).view(np.uint32),
                                       fr.depth.view(np.uint32)):
-                    raise ValueError("synthetic depth is not uint16 / 1000")
+                    raise ValueError("synthetic depth is not uint16 / depth_scale")
                 u16.flags.writeable = False
                 fr._depth_u16 = u16
             self.get_depth_raw = lambda f: u16[self.col[f]]

@@ -4,8 +4,10 @@ A static world of boxes on a floor is rendered analytically (ray/box slabs)
 from a camera that travels along the row of boxes.  Every frame yields what the
 reference's datasets return for one frame id:
 
-* ``depth``   float32 [H,W] metres, quantised like ScanNet's uint16 / 1000
-              (``dataset/scannet.py:49-54``); floor and back wall give depth
+* ``depth``   float32 [H,W] metres, quantised like the datasets' uint16 PNGs:
+              float32(uint16 / depth_scale) computed in float64
+              (``dataset/scannet.py:49-54``: 1000; ``matterport.py:89-94``: 4000,
+              values past 65535 units read as 0); floor and back wall give depth
               but no mask;
 * ``seg``     uint8 [H,W] instance ids 1..k ascending in object order
               (``mask_predict.py:102-113``), with occasional split masks (one
@@ -57,6 +59,10 @@ FRAME_SHAPES = {
     # ~80k masks
     "c3": dict(num_objects=3100, num_frames=1500, H=1440, W=1920, length=230.0, spacing=0.025, size=(0.1, 0.3),
                frame_rng=True),
+    # Matterport3D-region-shaped (BASELINE configs[3], dataset/matterport.py:23-24): 1280x1024 frames, depth
+    # in 1/4000 m units, 2000 frames along a 300 m path, ~120k masks
+    "c4": dict(num_objects=4050, num_frames=2000, H=1024, W=1280, length=300.0, spacing=0.025, size=(0.1, 0.3),
+               frame_rng=True, depth_scale=4000.0),
 }
 
 
@@ -112,7 +118,7 @@ def _cameras(F, H, W, length, yaw):
 
 
 def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_split=0.06, p_merge=0.04,
-                device="cpu", yaw=0.12, frame_rng=False, frames=None, out="numpy"):
+                device="cpu", yaw=0.12, frame_rng=False, frames=None, out="numpy", depth_scale=1000.0):
     """Render the scene.  frames: the frame indices to render (default all; the scene points,
     intrinsics and poses always cover every frame).  frame_rng: the split / merge noise of frame f
     is drawn from its own generator (seed, f), so that any frame slice renders the same frames as
@@ -171,9 +177,11 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
             use_obj = best_t < bg
             t = torch.where(use_obj, best_t, bg).reshape(H, W)
             obj = torch.where(use_obj, best_o, torch.full_like(best_o, -1)).reshape(H, W)
-            # depth quantised like ScanNet's uint16 millimetres (round half to even, as numpy)
-            dq = torch.where(torch.isfinite(t) & (t < 60.0), torch.round(t * 1000.0), torch.zeros_like(t))
-            dz = dq.to(torch.int32).to(torch.float32) / np.float32(1000.0)
+            # depth quantised like the uint16 PNGs (round half to even, as numpy), decoded as the datasets
+            # do: float32(u16 / depth_scale) in float64 (for 1000 the same bits as a float32 division)
+            dq = torch.where(torch.isfinite(t) & (t < 60.0), torch.round(t * depth_scale), torch.zeros_like(t))
+            dq = torch.where(dq <= 65535.0, dq, torch.zeros_like(dq))
+            dz = (dq / float(depth_scale)).to(torch.float32)
             # per-frame instance ids: visible objects in object order, with split / merge noise
             vis = torch.unique(obj[obj >= 0]).cpu().numpy()
             r = np.random.default_rng([seed, f]) if frame_rng else rng
@@ -207,7 +215,7 @@ def make_frames(num_objects, num_frames, H, W, length, spacing, size, seed=0, p_
             seg[i] = s_.cpu().numpy()
     return SceneFrames(scene, depth, seg, intr[sel], poses[sel],
                        meta=dict(seed=seed, num_objects=K, length=length, spacing=spacing, frames=sel,
-                                 num_frames_total=F))
+                                 num_frames_total=F, depth_scale=float(depth_scale)))
 
 
 def make_frames_shape(name: str, seed: int = 0, device: str = "cpu", **kw) -> SceneFrames:

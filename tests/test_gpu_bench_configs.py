@@ -9,6 +9,9 @@ the C-ABI against the CPU oracle, bit for bit:
 * ``c3_e2e``: the full C3 scene as the bench runs it (1500 frames resident in HBM, S1 -> S6): every
   frame's S1 against the oracle's, then S2-S6 against the sparse oracle (oracle/graph_sparse.c) on
   that mask set.
+* ``c4``: the Matterport-region-shaped scene (BASELINE configs[3]: 2000 frames of 1280x1024, depth in
+  1/4000 m units, ~120k masks): three 16-frame windows' S1 against the oracle, then the whole scene
+  S1 -> S6 on the device with S2-S6 against the sparse oracle on the device's mask set.
 
 The oracle is pinned to the reference's own outputs by tests/test_s1_oracle.py and
 tests/test_oracle_golden.py; the Open3D / pytorch3d arithmetic inside S1 is parity unpinned
@@ -122,6 +125,75 @@ def test_c3_e2e_matches_oracle():
     del fr
     torch.cuda.empty_cache()
     assert len(col) > 70_000
+    run.P, run.F = len(t_scene), F
+    run.mask_col, run.mask_label = col, lab
+    ctx.use_backprojection()
+    run.step(**CFG)
+    got = run.canonical(dense=False)
+    want = oracle.run_sparse(len(t_scene), F, col.astype(np.int32), lab.astype(np.int32), np.asarray(off, np.int64),
+                             np.asarray(pts, np.int32), **CFG)
+    for k in ["gl_col", "gl_label", "boundary", "vf_bits", "c_row", "c_col", "undersegment", "node0_g", "thr_value",
+              "thr_is_int", "num_iters", "level_sizes", "edge_counts", "obj_mask_off", "obj_mask_idx", "obj_pt_off",
+              "obj_pt_idx", "obj_vf_bits", "obj_c_off", "obj_c_idx", "obj_node_info"]:
+        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=k)
+    for t in range(int(want["num_iters"])):
+        np.testing.assert_array_equal(got[f"part_{t}"], want[f"part_{t}"], err_msg=f"partition {t}")
+
+
+def _c4_frames_window():
+    from maskclustering_amd.synthetic_frames import FRAME_SHAPES
+    F = FRAME_SHAPES["c4"]["num_frames"]
+    return [*range(0, 16), *range(F // 2 - 8, F // 2 + 8), *range(F - 16, F)]
+
+
+def test_c4_s1_windows_match_oracle():
+    from maskclustering_amd import _native
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    frames = _c4_frames_window()
+    fr = make_frames_shape("c4", seed=0, device="cuda:0", frames=frames)
+    assert fr.depth.shape == (48, 1024, 1280)
+    scene = fr.scene_points.astype(np.float32)
+    ctx = _native.Context(0)
+    ctx.set_points(scene)
+    ctx.backproject(fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    s1 = oracle.s1_frames(scene, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    _compare_s1(ctx.bp_masks(), ctx.bp_candidates(), s1, frames)
+
+
+def test_c4_e2e_matches_oracle():
+    """the whole C4 scene S1 -> S6 on the device (frames resident in HBM); the device's S1 of the
+    windows is checked above, S2-S6 here against the sparse oracle on the device's mask set"""
+    import torch
+    from maskclustering_amd import _native
+    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("c4", seed=0, device="cuda:0", out="torch")
+    dev = torch.device("cuda", 0)
+    t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
+    t_K = torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev)
+    t_T = torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)
+    run = GraphRun(0)
+    ctx = run.ctx
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)
+    F, H, W = fr.depth.shape
+    ctx.backproject(None, None, None, None, _native.bp_params(), shape=(F, H, W),
+                    device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), t_K.data_ptr(), t_T.data_ptr()))
+    col, lab, off, pts = ctx.bp_masks()
+    # the windows' masks equal a run over the windows alone (S1 is per frame)
+    win = _c4_frames_window()
+    sub = _native.Context(0)
+    sub.set_points(fr.scene_points.astype(np.float32))
+    idx = torch.as_tensor(win, device=dev)
+    sub.backproject(fr.depth[idx].cpu().numpy(), fr.seg[idx].cpu().numpy(), fr.intrinsics[win], fr.poses[win])
+    scol, slab, soff, spts = sub.bp_masks()
+    rows = np.nonzero(np.isin(col, win))[0]
+    np.testing.assert_array_equal(np.asarray(win)[scol], col[rows])
+    np.testing.assert_array_equal(slab, lab[rows])
+    np.testing.assert_array_equal(np.concatenate([pts[off[r]:off[r + 1]] for r in rows]), spts)
+    del fr, sub
+    torch.cuda.empty_cache()
+    assert len(col) > 100_000
     run.P, run.F = len(t_scene), F
     run.mask_col, run.mask_label = col, lab
     ctx.use_backprojection()
