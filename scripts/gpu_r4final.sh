@@ -10,7 +10,7 @@ OUT=${OUT:-gpurun_out/r4final}
 mkdir -p "$OUT"
 run() { echo "== $* $(date +%T)" >&2; "$@"; local rc=$?; echo "rc=$rc" >&2; return $rc; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  run timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+  run timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
       --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -2 "$OUT/pytest_gpu.log"
   run timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
