@@ -745,7 +745,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 }
                 if (v >= 0) {
                     const int rk = gb[wv][leader] + rank;
-                    if (rk >= (1 << 19)) s_flag = 1;
+                    if (rk >= (1 << 18)) s_flag = 1;  // v | rk << 13 stays a non-negative int
                     else pvid[base + k] = v | (rk << 13);
                 }
             } else if (h >= 0) {
