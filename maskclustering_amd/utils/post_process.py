@@ -75,6 +75,11 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
     unique_frames = len(fcol) == F
 
     lazy = csr is not None and hasattr(mask_point_clouds, "is_materialized")
+    # no set of the mapping made yet (the drop-in construction's lazy mapping, untouched): every key
+    # is served by its CSR row, looked up directly (KeyError for a missing key, as at :70)
+    direct = lazy and dict.__len__(mask_point_clouds) == 0
+    row_of = csr[0] if direct else None
+    q_rows = []
 
     def add(key):
         if lazy and not mask_point_clouds.is_materialized(key):  # the CSR row serves it: no set made
@@ -92,10 +97,13 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
         cols = np.array([fcol.get(f, -1) for f, _ in ml], np.int64) if unique_frames else None
         if cols is not None and (cols >= 0).all() and vf[cols].all():
             keys = [f"{f}_{m}" for f, m in ml]
-            for key in keys:
-                if key not in table:
-                    add(key)
-            q_mask.extend([table[k] for k in keys])
+            if direct:
+                q_rows.extend([row_of[k] for k in keys])
+            else:
+                for key in keys:
+                    if key not in table:
+                        add(key)
+                q_mask.extend([table[k] for k in keys])
             q_col.extend(cols.tolist())
             q_key.extend(ml)
         else:                                                     # per mask, in the reference's order
@@ -108,9 +116,12 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
                 if c is None:                                     # :69
                     raise IndexError("index 0 is out of bounds for axis 0 with size 0")
                 key = f"{f}_{m}"
-                if key not in table:
-                    add(key)
-                q_mask.append(table[key])
+                if direct:
+                    q_rows.append(row_of[key])
+                else:
+                    if key not in table:
+                        add(key)
+                    q_mask.append(table[key])
                 q_col.append(c)
                 q_key.append((f, m))
         vf_rows.append(vf)
@@ -122,23 +133,27 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
     pfm = getattr(point_frame_matrix, "_mc_bits", None)           # construction's packed words
     if pfm is None or point_frame_matrix.flags.writeable or point_frame_matrix.shape[1] != F:
         pfm = _bits(_host(point_frame_matrix), F)
-    if csr is not None:      # the construction's rows: table entry -> CSR row, no set is re-read
-        rows = np.fromiter((csr[0][k] for k in table), np.int64, count=len(table))
-        clen = np.diff(csr[1])[rows]
-        lens = np.fromiter((len(p) if p is not None else -1 for p in mask_arrays), np.int64, count=len(mask_arrays))
-        lens = np.where(lens < 0, clen, lens)
-        if not np.array_equal(clen, lens):                        # a set changed in place
-            csr = None
-            mask_arrays = [p if p is not None else mask_point_clouds[k] for k, p in zip(table, mask_arrays)]
-    if csr is not None:
-        q_dev = rows[np.asarray(q_mask, np.int64)]
+    if direct:
+        q_dev = np.asarray(q_rows, np.int64)
         mask_off, mask_pts = csr[1], csr[2]
     else:
-        q_dev = np.asarray(q_mask, np.int64)
-        arrs = [np.fromiter(p, np.int64, count=len(p)) for p in mask_arrays]
-        mask_off = np.zeros(len(arrs) + 1, np.int64)
-        np.cumsum([len(a) for a in arrs], out=mask_off[1:])
-        mask_pts = np.concatenate(arrs) if arrs else np.zeros(0, np.int64)
+        if csr is not None:  # the construction's rows: table entry -> CSR row, no set is re-read
+            rows = np.fromiter((csr[0][k] for k in table), np.int64, count=len(table))
+            clen = np.diff(csr[1])[rows]
+            lens = np.fromiter((len(p) if p is not None else -1 for p in mask_arrays), np.int64, count=len(mask_arrays))
+            lens = np.where(lens < 0, clen, lens)
+            if not np.array_equal(clen, lens):                    # a set changed in place
+                csr = None
+                mask_arrays = [p if p is not None else mask_point_clouds[k] for k, p in zip(table, mask_arrays)]
+        if csr is not None:
+            q_dev = rows[np.asarray(q_mask, np.int64)]
+            mask_off, mask_pts = csr[1], csr[2]
+        else:
+            q_dev = np.asarray(q_mask, np.int64)
+            arrs = [np.fromiter(p, np.int64, count=len(p)) for p in mask_arrays]
+            mask_off = np.zeros(len(arrs) + 1, np.int64)
+            np.cumsum([len(a) for a in arrs], out=mask_off[1:])
+            mask_pts = np.concatenate(arrs) if arrs else np.zeros(0, np.int64)
     pt_off = np.zeros(len(nodes) + 1, np.int64)
     np.cumsum([len(o) for o in orders], out=pt_off[1:])
     q_off = np.zeros(len(nodes) + 1, np.int64)
