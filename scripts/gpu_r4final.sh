@@ -17,11 +17,13 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
       || { tail -20 "$OUT/smoke.log"; exit 1; }
   tail -1 "$OUT/smoke.log"
 fi
-run timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
-cat "$OUT/bench.json"
-run timeout -k 10 300 python bench.py --shape c4 --steps 5 --warmup 1 --no-cpu-baseline --no-secondary \
-    > "$OUT/bench_e2e_c4.json" 2> "$OUT/bench_e2e_c4.err" || { tail -20 "$OUT/bench_e2e_c4.err"; exit 1; }
-cat "$OUT/bench_e2e_c4.json"
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  run timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+  cat "$OUT/bench.json"
+  run timeout -k 10 300 python bench.py --shape c4 --steps 5 --warmup 1 --no-cpu-baseline --no-secondary \
+      > "$OUT/bench_e2e_c4.json" 2> "$OUT/bench_e2e_c4.err" || { tail -20 "$OUT/bench_e2e_c4.err"; exit 1; }
+  cat "$OUT/bench_e2e_c4.json"
+fi
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 RAW=/tmp/mc_raw_$$
 mkdir -p "$RAW"
