@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# Round 4, call c: where the time goes after the denoise split.  Per-phase stamps of the class
+# kernels (libmcgraph_stamps.so, C3 frames 600-699), and the reference-API C2 path under cProfile
+# (reference orders with post_process, then canonical) to split its host time.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${OUT:-gpurun_out/r4c}
+mkdir -p "$OUT"
+step() { local name=$1; shift; echo "== $name $(date +%T)"; timeout -k 10 "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" \
+    || { echo "$name failed"; tail -30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }; tail -3 "$OUT/$name.out"; }
+export MCGRAPH_LIB_PARTIAL=1
+step stamps_c3 300 env MCGRAPH_LIB=$PWD/maskclustering_amd/libmcgraph_stamps.so python -u scripts/bp_stamps.py c3 600 100
+step api_c2_prof 300 python -u bench.py --variant api --shape c2 --steps 5 --warmup 2 --with-pp --profile
+step api_c2_canonical_prof 300 python -u bench.py --variant api --shape c2 --steps 5 --warmup 2 --canonical --profile
