@@ -12,3 +12,8 @@ export MCGRAPH_LIB_PARTIAL=1
 step stamps_c3 300 env MCGRAPH_LIB=$PWD/maskclustering_amd/libmcgraph_stamps.so python -u scripts/bp_stamps.py c3 600 100
 step api_c2_prof 300 python -u bench.py --variant api --shape c2 --steps 5 --warmup 2 --with-pp --profile
 step api_c2_canonical_prof 300 python -u bench.py --variant api --shape c2 --steps 5 --warmup 2 --canonical --profile
+# voxel phase shares of the current kernel (timing-only ablations: 1 = no phases 3-4, 2 = no phase 4)
+L=maskclustering_amd
+OUT=$OUT/ab_vx SHAPES="c3:600:100" REPS=2 \
+    LIBS="$L/libmcgraph.so $L/libmcgraph_vxab1.so $L/libmcgraph_vxab2.so $L/libmcgraph_vxfr.so" \
+    timeout -k 10 300 bash scripts/gpu_ab_s1.sh || { echo "A/B failed"; exit 1; }
