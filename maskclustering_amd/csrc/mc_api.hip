@@ -1754,8 +1754,8 @@ enum BpStat : int {
     BS_TK = BS_CLS + mc::kBpClasses + 1,  // ticket counters of the LDS classes
     BS_VXFB = BS_TK + mc::kBpClasses,     // slots the first voxel tier hands to the second
     BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
-    BS_DQ,                                // points queued for the k-NN ring search
-    BS_COUNT
+    BS_DQ,                                // points queued for the k-NN ring search (one counter per class)
+    BS_COUNT = BS_DQ + mc::kBpClasses
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
@@ -1892,18 +1892,53 @@ constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 
 // one LDS size class of the denoise: as many workgroups as are resident at once, each taking the
 // class's slots from a ticket counter
+// The k-NN ring search (k_bp_knn_ring) and the statistics / survivors (k_bp_denoise_tail) of the LDS
+// classes: by default each class's own, queued on its stream right after its class kernel, so that they
+// run while the other classes still compute (one queue region of px / kBpClasses entries per class; a
+// slot that finds its class's region full takes the whole-cloud scan in the class kernel instead);
+// MC_BP_TAIL_JOINED=1: one queue for every class and both kernels once after the join.
+static bool bp_tail_per_class()
+{
+    const char *e = getenv("MC_BP_TAIL_JOINED");  // read per call (the tests switch it)
+    return !(e && atoi(e) != 0);
+}
+inline size_t bp_dq_region(const mc_ctx *ctx)
+{
+    size_t r = bp_tail_per_class() ? ctx->bp_px_cap / mc::kBpClasses : ctx->bp_px_cap;
+    if (const char *e = getenv("MC_BP_DQ_CAP")) r = std::min<size_t>(r, strtoull(e, nullptr, 10));  // test knob
+    return std::min<size_t>(r, INT_MAX);
+}
+
+void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int cls_lo, int cls_hi, int ncap, int *st, const mc::BpDev &dv)
+{
+    const size_t off = bp_tail_per_class() ? bp_dq_region(ctx) * cls_lo : 0;
+    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ + (bp_tail_per_class() ? cls_lo : 0),
+                       ctx->d_vx_pvid.as<int>() + off, ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
+                       ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>() + off, ctx->d_slot_grid.as<double>(),
+                       ctx->d_avg.as<double>(), static_cast<int>(bp_dq_region(ctx)));
+    hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * (bp_tail_per_class() ? 2 : 4)), dim3(256), 0, s,
+                       st + BS_CLS, ctx->d_cls_list.as<int>(), ncap, cls_lo, cls_hi, ctx->d_slot_pix.as<int>(),
+                       ctx->d_slot_m.as<int>(), dv, ctx->d_vpts.as<double>(), ctx->d_avg.as<double>(),
+                       ctx->d_ssidx.as<int>(), ctx->d_qpts.as<float>(), ctx->d_slot_ns.as<int>(),
+                       ctx->d_slot_box.as<float>());
+}
+
 template <int N>
 void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, const mc::BpDev &dv)
 {
     using C = mc::BpLdsClass<N>;
+    const bool own = bp_tail_per_class();
+    const size_t off = own ? bp_dq_region(ctx) * cls : 0;
     // the classes run concurrently: each has its own region of per-workgroup neighbour lists
     hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * kBpOversub), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
                        ctx->d_slot_m.as<int>(), ctx->d_avg.as<double>(), ctx->d_ssidx.as<int>(),
-                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
-                       ctx->d_vx_pvid.as<int>(), st + BS_DQ, ctx->d_slot_grid.as<double>());
+                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>() + off,
+                       ctx->d_vx_pvid.as<int>() + off, st + BS_DQ + (own ? cls : 0),
+                       static_cast<int>(bp_dq_region(ctx)), ctx->d_slot_grid.as<double>());
+    if (own) bp_denoise_tail_launch(ctx, s, cls, cls + 1, ncap, st, dv);
 }
 // MC_BP_DEBUG_SYNC=1: synchronise and report after every S1 group (diagnostics of a stalled batch)
 void bp_debug_sync(hipStream_t s, const char *what)
@@ -2364,15 +2399,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                     MC_HIP(hipStreamWaitEvent(s, ctx->ev_cls[c], 0));
                 }
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
-                // the deferred points' ring search, then every LDS-class slot's statistics and survivors
-                hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ,
-                                   ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
-                                   ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_slot_grid.as<double>(),
-                                   ctx->d_avg.as<double>());
-                hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * 4), dim3(256), 0, s, st + BS_CLS,
-                                   ctx->d_cls_list.as<int>(), ncap, ctx->d_slot_pix.as<int>(), ctx->d_slot_m.as<int>(),
-                                   dv, ctx->d_vpts.as<double>(), ctx->d_avg.as<double>(), ctx->d_ssidx.as<int>(),
-                                   ctx->d_qpts.as<float>(), ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>());
+                // (MC_BP_TAIL_JOINED) the deferred points' ring search, then every LDS-class slot's
+                // statistics and survivors, once after the join
+                if (!bp_tail_per_class()) bp_denoise_tail_launch(ctx, s, 0, mc::kBpClasses, ncap, st, dv);
                 bp_debug_sync(s, "bp_denoise");
             }
             {

@@ -1738,7 +1738,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
     unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, int *__restrict__ slot_m, double *__restrict__ gavg,
     int *__restrict__ gsx, double4 *__restrict__ grec, int *__restrict__ gbs, int *__restrict__ gitem,
-    int *__restrict__ dq, int *__restrict__ dq_cnt, double *__restrict__ slot_grid)
+    int *__restrict__ dq, int *__restrict__ dq_cnt, int dq_cap, double *__restrict__ slot_grid)
 {
     constexpr int T = BpLdsClass<N>::T;
     constexpr int NW = T / 64;
@@ -2166,13 +2166,31 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         // position | rank << 14; at most one entry per voxel of the batch, so a pixel-sized array holds it)
         const int nd = s_ndef;
         if (nd > 0) {
+            if (t == 0) s_slot = atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
+            bar();
+            const int e0 = s_slot;
+            if (e0 + nd > dq_cap) {  // the queue region is full (not seen in practice): this slot's
+                                     // deferred points take the whole-cloud scan here, a wave per point;
+                                     // its entries inside the region are marked empty for k_bp_knn_ring
+                for (int f = e0 + t; f < dq_cap; f += T) dq[f] = -1;
+                for (int f = wv; f < nd; f += NW) {
+                    const int q = sring[f];
+                    const double4 a = spt[q];
+                    const double mean = wave_knn_mean(m, kk, [&](int j) {
+                        const double4 p = spt[spos[sX[j]]];
+                        const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                        return ((ex * ex) + (ey * ey)) + (ez * ez);
+                    });
+                    if (lane == 0) mavg[spar[q]] = mean;
+                }
+                if (t == 0) slot_m[s] = m;
+                bar();
+                continue;
+            }
             double4 *gr = grec + base;
             for (int i = t; i < n; i += T) gr[i] = spt[i];
             int *gb = gbs + 2 * static_cast<size_t>(base) + s;
             for (int b = t; b <= NBK * n; b += T) gb[b] = sA[b];
-            if (t == 0) s_slot = atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
-            bar();
-            const int e0 = s_slot;
             for (int f = t; f < nd; f += T) {
                 const int q = sring[f];
                 dq[e0 + f] = s;
@@ -2205,11 +2223,12 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                                                      const int *__restrict__ slot_pix, BpDev pr,
                                                      const double4 *__restrict__ grec, const int *__restrict__ gbs,
                                                      const int *__restrict__ gitem, const double *__restrict__ slot_grid,
-                                                     double *__restrict__ gavg)
+                                                     double *__restrict__ gavg, int dq_cap)
 {
-    const int ne = *dq_cnt;
+    const int ne = min(*dq_cnt, dq_cap);  // (the counter runs past the region when a slot found it full)
     for (int f = blockIdx.x * 256 + threadIdx.x; f < ne; f += gridDim.x * 256) {
         const int s = dq[f];
+        if (s < 0) continue;  // an entry of a slot that took the in-kernel scan
         const int base = slot_pix[s];
         const double *gm = slot_grid + 8 * static_cast<size_t>(s);
         const double mn[3] = {gm[0], gm[1], gm[2]};
@@ -2278,7 +2297,7 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
 // in index order (std::accumulate: 64 values read at once, then added in order as scalars), the
 // survivors 0 < d < mean + std_ratio * std in index order -> float32 mask points and their AABB.
 __global__ __launch_bounds__(256) void k_bp_denoise_tail(const int *__restrict__ cls_cnt, const int *__restrict__ cls_list,
-                                                         int cap, const int *__restrict__ slot_pix,
+                                                         int cap, int cls_lo, int cls_hi, const int *__restrict__ slot_pix,
                                                          const int *__restrict__ slot_m, BpDev pr,
                                                          const double *__restrict__ vpts, const double *__restrict__ gavg,
                                                          const int *__restrict__ gsx, float *__restrict__ qpts,
@@ -2288,7 +2307,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise_tail(const int *__restrict__
     int total = 0;
 #pragma unroll
     for (int c = 0; c < kBpClasses; c++) {
-        cnt[c] = cls_cnt[c];
+        cnt[c] = c >= cls_lo && c < cls_hi ? cls_cnt[c] : 0;  // classes [cls_lo, cls_hi)
         total += cnt[c];
     }
     const int lane = lane_id();

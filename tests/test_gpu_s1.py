@@ -267,6 +267,26 @@ def test_list_overflow_paths_agree(ctx, monkeypatch, nbcap):
             monkeypatch.delenv("MC_BP_MIN_CLASS")
 
 
+@pytest.mark.parametrize("env", [("MC_BP_TAIL_JOINED", "1"), ("MC_BP_DQ_CAP", "0"), ("MC_BP_DQ_CAP", "5")])
+def test_ring_queue_modes_agree(ctx, monkeypatch, env):
+    """The k-NN ring-search queue: per class (default; each class's ring search and statistics queued
+    behind its class kernel), one joined queue (MC_BP_TAIL_JOINED=1), and a region too small for the
+    deferred points (MC_BP_DQ_CAP: slots that find it full take the whole-cloud scan inside the class
+    kernel, their region entries marked empty) give the same masks, in every size class."""
+    for inp in _dense_inputs():
+        want = _run(ctx, *inp)
+        sa = ctx.bp_candidates()
+        for min_cls in ("0", "2", "5"):
+            monkeypatch.setenv(*env)
+            monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
+            got = _run(ctx, *inp)
+            np.testing.assert_array_equal(sa, ctx.bp_candidates(), err_msg=f"{env} class {min_cls}")
+            for x, y in zip(want, got):
+                np.testing.assert_array_equal(x, y)
+            monkeypatch.delenv(env[0])
+            monkeypatch.delenv("MC_BP_MIN_CLASS")
+
+
 def test_repeated_runs_identical(ctx):
     """Run-to-run determinism of the concurrent size classes (their lists are built with LDS-atomic
     slots, so any read of a slot before its store lands would vary between runs): the dense inputs
