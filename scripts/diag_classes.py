@@ -1,0 +1,41 @@
+"""Diagnostic: run the tiny dense S1 scene of test_denoise_size_classes_agree under every
+MC_BP_MIN_CLASS and both denoise tail modes (per class / joined), REPS times each, and print every
+candidate-statistics element that differs from the first run (slot, column, values)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from maskclustering_amd import _native  # noqa: E402
+from maskclustering_amd.synthetic_frames import make_frames_shape  # noqa: E402
+
+REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+COLS = ["frame", "id", "npix", "nvox", "ndbscan", "nsor", "ncand", "ncovered", "nneighbors", "kept"]
+fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
+ctx = _native.Context(0)
+ctx.set_points(fr.scene_points.astype(np.float32))
+
+
+def run():
+    ctx.backproject(fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    return ctx.bp_candidates().copy()
+
+
+os.environ.pop("MC_BP_MIN_CLASS", None)
+os.environ.pop("MC_BP_TAIL_JOINED", None)
+ref = run()
+bad = 0
+for joined in ("0", "1"):
+    os.environ["MC_BP_TAIL_JOINED"] = joined
+    for mc in ("0", "1", "2", "3", "4", "5", "6"):
+        os.environ["MC_BP_MIN_CLASS"] = mc
+        for r in range(REPS):
+            got = run()
+            d = np.argwhere(got != ref)
+            if len(d):
+                bad += 1
+                print(f"joined={joined} min_class={mc} rep={r}: " + "; ".join(
+                    f"slot {i} (frame {ref[i, 0]} id {ref[i, 1]} nvox {ref[i, 3]}) {COLS[j]} {ref[i, j]} -> {got[i, j]}"
+                    for i, j in d[:8]), flush=True)
+print("differing runs", bad, "of", 2 * 7 * REPS, flush=True)
