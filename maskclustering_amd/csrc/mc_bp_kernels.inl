@@ -1596,6 +1596,15 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
 #endif
 __device__ unsigned long long g_bp_dbg[8];
 __device__ unsigned g_bp_dbg_printed;
+// (diagnostics build) which step produced each kept point's k-NN mean, by batch pixel index base + rank:
+// 1 list pass, 2 whole cloud (m < k), 3 whole cloud (queue region full), 4 ring-search kernel; the
+// list pass also records the class size N and the list count
+constexpr int kBpDbgPath = MC_DBG_CHECK ? (1 << 24) : 1;
+__device__ unsigned g_bp_dbg_path[kBpDbgPath];
+__device__ __forceinline__ void bp_dbg_path(size_t i, unsigned code)
+{
+    if (MC_DBG_CHECK && i < static_cast<size_t>(kBpDbgPath)) g_bp_dbg_path[i] = code;
+}
 __device__ __forceinline__ bool bp_dbg_fail(int kind)
 {
     atomicAdd(&g_bp_dbg[kind], 1ull);
@@ -1662,7 +1671,8 @@ __device__ __noinline__ void bp_dbg_union(const BpLdsGrid &g, const int *spar, i
     sync_global();
 }
 // (in k_bp_denoise_tail, a wave per slot) kept point of rank r: original index sx[r], mean av[r]
-__device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, const double *av, int m, int kk, int slot)
+__device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, const double *av, int m, int kk, int slot,
+                                             int base)
 {
     for (int r = lane_id(); r < m; r += 64) {
         const double *a = P + 3 * sx[r];
@@ -1677,7 +1687,12 @@ __device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, con
         for (int k = 0; k < kk; k++) sum = sum + sqrt(best[k]);
         const double want = sum / static_cast<double>(kk), got = av[r];
         if (__double_as_longlong(want) != __double_as_longlong(got))
-            if (bp_dbg_fail(3)) printf("[bp dbg] slot=%d m=%d r=%d: k-NN mean %.17g, brute force %.17g\n", slot, m, r, got, want);
+            if (bp_dbg_fail(3)) {
+                const size_t gi = static_cast<size_t>(base) + r;
+                const unsigned pc = gi < static_cast<size_t>(kBpDbgPath) ? g_bp_dbg_path[gi] : 0u;
+                printf("[bp dbg] slot=%d m=%d r=%d: k-NN mean %.17g, brute force %.17g (path %u, class N %u, list count %u)\n",
+                       slot, m, r, got, want, pc & 0xFu, (pc >> 4) & 0xFFFFu, pc >> 20);
+            }
     }
 }
 
@@ -2143,6 +2158,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
             mavg[r] = sum / static_cast<double>(kk);
+            bp_dbg_path(static_cast<size_t>(base) + r, 1u | (static_cast<unsigned>(N) << 4) | (static_cast<unsigned>(cnt) << 20));
         }
         bar();
         BP_STAMP(34);  // k-NN: the list pass
@@ -2159,7 +2175,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
                 return ((ex * ex) + (ey * ey)) + (ez * ez);
             });
-            if (lane == 0) mavg[r] = mean;
+            if (lane == 0) {
+                mavg[r] = mean;
+                bp_dbg_path(static_cast<size_t>(base) + r, 2u | (static_cast<unsigned>(N) << 4));
+            }
         }
         // the deferred points: the slot's grid (cell-sorted records with kept bits, bucket starts,
         // origin and extent) to its own ranges, its points to the batch's ring-search queue (slot,
@@ -2181,7 +2200,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
                         return ((ex * ex) + (ey * ey)) + (ez * ez);
                     });
-                    if (lane == 0) mavg[spar[q]] = mean;
+                    if (lane == 0) {
+                        mavg[spar[q]] = mean;
+                        bp_dbg_path(static_cast<size_t>(base) + spar[q], 3u | (static_cast<unsigned>(N) << 4));
+                    }
                 }
                 if (t == 0) slot_m[s] = m;
                 bar();
@@ -2288,6 +2310,8 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
             gavg[base + r] = sum / static_cast<double>(kBpKnnMax);
+            bp_dbg_path(static_cast<size_t>(base) + r, 4u | (static_cast<unsigned>(found > 0xFFFF ? 0xFFFF : found) << 4) |
+                                                         (static_cast<unsigned>(done ? 1 : 0) << 20));
         }
     }
 }
@@ -2319,7 +2343,7 @@ __global__ __launch_bounds__(256) void k_bp_denoise_tail(const int *__restrict__
         const int base = slot_pix[s], m = slot_m[s];
         const double *av = gavg + base;
         const double *P = vpts + 3 * static_cast<size_t>(base);
-        if constexpr (MC_DBG_CHECK) bp_dbg_knn_tail(P, gsx + base, av, m, min(pr.knn, m), s);
+        if constexpr (MC_DBG_CHECK) bp_dbg_knn_tail(P, gsx + base, av, m, min(pr.knn, m), s, base);
         double mean = 0.0, sq = 0.0;
         for (int r0 = 0; r0 < m; r0 += 64) {
             // values that are not > 0 become +0.0, whose add leaves the (non-negative) sum as it is:

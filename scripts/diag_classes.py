@@ -31,6 +31,8 @@ for joined in ("0", "1"):
     for mc in ("0", "1", "2", "3", "4", "5", "6"):
         os.environ["MC_BP_MIN_CLASS"] = mc
         for r in range(REPS):
+            if os.environ.get("DIAG_VERBOSE"):
+                print(f"-- run joined={joined} min_class={mc} rep={r}", flush=True)
             got = run()
             d = np.argwhere(got != ref)
             if len(d):

@@ -9,4 +9,4 @@ mkdir -p "$OUT"
 step() { local name=$1; shift; echo "== $name $(date +%T)"; timeout -k 10 "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" \
     || { echo "$name failed"; tail -30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }; tail -12 "$OUT/$name.out"; }
 step diag 240 python -u scripts/diag_classes.py 4
-step diag_dbg 300 env MCGRAPH_LIB=$PWD/maskclustering_amd/libmcgraph_dbg.so python -u scripts/diag_classes.py 2
+step diag_dbg 300 env DIAG_VERBOSE=1 MCGRAPH_LIB=$PWD/maskclustering_amd/libmcgraph_dbg.so python -u scripts/diag_classes.py 1
