@@ -2306,6 +2306,33 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                     sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
                 }
             }
+            if constexpr (MC_DBG_CHECK) {  // the ring result against every kept record of the slot's grid
+                double bf[kBpKnnMax];
+                for (int k = 0; k < kBpKnnMax; k++) bf[k] = DBL_MAX;
+                for (int q2 = 0; q2 < n; q2++) {
+                    const double4 p = g.pt[q2];
+                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
+                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                    sorted_insert(bf, ((ex * ex) + (ey * ey)) + (ez * ez));
+                }
+                if (bf[kBpKnnMax - 1] != best[kBpKnnMax - 1] && bp_dbg_fail(4)) {
+                    printf("[bp dbg ring] slot=%d n=%d q=%d cell (%d,%d,%d) cmax (%d,%d,%d) nb=%u found=%d done=%d best19 %.17g brute19 %.17g\n",
+                           s, n, q, x, y, z, g.cmax[0], g.cmax[1], g.cmax[2], g.nb, found, done ? 1 : 0, best[kBpKnnMax - 1],
+                           bf[kBpKnnMax - 1]);
+                    for (int q2 = 0; q2 < n; q2++) {  // the kept records nearer than the ring's k-th
+                        const double4 p = g.pt[q2];
+                        const unsigned long long kw = static_cast<unsigned long long>(__double_as_longlong(p.w));
+                        if (!(kw & kKeptBit)) continue;
+                        const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                        const double d2 = ((ex * ex) + (ey * ey)) + (ez * ez);
+                        if (d2 >= best[kBpKnnMax - 1]) continue;
+                        int px, py, pz;
+                        unpack3(kw & ~kKeptBit, px, py, pz);
+                        const unsigned b = mod_mul(bp_hash3(px, py, pz), g.nb);
+                        printf("   rec %d cell (%d,%d,%d) d2 %.17g bucket %u [%d,%d)\n", q2, px, py, pz, d2, b, g.bs[b], g.bs[b + 1]);
+                    }
+                }
+            }
             double sum = 0.0;
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
