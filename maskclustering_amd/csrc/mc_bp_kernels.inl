@@ -2319,6 +2319,8 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                     printf("[bp dbg ring] slot=%d n=%d q=%d cell (%d,%d,%d) cmax (%d,%d,%d) nb=%u found=%d done=%d best19 %.17g brute19 %.17g\n",
                            s, n, q, x, y, z, g.cmax[0], g.cmax[1], g.cmax[2], g.nb, found, done ? 1 : 0, best[kBpKnnMax - 1],
                            bf[kBpKnnMax - 1]);
+                    printf("   a (%.17g, %.17g, %.17g) mn (%.17g, %.17g, %.17g) ce %.17g o (%.17g, %.17g, %.17g)\n", a.x, a.y, a.z,
+                           mn[0], mn[1], mn[2], ce, ox, oy, oz);
                     for (int q2 = 0; q2 < n; q2++) {  // the kept records nearer than the ring's k-th
                         const double4 p = g.pt[q2];
                         const unsigned long long kw = static_cast<unsigned long long>(__double_as_longlong(p.w));
@@ -2329,7 +2331,8 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                         int px, py, pz;
                         unpack3(kw & ~kKeptBit, px, py, pz);
                         const unsigned b = mod_mul(bp_hash3(px, py, pz), g.nb);
-                        printf("   rec %d cell (%d,%d,%d) d2 %.17g bucket %u [%d,%d)\n", q2, px, py, pz, d2, b, g.bs[b], g.bs[b + 1]);
+                        printf("   rec %d cell (%d,%d,%d) d2 %.17g bucket %u [%d,%d) p (%.17g, %.17g, %.17g)\n", q2, px, py, pz, d2, b,
+                               g.bs[b], g.bs[b + 1], p.x, p.y, p.z);
                     }
                 }
             }
