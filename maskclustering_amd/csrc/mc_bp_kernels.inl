@@ -2218,6 +2218,23 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 dq[e0 + f] = s;
                 gitem[e0 + f] = q | (spar[q] << 14);
             }
+            if (MC_DBG_CHECK && t == 0) {  // the origin handed to the ring kernel against the records' keys
+                double fm[3] = {DBL_MAX, DBL_MAX, DBL_MAX};
+                for (int i = 0; i < n; i++)
+                    for (int c = 0; c < 3; c++) fm[c] = fmin(fm[c], P[3 * i + c]);
+                for (int i = 0; i < n; i++) {
+                    int kx, ky, kz;
+                    unpack3(static_cast<unsigned long long>(__double_as_longlong(spt[i].w)) & ~kKeptBit, kx, ky, kz);
+                    const int cz = static_cast<int>(floor((spt[i].z - mn[2]) / pr.ce));
+                    const int cy = static_cast<int>(floor((spt[i].y - mn[1]) / pr.ce));
+                    if ((cz != kz || cy != ky) && bp_dbg_fail(5)) {
+                        printf("[bp dbg origin] N=%d slot=%d n=%d rec %d key (%d,%d,%d) from mn (%d,%d); mn (%.17g,%.17g,%.17g) "
+                               "fresh min (%.17g,%.17g,%.17g)\n", N, s, n, i, kx, ky, kz, cy, cz, mn[0], mn[1], mn[2], fm[0], fm[1],
+                               fm[2]);
+                        break;
+                    }
+                }
+            }
             if (t == 0) {
                 double *gm = slot_grid + 8 * static_cast<size_t>(s);
 #pragma unroll
