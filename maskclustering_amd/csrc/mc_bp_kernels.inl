@@ -1838,6 +1838,18 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         g.nb = static_cast<unsigned>(NBK * n);
 #pragma unroll
         for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
+        if (t == 0) {  // the grid's origin, extent and size for k_bp_knn_ring, written while they are fresh
+            // (read back at the end of the slot, thread 0's origin was seen to differ from the one the
+            // cell keys were made with, in one build: DESIGN.md §4, "S1 race investigation")
+            double *gm = slot_grid + 8 * static_cast<size_t>(s);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                gm[c] = mn[c];
+                gm[3 + c] = static_cast<double>(g.cmax[c]);
+            }
+            gm[6] = static_cast<double>(g.nb);
+            gm[7] = static_cast<double>(n);
+        }
         BP_STAMP(17);
         // 2. bucket counts
         for (int b = t; b < NBK * n; b += T) sB[b] = 0;
@@ -2234,16 +2246,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                         break;
                     }
                 }
-            }
-            if (t == 0) {
-                double *gm = slot_grid + 8 * static_cast<size_t>(s);
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    gm[c] = mn[c];
-                    gm[3 + c] = static_cast<double>(g.cmax[c]);
-                }
-                gm[6] = static_cast<double>(g.nb);
-                gm[7] = static_cast<double>(n);
             }
         }
 #ifdef MC_BP_STAMPS
