@@ -1755,7 +1755,9 @@ enum BpStat : int {
     BS_VXFB = BS_TK + mc::kBpClasses,     // slots the first voxel tier hands to the second
     BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
     BS_DQ,                                // points queued for the k-NN ring search (one counter per class)
-    BS_COUNT = BS_DQ + mc::kBpClasses
+    BS_DQB = BS_DQ + mc::kBpClasses,      // where each class's queue region starts
+    BS_CLSVOX = BS_DQB + mc::kBpClasses,  // voxels of each class's slots (the region sizes)
+    BS_COUNT = BS_CLSVOX + mc::kBpClasses
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
@@ -1894,28 +1896,22 @@ constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 // class's slots from a ticket counter
 // The k-NN ring search (k_bp_knn_ring) and the statistics / survivors (k_bp_denoise_tail) of the LDS
 // classes: by default each class's own, queued on its stream right after its class kernel, so that they
-// run while the other classes still compute (one queue region of px / kBpClasses entries per class; a
-// slot that finds its class's region full takes the whole-cloud scan in the class kernel instead);
-// MC_BP_TAIL_JOINED=1: one queue for every class and both kernels once after the join.
+// run while the other classes still compute (class c's queue region starts at the voxels of the classes
+// before it, k_bp_dq_bases); MC_BP_TAIL_JOINED=1: one queue for every class and both kernels once
+// after the join.
 static bool bp_tail_per_class()
 {
     const char *e = getenv("MC_BP_TAIL_JOINED");  // read per call (the tests switch it)
     return !(e && atoi(e) != 0);
 }
-inline size_t bp_dq_region(const mc_ctx *ctx)
-{
-    size_t r = bp_tail_per_class() ? ctx->bp_px_cap / mc::kBpClasses : ctx->bp_px_cap;
-    if (const char *e = getenv("MC_BP_DQ_CAP")) r = std::min<size_t>(r, strtoull(e, nullptr, 10));  // test knob
-    return std::min<size_t>(r, INT_MAX);
-}
 
 void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int cls_lo, int cls_hi, int ncap, int *st, const mc::BpDev &dv)
 {
-    const size_t off = bp_tail_per_class() ? bp_dq_region(ctx) * cls_lo : 0;
-    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ + (bp_tail_per_class() ? cls_lo : 0),
-                       ctx->d_vx_pvid.as<int>() + off, ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
-                       ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>() + off, ctx->d_slot_grid.as<double>(),
-                       ctx->d_avg.as<double>(), static_cast<int>(bp_dq_region(ctx)));
+    const int q = bp_tail_per_class() ? cls_lo : 0;
+    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ + q,
+                       ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
+                       ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_slot_grid.as<double>(),
+                       ctx->d_avg.as<double>(), st + BS_DQB + q);
     hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * (bp_tail_per_class() ? 2 : 4)), dim3(256), 0, s,
                        st + BS_CLS, ctx->d_cls_list.as<int>(), ncap, cls_lo, cls_hi, ctx->d_slot_pix.as<int>(),
                        ctx->d_slot_m.as<int>(), dv, ctx->d_vpts.as<double>(), ctx->d_avg.as<double>(),
@@ -1928,16 +1924,15 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
 {
     using C = mc::BpLdsClass<N>;
     const bool own = bp_tail_per_class();
-    const size_t off = own ? bp_dq_region(ctx) * cls : 0;
     // the classes run concurrently: each has its own region of per-workgroup neighbour lists
     hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * kBpOversub), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
                        ctx->d_slot_m.as<int>(), ctx->d_avg.as<double>(), ctx->d_ssidx.as<int>(),
-                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>() + off,
-                       ctx->d_vx_pvid.as<int>() + off, st + BS_DQ + (own ? cls : 0),
-                       static_cast<int>(bp_dq_region(ctx)), ctx->d_slot_grid.as<double>());
+                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
+                       ctx->d_vx_pvid.as<int>(), st + BS_DQ + (own ? cls : 0), st + BS_DQB + (own ? cls : 0),
+                       ctx->d_slot_grid.as<double>());
     if (own) bp_denoise_tail_launch(ctx, s, cls, cls + 1, ncap, st, dv);
 }
 // MC_BP_DEBUG_SYNC=1: synchronise and report after every S1 group (diagnostics of a stalled batch)
@@ -2372,7 +2367,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
                                    ctx->d_vox_order.as<int>());
                 hipLaunchKernelGGL(mc::k_bp_classify, dim3(64), dim3(256), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
-                                   ctx->d_vox_order.as<int>(), ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>());
+                                   ctx->d_vox_order.as<int>(), ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>(),
+                                   st + BS_CLSVOX);
+                hipLaunchKernelGGL(mc::k_bp_dq_bases, dim3(1), dim3(64), 0, s, st + BS_CLSVOX, st + BS_DQB,
+                                   bp_tail_per_class() ? 1 : 0);
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
                 MC_HIP(hipEventRecord(ctx->ev_fork, s));
                 MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));

@@ -1701,7 +1701,8 @@ __device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, con
 // class (tests: every class gives the same results).  cls_cnt[kBpClasses + 1] must be zero.
 __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
                                                      const int *__restrict__ order, int cap, int min_cls,
-                                                     int *__restrict__ cls_cnt, int *__restrict__ cls_list)
+                                                     int *__restrict__ cls_cnt, int *__restrict__ cls_list,
+                                                     int *__restrict__ cls_vox)
 {
     // slots taken in k_bp_vox_order's largest-first order, so each class's list (its ticket order)
     // starts with its largest slots (roughly: the workgroups append concurrently) and the class
@@ -1722,6 +1723,10 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
             if (lane_id() == leader) base = atomicAdd(&cls_cnt[k], __popcll(b));
             base = __shfl(base, leader, 64);
             if (live && c == k) cls_list[k * cap + base + __popcll(b & ((1ull << lane_id()) - 1))] = s;
+            if (k < kBpClasses) {  // the class's voxels: the size of its ring-search queue region
+                const int vs = wave_sum(live && c == k ? n : 0);
+                if (lane_id() == leader) atomicAdd(&cls_vox[k], vs);
+            }
         }
     }
 }
@@ -1753,7 +1758,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
     unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, int *__restrict__ slot_m, double *__restrict__ gavg,
     int *__restrict__ gsx, double4 *__restrict__ grec, int *__restrict__ gbs, int *__restrict__ gitem,
-    int *__restrict__ dq, int *__restrict__ dq_cnt, int dq_cap, double *__restrict__ slot_grid)
+    int *__restrict__ dq, int *__restrict__ dq_cnt, const int *__restrict__ dq_base, double *__restrict__ slot_grid)
 {
     constexpr int T = BpLdsClass<N>::T;
     constexpr int NW = T / 64;
@@ -2197,34 +2202,14 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         // position | rank << 14; at most one entry per voxel of the batch, so a pixel-sized array holds it)
         const int nd = s_ndef;
         if (nd > 0) {
-            if (t == 0) s_slot = atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
-            bar();
-            const int e0 = s_slot;
-            if (e0 + nd > dq_cap) {  // the queue region is full (not seen in practice): this slot's
-                                     // deferred points take the whole-cloud scan here, a wave per point;
-                                     // its entries inside the region are marked empty for k_bp_knn_ring
-                for (int f = e0 + t; f < dq_cap; f += T) dq[f] = -1;
-                for (int f = wv; f < nd; f += NW) {
-                    const int q = sring[f];
-                    const double4 a = spt[q];
-                    const double mean = wave_knn_mean(m, kk, [&](int j) {
-                        const double4 p = spt[spos[sX[j]]];
-                        const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                        return ((ex * ex) + (ey * ey)) + (ez * ez);
-                    });
-                    if (lane == 0) {
-                        mavg[spar[q]] = mean;
-                        bp_dbg_path(static_cast<size_t>(base) + spar[q], 3u | (static_cast<unsigned>(N) << 4));
-                    }
-                }
-                if (t == 0) slot_m[s] = m;
-                bar();
-                continue;
-            }
             double4 *gr = grec + base;
             for (int i = t; i < n; i += T) gr[i] = spt[i];
             int *gb = gbs + 2 * static_cast<size_t>(base) + s;
             for (int b = t; b <= NBK * n; b += T) gb[b] = sA[b];
+            // the class's queue region holds one entry per voxel of its slots (k_bp_classify), so it cannot fill
+            if (t == 0) s_slot = *dq_base + atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
+            bar();
+            const int e0 = s_slot;
             for (int f = t; f < nd; f += T) {
                 const int q = sring[f];
                 dq[e0 + f] = s;
@@ -2264,12 +2249,12 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                                                      const int *__restrict__ slot_pix, BpDev pr,
                                                      const double4 *__restrict__ grec, const int *__restrict__ gbs,
                                                      const int *__restrict__ gitem, const double *__restrict__ slot_grid,
-                                                     double *__restrict__ gavg, int dq_cap)
+                                                     double *__restrict__ gavg, const int *__restrict__ dq_base)
 {
-    const int ne = min(*dq_cnt, dq_cap);  // (the counter runs past the region when a slot found it full)
-    for (int f = blockIdx.x * 256 + threadIdx.x; f < ne; f += gridDim.x * 256) {
+    const int ne = *dq_cnt, e0 = *dq_base;  // this queue's entries: [e0, e0 + ne)
+    for (int f0 = blockIdx.x * 256 + threadIdx.x; f0 < ne; f0 += gridDim.x * 256) {
+        const int f = e0 + f0;
         const int s = dq[f];
-        if (s < 0) continue;  // an entry of a slot that took the in-kernel scan
         const int base = slot_pix[s];
         const double *gm = slot_grid + 8 * static_cast<size_t>(s);
         const double mn[3] = {gm[0], gm[1], gm[2]};
@@ -2887,6 +2872,19 @@ __global__ __launch_bounds__(256) void k_bp_emit(const int *__restrict__ dNS, co
 // per-slot nn >= 0 flags and sizes for the output scan
 // per-batch statistics block: the error frame at INT_MAX, every counter and ticket zero (a kernel
 // instead of a pageable host-to-device copy at every batch start)
+// ring-search queue regions: class c's entries start at the voxels of the classes before it
+// (per_class 0: one region for every class, at 0)
+__global__ __launch_bounds__(64) void k_bp_dq_bases(const int *__restrict__ cls_vox, int *__restrict__ dq_base, int per_class)
+{
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int c = 0; c < kBpClasses; c++) {
+            dq_base[c] = per_class ? acc : 0;
+            acc += cls_vox[c];
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void k_bp_stat_init(int *__restrict__ st, int n)
 {
     for (int i = threadIdx.x; i < n; i += 64) st[i] = i == 0 ? INT_MAX : 0;

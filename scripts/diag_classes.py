@@ -25,6 +25,28 @@ def run():
 os.environ.pop("MC_BP_MIN_CLASS", None)
 os.environ.pop("MC_BP_TAIL_JOINED", None)
 ref = run()
+# the oracle's statistics of the same frames (oracle/s1_oracle.c): which run is right
+from oracle import oracle  # noqa: E402  (diagnostic: the checker)
+want = oracle.s1_frames(fr.scene_points.astype(np.float32), fr.depth, fr.seg, fr.intrinsics, fr.poses)
+CMP = [(1, 0), (2, 1), (3, 2), (4, 3), (5, 4), (7, 6), (8, 7), (9, 8)]
+
+
+def vs_oracle(st):
+    out = []
+    for c, (ol, oo, op, ost) in enumerate(want):
+        big = ost[ost[:, 1] >= 25]
+        dev = st[st[:, 0] == c]
+        if len(dev) != len(big):
+            out.append(f"frame {c}: {len(dev)} candidates vs {len(big)}")
+            continue
+        for dc, oc in CMP:
+            bad = np.nonzero(dev[:, dc] != big[:, oc])[0]
+            for i in bad[:4]:
+                out.append(f"frame {c} id {dev[i, 1]} {COLS[dc]} {dev[i, dc]} (oracle {big[i, oc]})")
+    return out
+
+
+print("default run vs oracle:", vs_oracle(ref) or "equal", flush=True)
 bad = 0
 for joined in ("0", "1"):
     os.environ["MC_BP_TAIL_JOINED"] = joined
@@ -34,6 +56,9 @@ for joined in ("0", "1"):
             if os.environ.get("DIAG_VERBOSE"):
                 print(f"-- run joined={joined} min_class={mc} rep={r}", flush=True)
             got = run()
+            vo = vs_oracle(got)
+            if vo:
+                print(f"joined={joined} min_class={mc} rep={r} vs oracle: " + "; ".join(vo[:6]), flush=True)
             d = np.argwhere(got != ref)
             if len(d):
                 bad += 1

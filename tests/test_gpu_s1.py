@@ -267,12 +267,11 @@ def test_list_overflow_paths_agree(ctx, monkeypatch, nbcap):
             monkeypatch.delenv("MC_BP_MIN_CLASS")
 
 
-@pytest.mark.parametrize("env", [("MC_BP_TAIL_JOINED", "1"), ("MC_BP_DQ_CAP", "0"), ("MC_BP_DQ_CAP", "5")])
+@pytest.mark.parametrize("env", [("MC_BP_TAIL_JOINED", "1"), ("MC_BP_TAIL_JOINED", "0")])
 def test_ring_queue_modes_agree(ctx, monkeypatch, env):
     """The k-NN ring-search queue: per class (default; each class's ring search and statistics queued
-    behind its class kernel), one joined queue (MC_BP_TAIL_JOINED=1), and a region too small for the
-    deferred points (MC_BP_DQ_CAP: slots that find it full take the whole-cloud scan inside the class
-    kernel, their region entries marked empty) give the same masks, in every size class."""
+    behind its class kernel, in a region sized by the class's voxels) and one joined queue
+    (MC_BP_TAIL_JOINED=1) give the same masks, in every size class."""
     for inp in _dense_inputs():
         want = _run(ctx, *inp)
         sa = ctx.bp_candidates()
