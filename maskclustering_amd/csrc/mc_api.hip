@@ -1895,14 +1895,15 @@ constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 // one LDS size class of the denoise: as many workgroups as are resident at once, each taking the
 // class's slots from a ticket counter
 // The k-NN ring search (k_bp_knn_ring) and the statistics / survivors (k_bp_denoise_tail) of the LDS
-// classes: by default each class's own, queued on its stream right after its class kernel, so that they
-// run while the other classes still compute (class c's queue region starts at the voxels of the classes
-// before it, k_bp_dq_bases); MC_BP_TAIL_JOINED=1: one queue for every class and both kernels once
-// after the join.
+// classes: by default once after the join, over one queue for every class; MC_BP_TAIL_PER_CLASS=1:
+// each class's own, queued on its stream right after its class kernel (class c's queue region starts
+// at the voxels of the classes before it, k_bp_dq_bases), so that they run while the other classes
+// still compute.  Measured at C3 (profiles/r04/r4e_tail_ab.jsonl): the group 4.45 ms joined against
+// 4.53 ms per class, so the joined tail stays the default.
 static bool bp_tail_per_class()
 {
-    const char *e = getenv("MC_BP_TAIL_JOINED");  // read per call (the tests switch it)
-    return !(e && atoi(e) != 0);
+    const char *e = getenv("MC_BP_TAIL_PER_CLASS");  // read per call (the tests switch it)
+    return e && atoi(e) != 0;
 }
 
 void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int cls_lo, int cls_hi, int ncap, int *st, const mc::BpDev &dv)

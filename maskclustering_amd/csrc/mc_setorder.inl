@@ -44,6 +44,50 @@ struct PySet {
     PySet() : t(kMinSize, -1) {}
 };
 
+// Tables are recycled per thread (by power-of-two size, up to 64 MB held per thread): a replay makes
+// and drops tens of millions of slots, and fresh large blocks cost page faults and, when returned to
+// the OS from a many-threaded process, TLB shootdowns.
+struct TablePool {
+    std::vector<std::vector<int32_t>> bins[40];
+    size_t bytes = 0;
+};
+inline TablePool &table_pool()
+{
+    thread_local TablePool p;
+    return p;
+}
+inline int log2_pow2(size_t n)
+{
+    int b = 0;
+    while ((static_cast<size_t>(1) << b) < n) b++;
+    return b;
+}
+constexpr size_t kPoolMinSlots = 256;
+inline std::vector<int32_t> take_table(size_t ns)
+{
+    if (ns >= kPoolMinSlots) {
+        TablePool &p = table_pool();
+        auto &bin = p.bins[log2_pow2(ns)];
+        if (!bin.empty()) {
+            std::vector<int32_t> v = std::move(bin.back());
+            bin.pop_back();
+            p.bytes -= ns * sizeof(int32_t);
+            std::fill(v.begin(), v.end(), -1);
+            return v;
+        }
+    }
+    return std::vector<int32_t>(ns, -1);
+}
+inline void give_table(std::vector<int32_t> &&v)
+{
+    const size_t ns = v.size();
+    if (ns < kPoolMinSlots || (ns & (ns - 1))) return;
+    TablePool &p = table_pool();
+    if (p.bytes + ns * sizeof(int32_t) > (static_cast<size_t>(64) << 20)) return;
+    p.bins[log2_pow2(ns)].push_back(std::move(v));
+    p.bytes += ns * sizeof(int32_t);
+}
+
 // set_insert_clean: the first empty slot of key's probe sequence (no key comparisons)
 inline void insert_clean(int32_t *tab, size_t mask, int32_t key)
 {
@@ -72,11 +116,12 @@ inline void resize(PySet &s, size_t minused)
     size_t ns = kMinSize;
     while (ns <= minused) ns <<= 1;
     if (ns == kMinSize && s.mask == kMinSize - 1) return;  // the small table, no dummies: nothing to do
-    std::vector<int32_t> nt(ns, -1);
+    std::vector<int32_t> nt = take_table(ns);
     for (int32_t k : s.t)
         if (k >= 0) insert_clean(nt.data(), ns - 1, k);
     s.t.swap(nt);
     s.mask = ns - 1;
+    give_table(std::move(nt));
 }
 
 // set_add_entry (keys are distinct ints: an equal hash is an equal key)
@@ -166,14 +211,16 @@ inline PySet union_consume(PySet &&a, PySet &&b)
         if (ns - 1 == a.mask) {
             r = std::move(a);
         } else {
-            r.t.assign(ns, -1);
+            r.t = take_table(ns);
             r.mask = ns - 1;
             for (int32_t k : a.t)
                 if (k >= 0) insert_clean(r.t.data(), r.mask, k);
             r.used = a.used;
+            give_table(std::move(a.t));
         }
     }
     merge_consume(r, std::move(b));
+    give_table(std::move(b.t));  // (empty when b's table moved into r)
     return r;
 }
 
@@ -187,11 +234,12 @@ inline PySet union_consume(PySet &&a, const PySet &b)
         if (ns - 1 == a.mask) {
             r = std::move(a);
         } else {
-            r.t.assign(ns, -1);
+            r.t = take_table(ns);
             r.mask = ns - 1;
             for (int32_t k : a.t)
                 if (k >= 0) insert_clean(r.t.data(), r.mask, k);
             r.used = a.used;
+            give_table(std::move(a.t));
         }
     }
     merge(r, b);

@@ -1,5 +1,5 @@
 """Diagnostic: run the tiny dense S1 scene of test_denoise_size_classes_agree under every
-MC_BP_MIN_CLASS and both denoise tail modes (per class / joined), REPS times each, and print every
+MC_BP_MIN_CLASS and both denoise tail modes (per class / per_class), REPS times each, and print every
 candidate-statistics element that differs from the first run (slot, column, values)."""
 import os
 import sys
@@ -23,7 +23,7 @@ def run():
 
 
 os.environ.pop("MC_BP_MIN_CLASS", None)
-os.environ.pop("MC_BP_TAIL_JOINED", None)
+os.environ.pop("MC_BP_TAIL_PER_CLASS", None)
 ref = run()
 # the oracle's statistics of the same frames (oracle/s1_oracle.c): which run is right
 from oracle import oracle  # noqa: E402  (diagnostic: the checker)
@@ -48,21 +48,21 @@ def vs_oracle(st):
 
 print("default run vs oracle:", vs_oracle(ref) or "equal", flush=True)
 bad = 0
-for joined in ("0", "1"):
-    os.environ["MC_BP_TAIL_JOINED"] = joined
+for per_class in ("0", "1"):
+    os.environ["MC_BP_TAIL_PER_CLASS"] = per_class
     for mc in ("0", "1", "2", "3", "4", "5", "6"):
         os.environ["MC_BP_MIN_CLASS"] = mc
         for r in range(REPS):
             if os.environ.get("DIAG_VERBOSE"):
-                print(f"-- run joined={joined} min_class={mc} rep={r}", flush=True)
+                print(f"-- run per_class={per_class} min_class={mc} rep={r}", flush=True)
             got = run()
             vo = vs_oracle(got)
             if vo:
-                print(f"joined={joined} min_class={mc} rep={r} vs oracle: " + "; ".join(vo[:6]), flush=True)
+                print(f"per_class={per_class} min_class={mc} rep={r} vs oracle: " + "; ".join(vo[:6]), flush=True)
             d = np.argwhere(got != ref)
             if len(d):
                 bad += 1
-                print(f"joined={joined} min_class={mc} rep={r}: " + "; ".join(
+                print(f"per_class={per_class} min_class={mc} rep={r}: " + "; ".join(
                     f"slot {i} (frame {ref[i, 0]} id {ref[i, 1]} nvox {ref[i, 3]}) {COLS[j]} {ref[i, j]} -> {got[i, j]}"
                     for i, j in d[:8]), flush=True)
 print("differing runs", bad, "of", 2 * 7 * REPS, flush=True)

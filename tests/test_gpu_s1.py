@@ -267,11 +267,11 @@ def test_list_overflow_paths_agree(ctx, monkeypatch, nbcap):
             monkeypatch.delenv("MC_BP_MIN_CLASS")
 
 
-@pytest.mark.parametrize("env", [("MC_BP_TAIL_JOINED", "1"), ("MC_BP_TAIL_JOINED", "0")])
+@pytest.mark.parametrize("env", [("MC_BP_TAIL_PER_CLASS", "1"), ("MC_BP_TAIL_PER_CLASS", "0")])
 def test_ring_queue_modes_agree(ctx, monkeypatch, env):
-    """The k-NN ring-search queue: per class (default; each class's ring search and statistics queued
-    behind its class kernel, in a region sized by the class's voxels) and one joined queue
-    (MC_BP_TAIL_JOINED=1) give the same masks, in every size class."""
+    """The k-NN ring-search queue: one joined queue (default) and per class (MC_BP_TAIL_PER_CLASS=1:
+    each class's ring search and statistics queued behind its class kernel, in a region sized by the
+    class's voxels) give the same masks, in every size class."""
     for inp in _dense_inputs():
         want = _run(ctx, *inp)
         sa = ctx.bp_candidates()
