@@ -1,5 +1,5 @@
 """Diagnostic: run the tiny dense S1 scene of test_denoise_size_classes_agree under every
-MC_BP_MIN_CLASS and both denoise tail modes (per class / per_class), REPS times each, and print every
+MC_BP_MIN_CLASS and both denoise tail modes (joined / per class), REPS times each, and print every
 candidate-statistics element that differs from the first run (slot, column, values)."""
 import os
 import sys
