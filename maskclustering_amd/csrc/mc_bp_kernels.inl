@@ -1747,6 +1747,9 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 #ifndef MC_ABLATE_BP
 #define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union
 #endif
+#ifndef MC_BP_KNN_LATE_INIT
+#define MC_BP_KNN_LATE_INIT 0  // 1: the k-NN list pass loads its point and sets up the k best after the list walk (A/B)
+#endif
 #ifndef MC_BP_FUSED_UNION
 #define MC_BP_FUSED_UNION 1  // union every pair while the lists are built; the separate union pass only for
                              // slots with a non-core point that has neighbours (0: A/B baseline)
@@ -2125,14 +2128,16 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 sring[atomicAdd(&s_ndef, 1)] = q;
                 continue;
             }
+            double best[kBpKnnMax];
+#if !MC_BP_KNN_LATE_INIT
             const double4 a = spt[q];
             auto d2of = [&](const double4 &p) {
                 const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
                 return ((ex * ex) + (ey * ey)) + (ez * ez);
             };
-            double best[kBpKnnMax];
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+#endif
             // selection pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = slot k),
             // from the entries' radius classes; if >= k of them lie inside radius i, the k nearest are
             // among those (every other kept candidate is farther than >= k others), so only they are
@@ -2152,6 +2157,15 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     });
             const int found = __popcll(mall);
             unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
+#if MC_BP_KNN_LATE_INIT  // (the point and the k best only from here: not live across the list walk)
+            const double4 a = spt[q];
+            auto d2of = [&](const double4 &p) {
+                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
+                return ((ex * ex) + (ey * ey)) + (ez * ez);
+            };
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+#endif
             if (found >= kk) {
                 const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
                 auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)] & kNbPos); };
