@@ -72,6 +72,23 @@ __device__ __forceinline__ int scene_cell(float v, float inv)
 }
 
 // (a1, u1): Open3D create_from_depth_image + transform, in double, no FMA
+#ifndef MC_FAST_FLOORDIV
+#define MC_FAST_FLOORDIV 0  // 1: floor(a / b) of cell / voxel indices from a * (1 / b) unless that is within a
+                            //    margin of an integer (then the division): the same integers (A/B knob)
+#endif
+// floor(a / b) for the cell and voxel indices: a * inv_b differs from the rounded quotient by a few
+// ulps, so its floor is the quotient's unless it lies within 1e-12 |q| + 1e-12 of an integer, where
+// the division itself decides
+__device__ __forceinline__ double floor_div(double a, double b, double inv_b)
+{
+    if (!MC_FAST_FLOORDIV) return floor(a / b);
+    const double q = a * inv_b;
+    const double f = floor(q);
+    const double m = 1e-12 * fabs(q) + 1e-12;
+    if (q - f > m && (f + 1.0) - q > m) return f;
+    return floor(a / b);
+}
+
 __device__ __forceinline__ void bp_world(const double *__restrict__ K, const double *__restrict__ T, int u, int v,
                                          float d, double &ox, double &oy, double &oz)
 {
@@ -615,6 +632,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
+    const double inv_vs = 1.0 / pr.vs;
     for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
         const int s = order[idx];
         if (force_fb) {  // test knob: every slot to the global-hash kernel
@@ -680,7 +698,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 bool fits = true;
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    const double r = floor((p[c] - vmin[c]) / pr.vs);
+                    const double r = floor_div(p[c] - vmin[c], pr.vs, inv_vs);
                     fits = fits && r >= 0.0 && r < 1024.0;
                     key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
                 }
@@ -1802,6 +1820,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     int *ccnt = sB + N;
     int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
     const int cnt_cls = *cls_cnt;
+    const double inv_ce = 1.0 / pr.ce;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     unsigned short *nbw = nbl + static_cast<size_t>(blockIdx.x) * N * kBpNbCap;
     // one array for the list words of every walk (union, labels, k-NN): the compiler keeps a
@@ -1865,7 +1884,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         for (int i = t; i < n; i += T) {
             int c3[3];
 #pragma unroll
-            for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor((P[3 * i + c] - mn[c]) / pr.ce));
+            for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor_div(P[3 * i + c] - mn[c], pr.ce, inv_ce));
             const unsigned b = mod_mul(bp_hash3(c3[0], c3[1], c3[2]), g.nb);
             sX[i] = static_cast<int>(b);
             atomicAdd(&sB[b], 1);
@@ -1892,9 +1911,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const int b = sX[i];
             const int q = sA[b] + atomicSub(&sB[b], 1) - 1;
             const double x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
-            const unsigned long long ck = pack3(static_cast<int>(floor((x - mn[0]) / pr.ce)),
-                                                static_cast<int>(floor((y - mn[1]) / pr.ce)),
-                                                static_cast<int>(floor((z - mn[2]) / pr.ce)));
+            const unsigned long long ck = pack3(static_cast<int>(floor_div(x - mn[0], pr.ce, inv_ce)),
+                                                static_cast<int>(floor_div(y - mn[1], pr.ce, inv_ce)),
+                                                static_cast<int>(floor_div(z - mn[2], pr.ce, inv_ce)));
             spt[q] = make_double4(x, y, z, __longlong_as_double(static_cast<long long>(ck)));
             sorig[q] = static_cast<short>(i);
             spos[i] = static_cast<short>(q);
