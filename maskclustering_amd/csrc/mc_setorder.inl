@@ -26,6 +26,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <system_error>
 #include <thread>
@@ -44,7 +45,7 @@ struct PySet {
     PySet() : t(kMinSize, -1) {}
 };
 
-// Tables are recycled per thread (by power-of-two size, up to 64 MB held per thread): a replay makes
+// Tables are recycled per thread (by power-of-two size, up to 8 MB held per thread): a replay makes
 // and drops tens of millions of slots, and fresh large blocks cost page faults and, when returned to
 // the OS from a many-threaded process, TLB shootdowns.
 struct TablePool {
@@ -83,7 +84,7 @@ inline void give_table(std::vector<int32_t> &&v)
     const size_t ns = v.size();
     if (ns < kPoolMinSlots || (ns & (ns - 1))) return;
     TablePool &p = table_pool();
-    if (p.bytes + ns * sizeof(int32_t) > (static_cast<size_t>(64) << 20)) return;
+    if (p.bytes + ns * sizeof(int32_t) > (static_cast<size_t>(8) << 20)) return;
     p.bins[log2_pow2(ns)].push_back(std::move(v));
     p.bytes += ns * sizeof(int32_t);
 }
@@ -315,6 +316,41 @@ class Pool {
     bool quit_ = false;
 };
 
+// The workers of every replay in the process (created on first use, re-created when the thread count
+// changes, left idle between calls): their per-thread table pools and malloc arenas stay warm.
+// One replay step runs on them at a time.  MC_SETORDER_PERSIST=0: a pool per call instead.
+class SharedPool {
+  public:
+    template <typename F>
+    void run(int nth, F &&fn)
+    {
+        if (const char *e = getenv("MC_SETORDER_PERSIST"); e && atoi(e) == 0) {
+            Pool p(nth);
+            const std::function<void()> f = fn;
+            p.run(f);
+            return;
+        }
+        std::lock_guard<std::mutex> g(mu_);
+        if (!pool_ || n_ != nth) {
+            pool_.reset();
+            pool_.reset(new Pool(nth));
+            n_ = nth;
+        }
+        const std::function<void()> f = fn;
+        pool_->run(f);
+    }
+
+  private:
+    std::mutex mu_;
+    std::unique_ptr<Pool> pool_;
+    int n_ = 0;
+};
+inline SharedPool &shared_pool()
+{
+    static SharedPool *p = new SharedPool;  // never destroyed: idle workers end with the process
+    return *p;
+}
+
 }  // namespace mcso
 
 // Level-0 sets built ahead (mc_setorder_begin): a background thread makes every set(ascending ids)
@@ -352,8 +388,7 @@ inline void build_level0(mc_setorder *h, const int64_t *node_start, const int64_
             for (int c = next.fetch_add(64); c < N0; c = next.fetch_add(64))
                 for (int i = c; i < std::min(N0, c + 64); i++) h->sets[i] = from_sequence(pts + node_start[i], node_len[i]);
         };
-        Pool pool(h->nth);
-        pool.run(work);
+        shared_pool().run(h->nth, work);
     } catch (const std::bad_alloc &) {
         h->rc = MC_ERR_HIP;
     }
@@ -417,7 +452,6 @@ extern "C" int mc_setorder_finish(mc_setorder *h, int32_t num_levels, const int3
         const int N0 = level_sizes[0];
         if (N0 != h->n0) return MC_ERR_INVALID;
         h->consumed = true;
-        mcso::Pool pool(h->nth);
 
         // per node of the current level: its mask order (level-0 indices) and point set
         std::vector<std::vector<int32_t>> morder(N0);
@@ -512,7 +546,7 @@ extern "C" int mc_setorder_finish(mc_setorder *h, int32_t num_levels, const int3
                     nsets[k] = std::move(acc);
                 }
             };
-            pool.run(work);
+            mcso::shared_pool().run(h->nth, work);
             morder.swap(nmorder);
             sets.swap(nsets);
         }
