@@ -368,12 +368,20 @@ namespace mcso {
 
 inline int threads_for(int32_t num_threads)
 {
-    // the caller's count, else the host's, capped by OMP_NUM_THREADS (a process's CPU share:
-    // hardware_concurrency reports the whole machine)
+    // the caller's count, else half of the process's CPU share (the host's threads capped by
+    // OMP_NUM_THREADS: hardware_concurrency reports the whole machine).  Half, because the caller's
+    // process keeps its own busy threads (the HIP runtime's, the interpreter): the C2 API path's replay
+    // took 28.5 ms on 8 workers against 34-37 ms on 16 on a 16-CPU box share (profiles/r04/
+    // r4y_api_threads.txt); MC_SETORDER_THREADS overrides
     int nth = num_threads;
     if (nth <= 0) {
-        nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-        if (const char *e = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(e)));
+        if (const char *e = getenv("MC_SETORDER_THREADS")) {
+            nth = std::max(1, atoi(e));
+        } else {
+            nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+            if (const char *o = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(o)));
+            nth = std::max(1, nth / 2);
+        }
     }
     return std::max(1, std::min(nth, 64));
 }
