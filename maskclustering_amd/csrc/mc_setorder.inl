@@ -375,8 +375,8 @@ inline int threads_for(int32_t num_threads)
     // r4y_api_threads.txt); MC_SETORDER_THREADS overrides
     int nth = num_threads;
     if (nth <= 0) {
-        if (const char *e = getenv("MC_SETORDER_THREADS")) {
-            nth = std::max(1, atoi(e));
+        if (const char *e = getenv("MC_SETORDER_THREADS"); e && atoi(e) > 0) {
+            nth = atoi(e);
         } else {
             nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
             if (const char *o = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(o)));
