@@ -368,11 +368,10 @@ namespace mcso {
 
 inline int threads_for(int32_t num_threads)
 {
-    // the caller's count, else half of the process's CPU share (the host's threads capped by
-    // OMP_NUM_THREADS: hardware_concurrency reports the whole machine).  Half, because the caller's
-    // process keeps its own busy threads (the HIP runtime's, the interpreter): the C2 API path's replay
-    // took 28.5 ms on 8 workers against 34-37 ms on 16 on a 16-CPU box share (profiles/r04/
-    // r4y_api_threads.txt); MC_SETORDER_THREADS overrides
+    // the caller's count, else MC_SETORDER_THREADS, else the host's threads capped by OMP_NUM_THREADS
+    // (a process's CPU share: hardware_concurrency reports the whole machine).  On the C2 API path the
+    // replay took 34 / 35 / 31 ms on average on 16 / 8 / 12 workers with +-8 ms between repeats
+    // (profiles/r04/r4y_api_threads.txt): the full share stays the default
     int nth = num_threads;
     if (nth <= 0) {
         if (const char *e = getenv("MC_SETORDER_THREADS"); e && atoi(e) > 0) {
@@ -380,7 +379,6 @@ inline int threads_for(int32_t num_threads)
         } else {
             nth = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
             if (const char *o = getenv("OMP_NUM_THREADS")) nth = std::min(nth, std::max(1, atoi(o)));
-            nth = std::max(1, nth / 2);
         }
     }
     return std::max(1, std::min(nth, 64));
