@@ -1909,7 +1909,8 @@ static bool bp_tail_per_class()
 void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int cls_lo, int cls_hi, int ncap, int *st, const mc::BpDev &dv)
 {
     const int q = bp_tail_per_class() ? cls_lo : 0;
-    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ + q,
+    static const int ring_wgs = getenv("MC_BP_RING_WGS") ? std::max(1, atoi(getenv("MC_BP_RING_WGS"))) : 8;  // per CU (A/B knob)
+    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * ring_wgs), dim3(256), 0, s, st + BS_DQ + q,
                        ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
                        ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_slot_grid.as<double>(),
                        ctx->d_avg.as<double>(), st + BS_DQB + q);
@@ -1926,7 +1927,8 @@ void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, co
     using C = mc::BpLdsClass<N>;
     const bool own = bp_tail_per_class();
     // the classes run concurrently: each has its own region of per-workgroup neighbour lists
-    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * kBpOversub), dim3(C::T), 0, s, st + BS_CLS + cls,
+    static const int oversub = getenv("MC_BP_OVERSUB_RT") ? std::max(1, atoi(getenv("MC_BP_OVERSUB_RT"))) : kBpOversub;
+    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * oversub), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
