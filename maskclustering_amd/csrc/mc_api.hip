@@ -1754,10 +1754,9 @@ enum BpStat : int {
     BS_TK = BS_CLS + mc::kBpClasses + 1,  // ticket counters of the LDS classes
     BS_VXFB = BS_TK + mc::kBpClasses,     // slots the first voxel tier hands to the second
     BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
-    BS_DQ,                                // points queued for the k-NN ring search (one counter per class)
-    BS_DQB = BS_DQ + mc::kBpClasses,      // where each class's queue region starts
-    BS_CLSVOX = BS_DQB + mc::kBpClasses,  // voxels of each class's slots (the region sizes)
-    BS_COUNT = BS_CLSVOX + mc::kBpClasses
+    BS_DQ,                                // points queued for the k-NN ring search
+    BS_DNERR,                             // denoise internal-error bits (queue entry / region out of range)
+    BS_COUNT
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
@@ -1894,28 +1893,18 @@ constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 
 // one LDS size class of the denoise: as many workgroups as are resident at once, each taking the
 // class's slots from a ticket counter
-// The k-NN ring search (k_bp_knn_ring) and the statistics / survivors (k_bp_denoise_tail) of the LDS
-// classes: by default once after the join, over one queue for every class; MC_BP_TAIL_PER_CLASS=1:
-// each class's own, queued on its stream right after its class kernel (class c's queue region starts
-// at the voxels of the classes before it, k_bp_dq_bases), so that they run while the other classes
-// still compute.  Measured at C3 (profiles/r04/r4e_tail_ab.jsonl): the group 4.45 ms joined against
-// 4.53 ms per class, so the joined tail stays the default.
-static bool bp_tail_per_class()
+// The k-NN ring search (k_bp_knn_ring) and the statistics / survivors (k_bp_denoise_tail) of every LDS
+// class, once after the classes join, over one queue (queued per class behind each class kernel they
+// measured 2 % slower at C3: the concurrent ring searches competed with the remaining classes,
+// profiles/r04/r4e_tail_ab.jsonl)
+void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int ncap, int *st, const mc::BpDev &dv)
 {
-    const char *e = getenv("MC_BP_TAIL_PER_CLASS");  // read per call (the tests switch it)
-    return e && atoi(e) != 0;
-}
-
-void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int cls_lo, int cls_hi, int ncap, int *st, const mc::BpDev &dv)
-{
-    const int q = bp_tail_per_class() ? cls_lo : 0;
-    static const int ring_wgs = getenv("MC_BP_RING_WGS") ? std::max(1, atoi(getenv("MC_BP_RING_WGS"))) : 8;  // per CU (A/B knob)
-    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * ring_wgs), dim3(256), 0, s, st + BS_DQ + q,
-                       ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), dv, ctx->d_acc.as<double4>(),
-                       ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_slot_grid.as<double>(),
-                       ctx->d_avg.as<double>(), st + BS_DQB + q);
-    hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * (bp_tail_per_class() ? 2 : 4)), dim3(256), 0, s,
-                       st + BS_CLS, ctx->d_cls_list.as<int>(), ncap, cls_lo, cls_hi, ctx->d_slot_pix.as<int>(),
+    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ,
+                       ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_slot_m.as<int>(), dv,
+                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
+                       ctx->d_slot_grid.as<double>(), ctx->d_avg.as<double>(), st + BS_DNERR);
+    hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * 4), dim3(256), 0, s,
+                       st + BS_CLS, ctx->d_cls_list.as<int>(), ncap, 0, mc::kBpClasses, ctx->d_slot_pix.as<int>(),
                        ctx->d_slot_m.as<int>(), dv, ctx->d_vpts.as<double>(), ctx->d_avg.as<double>(),
                        ctx->d_ssidx.as<int>(), ctx->d_qpts.as<float>(), ctx->d_slot_ns.as<int>(),
                        ctx->d_slot_box.as<float>());
@@ -1925,18 +1914,15 @@ template <int N>
 void bp_denoise_class(mc_ctx *ctx, hipStream_t s, int cls, int ncap, int *st, const mc::BpDev &dv)
 {
     using C = mc::BpLdsClass<N>;
-    const bool own = bp_tail_per_class();
     // the classes run concurrently: each has its own region of per-workgroup neighbour lists
-    static const int oversub = getenv("MC_BP_OVERSUB_RT") ? std::max(1, atoi(getenv("MC_BP_OVERSUB_RT"))) : kBpOversub;
-    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * oversub), dim3(C::T), 0, s, st + BS_CLS + cls,
+    hipLaunchKernelGGL(mc::k_bp_denoise_lds<N>, dim3(ctx->num_cu * C::kWgPerCu * kBpOversub), dim3(C::T), 0, s, st + BS_CLS + cls,
                        ctx->d_cls_list.as<int>() + static_cast<size_t>(cls) * ncap, st + BS_TK + cls,
                        ctx->d_slot_pix.as<int>(), ctx->d_slot_nv.as<int>(), dv, ctx->d_vpts.as<double>(),
                        ctx->d_nbl.as<unsigned short>() + nbl_offset(ctx, cls), ctx->d_lean.as<int>() + lean_offset(ctx, cls),
                        ctx->d_slot_m.as<int>(), ctx->d_avg.as<double>(), ctx->d_ssidx.as<int>(),
                        ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
-                       ctx->d_vx_pvid.as<int>(), st + BS_DQ + (own ? cls : 0), st + BS_DQB + (own ? cls : 0),
-                       ctx->d_slot_grid.as<double>());
-    if (own) bp_denoise_tail_launch(ctx, s, cls, cls + 1, ncap, st, dv);
+                       ctx->d_vx_pvid.as<int>(), st + BS_DQ, static_cast<int>(std::min<size_t>(ctx->bp_px_cap, INT_MAX)),
+                       ctx->d_slot_grid.as<double>(), st + BS_DNERR);
 }
 // MC_BP_DEBUG_SYNC=1: synchronise and report after every S1 group (diagnostics of a stalled batch)
 void bp_debug_sync(hipStream_t s, const char *what)
@@ -2370,10 +2356,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
                                    ctx->d_vox_order.as<int>());
                 hipLaunchKernelGGL(mc::k_bp_classify, dim3(64), dim3(256), 0, s, st + BS_NS, ctx->d_slot_nv.as<int>(),
-                                   ctx->d_vox_order.as<int>(), ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>(),
-                                   st + BS_CLSVOX);
-                hipLaunchKernelGGL(mc::k_bp_dq_bases, dim3(1), dim3(64), 0, s, st + BS_CLSVOX, st + BS_DQB,
-                                   bp_tail_per_class() ? 1 : 0);
+                                   ctx->d_vox_order.as<int>(), ncap, min_cls, st + BS_CLS, ctx->d_cls_list.as<int>());
                 // the few slots beyond the LDS classes run on the side stream, beside the classes
                 MC_HIP(hipEventRecord(ctx->ev_fork, s));
                 MC_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
@@ -2400,9 +2383,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                     MC_HIP(hipStreamWaitEvent(s, ctx->ev_cls[c], 0));
                 }
                 MC_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
-                // (MC_BP_TAIL_JOINED) the deferred points' ring search, then every LDS-class slot's
-                // statistics and survivors, once after the join
-                if (!bp_tail_per_class()) bp_denoise_tail_launch(ctx, s, 0, mc::kBpClasses, ncap, st, dv);
+                // the deferred points' ring search, then every LDS-class slot's statistics and survivors
+                bp_denoise_tail_launch(ctx, s, ncap, st, dv);
                 bp_debug_sync(s, "bp_denoise");
             }
             {
@@ -2434,6 +2416,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                                   "IndexError at utils/mask_backprojection.py:100)"};
             }
             MC_REQUIRE(!(hs[BS_VOXERR] & 2), MC_ERR_HIP, "voxel hash table not empty at slot start (internal error)");
+            MC_REQUIRE(hs[BS_DNERR] == 0, MC_ERR_HIP,
+                       "denoise: k-NN ring-search queue " + std::string(hs[BS_DNERR] & 1 ? "entry" : "region") +
+                           " out of range (internal error)");
             MC_REQUIRE(hs[BS_VOXERR] == 0, MC_ERR_UNSUPPORTED, "voxel index beyond 2^21 per axis");
             if (hs[BS_OVF]) {  // neighbour sets overflowed tmp: grow and redo the batch
                 tmp_cap = static_cast<size_t>(hs[BS_TOP]) + (static_cast<size_t>(hs[BS_TOP]) >> 1) + 1024;

@@ -72,22 +72,9 @@ __device__ __forceinline__ int scene_cell(float v, float inv)
 }
 
 // (a1, u1): Open3D create_from_depth_image + transform, in double, no FMA
-#ifndef MC_FAST_FLOORDIV
-#define MC_FAST_FLOORDIV 0  // 1: floor(a / b) of cell / voxel indices from a * (1 / b) unless that is within a
-                            //    margin of an integer (then the division): the same integers (A/B knob)
-#endif
-// floor(a / b) for the cell and voxel indices: a * inv_b differs from the rounded quotient by a few
-// ulps, so its floor is the quotient's unless it lies within 1e-12 |q| + 1e-12 of an integer, where
-// the division itself decides
-__device__ __forceinline__ double floor_div(double a, double b, double inv_b)
-{
-    if (!MC_FAST_FLOORDIV) return floor(a / b);
-    const double q = a * inv_b;
-    const double f = floor(q);
-    const double m = 1e-12 * fabs(q) + 1e-12;
-    if (q - f > m && (f + 1.0) - q > m) return f;
-    return floor(a / b);
-}
+// floor(a / b) of the cell and voxel indices, the division rounded as Open3D's (a reciprocal multiply
+// with an exact fallback near integers measured no faster: the indices are not what the kernels wait on)
+__device__ __forceinline__ double floor_div(double a, double b) { return floor(a / b); }
 
 __device__ __forceinline__ void bp_world(const double *__restrict__ K, const double *__restrict__ T, int u, int v,
                                          float d, double &ox, double &oy, double &oz)
@@ -580,20 +567,6 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
-#ifndef MC_KNN_CULL
-#define MC_KNN_CULL 1  // ring search: skip cells no nearer than the current k-th distance (0: A/B baseline)
-#endif
-#ifndef MC_ABLATE_VX
-#define MC_ABLATE_VX 0  // timing-only builds (results wrong): 1 = no 3. and 4., 2 = no 4.
-#endif
-#ifndef MC_VX_FUSED_RANK
-#define MC_VX_FUSED_RANK 0  // 1: every pixel's stable rank within its voxel taken in 1. (ballot groups, waves in
-                            //    order, beside the first-occurrence numbering), so 3. is a plain scatter (A/B knob)
-#endif
-#ifndef MC_VX_RECOMPUTE
-#define MC_VX_RECOMPUTE 0  // 1: no staged world points; 1. re-derives them in pixel order, 3. lists pixel
-                           //    indices and 4. re-derives its points from one depth gather each (A/B knob)
-#endif
 constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
 // tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
 // (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
@@ -601,14 +574,6 @@ constexpr int kVxH = 6144, kVxV = 4096;      // first tier: LDS hash entries (lo
 constexpr int kVxH2 = 12288, kVxV2 = 8192;   // second tier
 constexpr unsigned kVxEmpty = ~0u;
 
-
-__device__ __forceinline__ void vx_point(const unsigned *__restrict__ pl, const float *__restrict__ dep,
-                                         const double *__restrict__ K, const double *__restrict__ T, int W, int k,
-                                         double &x, double &y, double &z)
-{
-    const unsigned i = pl[k];
-    bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], x, y, z);
-}
 
 template <int kVxH, int kVxV>
 __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
@@ -632,7 +597,6 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
-    const double inv_vs = 1.0 / pr.vs;
     for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
         const int s = order[idx];
         if (force_fb) {  // test knob: every slot to the global-hash kernel
@@ -669,7 +633,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                     bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
-                        if (!MC_VX_RECOMPUTE) pp[3 * k + c] = p[c];
+                        pp[3 * k + c] = p[c];
                         mn[c] = fmin(mn[c], p[c]);
                     }
                 }
@@ -686,19 +650,12 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             const int k = c0 + t;
             int h = -1;
             if (k < n) {
-                double p[3];
-                if (MC_VX_RECOMPUTE) {
-                    vx_point(pl, dep, K, T, W, k, p[0], p[1], p[2]);
-                } else {
-                    p[0] = pp[3 * k];
-                    p[1] = pp[3 * k + 1];
-                    p[2] = pp[3 * k + 2];
-                }
+                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
                 unsigned key = 0;
                 bool fits = true;
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    const double r = floor_div(p[c] - vmin[c], pr.vs, inv_vs);
+                    const double r = floor_div(p[c] - vmin[c], pr.vs);
                     fits = fits && r >= 0.0 && r < 1024.0;
                     key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
                 }
@@ -732,41 +689,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 else s_flag = 1;
             }
             __syncthreads();
-            if (MC_VX_FUSED_RANK) {
-                // the pixel's rank within its voxel: lanes grouped by voxel, the groups' cursors advanced
-                // wave by wave (pixel order), packed with the voxel id (13 bits) for the scatter in 3.
-                int v = -1;
-                if (h >= 0) {
-                    const unsigned vv = hval[h] >> 16;
-                    if (vv < static_cast<unsigned>(kVxV)) v = static_cast<int>(vv);
-                }
-                int rank = 0, leader = 0, cnt = 0;
-                unsigned long long act = __ballot(v >= 0);
-                while (act) {
-                    const int L = __ffsll(static_cast<long long>(act)) - 1;
-                    const int vv = __shfl(v, L, 64);
-                    const unsigned long long m = __ballot(v == vv);
-                    if (v == vv) {
-                        rank = __popcll(m & ((1ull << lane) - 1ull));
-                        leader = L;
-                        cnt = __popcll(m);
-                    }
-                    act &= ~m;
-                }
-#pragma unroll
-                for (int w = 0; w < NW; w++) {
-                    if (wv == w && v >= 0 && lane == leader) {
-                        gb[w][lane] = vcur[v];
-                        vcur[v] += cnt;
-                    }
-                    lds_barrier();
-                }
-                if (v >= 0) {
-                    const int rk = gb[wv][leader] + rank;
-                    if (rk >= (1 << 18)) s_flag = 1;  // v | rk << 13 stays a non-negative int
-                    else pvid[base + k] = v | (rk << 13);
-                }
-            } else if (h >= 0) {
+            if (h >= 0) {
                 const unsigned v = hval[h] >> 16;
                 if (v < static_cast<unsigned>(kVxV)) {
                     pvid[base + k] = static_cast<int>(v);
@@ -795,15 +718,8 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         __syncthreads();
         // 3. stable scatter: list positions in pixel order within every voxel
-        if (MC_VX_FUSED_RANK) {  // the ranks are known: a plain scatter
-            for (int k = t; k < (MC_ABLATE_VX == 1 ? 0 : n); k += kVxT) {
-                const int pv = pvid[base + k];
-                vlist[base + vcur[pv & 0x1FFF] + (pv >> 13)] = MC_VX_RECOMPUTE ? static_cast<int>(pl[k]) : k;
-            }
-        }
-        int vnext = (!MC_VX_FUSED_RANK && t < n) ? pvid[base + t] : -1;  // the next chunk's ids stay in
-                                                                          // flight across the LDS-only barriers
-        for (int c0 = 0; c0 < (MC_ABLATE_VX == 1 || MC_VX_FUSED_RANK ? 0 : n); c0 += kVxT) {
+        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the LDS-only barriers
+        for (int c0 = 0; c0 < n; c0 += kVxT) {
             const int k = c0 + t;
             const int v = vnext;
             vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
@@ -828,44 +744,15 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
                 }
                 lds_barrier();
             }
-            if (v >= 0) vlist[base + gb[wv][leader] + rank] = MC_VX_RECOMPUTE ? static_cast<int>(pl[k]) : k;
+            if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
         }
         sync_global();  // 4. reads the lists other waves wrote
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
-        for (int v = t; v < (MC_ABLATE_VX ? 0 : nv); v += kVxT) {
-            // (vcur = list ends after the ordered scatter, list starts after the fused ranks)
-            const int b0 = MC_VX_FUSED_RANK ? vcur[v] : (v ? vcur[v - 1] : 0);
-            const int b1 = MC_VX_FUSED_RANK ? (v + 1 < nv ? vcur[v + 1] : n) : vcur[v];
+        for (int v = t; v < nv; v += kVxT) {
+            const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
             const int *vl = vlist + base;
             double ax = 0.0, ay = 0.0, az = 0.0;
             int j = b0;
-            if (MC_VX_RECOMPUTE) {  // the list holds pixel indices: one depth gather per point
-                for (; j + 4 <= b1; j += 4) {
-                    unsigned iv[4];
-                    float dv[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) iv[u] = static_cast<unsigned>(vl[j + u]);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) dv[u] = dep[iv[u]];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        double x, y, z;
-                        bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], x, y, z);
-                        ax = ax + x;
-                        ay = ay + y;
-                        az = az + z;
-                    }
-                }
-                for (; j < b1; j++) {
-                    const unsigned i = static_cast<unsigned>(vl[j]);
-                    double x, y, z;
-                    bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], x, y, z);
-                    ax = ax + x;
-                    ay = ay + y;
-                    az = az + z;
-                }
-                j = b1;
-            }
             for (; j + 4 <= b1; j += 4) {
                 const double *q[4];
 #pragma unroll
@@ -1297,9 +1184,6 @@ struct BpLdsClass;
 #endif
 // kLean: 0 = everything in LDS; 1 = one bucket per point, sort/rank/label/statistics arrays in global
 // scratch; 2 = also the neighbour counts and the union-find array in global scratch
-#ifndef MC_BP_LEAN2048
-#define MC_BP_LEAN2048 0
-#endif
 template <>
 struct BpLdsClass<512> {
     static constexpr int T = 256, kWgPerCu = MC_BP_WG512, kLean = 0;
@@ -1313,7 +1197,7 @@ struct BpLdsClass<1024> {
 #endif
 template <>
 struct BpLdsClass<2048> {
-    static constexpr int T = MC_BP_TBIG, kWgPerCu = MC_BP_LEAN2048 ? 2 : 1, kLean = MC_BP_LEAN2048;
+    static constexpr int T = MC_BP_TBIG, kWgPerCu = 1, kLean = 0;
 };
 template <>
 struct BpLdsClass<3072> {
@@ -1612,6 +1496,17 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
 #ifndef MC_DBG_CHECK
 #define MC_DBG_CHECK 0
 #endif
+#ifndef MC_DBG_NOINLINE
+#define MC_DBG_NOINLINE 0  // 1: the checks as calls (their spills misplaced by the compiler: DESIGN.md §4)
+#endif
+#ifndef MC_DBG_PRINT
+#define MC_DBG_PRINT 1     // 0: failures counted only (no device printf)
+#endif
+#if MC_DBG_NOINLINE
+#define MC_DBG_FN __device__ __noinline__
+#else
+#define MC_DBG_FN __device__ __forceinline__
+#endif
 __device__ unsigned long long g_bp_dbg[8];
 __device__ unsigned g_bp_dbg_printed;
 // (diagnostics build) which step produced each kept point's k-NN mean, by batch pixel index base + rank:
@@ -1626,7 +1521,7 @@ __device__ __forceinline__ void bp_dbg_path(size_t i, unsigned code)
 __device__ __forceinline__ bool bp_dbg_fail(int kind)
 {
     atomicAdd(&g_bp_dbg[kind], 1ull);
-    return atomicAdd(&g_bp_dbg_printed, 1u) < 16u;
+    return MC_DBG_PRINT && atomicAdd(&g_bp_dbg_printed, 1u) < 16u;
 }
 __device__ __forceinline__ unsigned long long bp_dbg_mix(unsigned long long k)
 {
@@ -1636,7 +1531,7 @@ __device__ __forceinline__ unsigned long long bp_dbg_mix(unsigned long long k)
     return k ^ (k >> 32);
 }
 template <int N>
-__device__ __noinline__ void bp_dbg_lists(const BpLdsGrid &g, const int *sflag, const unsigned short *nbw, int n,
+MC_DBG_FN void bp_dbg_lists(const BpLdsGrid &g, const int *sflag, const unsigned short *nbw, int n,
                                           const BpDev &pr, int slot)
 {
     for (int q = threadIdx.x; q < n; q += blockDim.x) {
@@ -1671,7 +1566,7 @@ __device__ __noinline__ void bp_dbg_lists(const BpLdsGrid &g, const int *sflag, 
     sync_global();
 }
 template <int N>
-__device__ __noinline__ void bp_dbg_union(const BpLdsGrid &g, const int *spar, int n, const BpDev &pr, int slot)
+MC_DBG_FN void bp_dbg_union(const BpLdsGrid &g, const int *spar, int n, const BpDev &pr, int slot)
 {
     for (int q = threadIdx.x; q < n; q += blockDim.x) {
         const int ra = spar[q];
@@ -1689,7 +1584,7 @@ __device__ __noinline__ void bp_dbg_union(const BpLdsGrid &g, const int *spar, i
     sync_global();
 }
 // (in k_bp_denoise_tail, a wave per slot) kept point of rank r: original index sx[r], mean av[r]
-__device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, const double *av, int m, int kk, int slot,
+MC_DBG_FN void bp_dbg_knn_tail(const double *P, const int *sx, const double *av, int m, int kk, int slot,
                                              int base)
 {
     for (int r = lane_id(); r < m; r += 64) {
@@ -1719,8 +1614,7 @@ __device__ __noinline__ void bp_dbg_knn_tail(const double *P, const int *sx, con
 // class (tests: every class gives the same results).  cls_cnt[kBpClasses + 1] must be zero.
 __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS, const int *__restrict__ slot_nv,
                                                      const int *__restrict__ order, int cap, int min_cls,
-                                                     int *__restrict__ cls_cnt, int *__restrict__ cls_list,
-                                                     int *__restrict__ cls_vox)
+                                                     int *__restrict__ cls_cnt, int *__restrict__ cls_list)
 {
     // slots taken in k_bp_vox_order's largest-first order, so each class's list (its ticket order)
     // starts with its largest slots (roughly: the workgroups append concurrently) and the class
@@ -1741,10 +1635,6 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
             if (lane_id() == leader) base = atomicAdd(&cls_cnt[k], __popcll(b));
             base = __shfl(base, leader, 64);
             if (live && c == k) cls_list[k * cap + base + __popcll(b & ((1ull << lane_id()) - 1))] = s;
-            if (k < kBpClasses) {  // the class's voxels: the size of its ring-search queue region
-                const int vs = wave_sum(live && c == k ? n : 0);
-                if (lane_id() == leader) atomicAdd(&cls_vox[k], vs);
-            }
         }
     }
 }
@@ -1759,19 +1649,6 @@ __global__ __launch_bounds__(256) void k_bp_classify(const int *__restrict__ dNS
 // kept points of a point with >= 20 kept eps-neighbours are among them (every other point is at
 // distance >= eps).  Workgroups take slots of their size class from a ticket counter.
 // ---------------------------------------------------------------------------------------------
-#ifndef MC_KNN_RING
-#define MC_KNN_RING 1  // 0: points whose eps list holds < k kept points skip the grid rings (whole-cloud scan)
-#endif
-#ifndef MC_ABLATE_BP
-#define MC_ABLATE_BP 0  // timing-only builds (results wrong): 1 = no kNN, 2 = no DBSCAN union
-#endif
-#ifndef MC_BP_KNN_LATE_INIT
-#define MC_BP_KNN_LATE_INIT 0  // 1: the k-NN list pass loads its point and sets up the k best after the list walk (A/B)
-#endif
-#ifndef MC_BP_FUSED_UNION
-#define MC_BP_FUSED_UNION 1  // union every pair while the lists are built; the separate union pass only for
-                             // slots with a non-core point that has neighbours (0: A/B baseline)
-#endif
 
 template <int N>
 __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsClass<N>::T / 256) void k_bp_denoise_lds(
@@ -1779,7 +1656,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     const int *__restrict__ slot_pix, const int *__restrict__ slot_nv, BpDev pr, const double *__restrict__ vpts,
     unsigned short *__restrict__ nbl, int *__restrict__ lean_scr, int *__restrict__ slot_m, double *__restrict__ gavg,
     int *__restrict__ gsx, double4 *__restrict__ grec, int *__restrict__ gbs, int *__restrict__ gitem,
-    int *__restrict__ dq, int *__restrict__ dq_cnt, const int *__restrict__ dq_base, double *__restrict__ slot_grid)
+    int *__restrict__ dq, int *__restrict__ dq_cnt, int dq_cap, double *__restrict__ slot_grid, int *__restrict__ err)
 {
     constexpr int T = BpLdsClass<N>::T;
     constexpr int NW = T / 64;
@@ -1820,7 +1697,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
     int *ccnt = sB + N;
     int *sfb = sB;  // kNN fallback list after the class filter (sB is free by then)
     const int cnt_cls = *cls_cnt;
-    const double inv_ce = 1.0 / pr.ce;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     unsigned short *nbw = nbl + static_cast<size_t>(blockIdx.x) * N * kBpNbCap;
     // one array for the list words of every walk (union, labels, k-NN): the compiler keeps a
@@ -1884,7 +1760,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         for (int i = t; i < n; i += T) {
             int c3[3];
 #pragma unroll
-            for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor_div(P[3 * i + c] - mn[c], pr.ce, inv_ce));
+            for (int c = 0; c < 3; c++) c3[c] = static_cast<int>(floor_div(P[3 * i + c] - mn[c], pr.ce));
             const unsigned b = mod_mul(bp_hash3(c3[0], c3[1], c3[2]), g.nb);
             sX[i] = static_cast<int>(b);
             atomicAdd(&sB[b], 1);
@@ -1911,9 +1787,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const int b = sX[i];
             const int q = sA[b] + atomicSub(&sB[b], 1) - 1;
             const double x = P[3 * i], y = P[3 * i + 1], z = P[3 * i + 2];
-            const unsigned long long ck = pack3(static_cast<int>(floor_div(x - mn[0], pr.ce, inv_ce)),
-                                                static_cast<int>(floor_div(y - mn[1], pr.ce, inv_ce)),
-                                                static_cast<int>(floor_div(z - mn[2], pr.ce, inv_ce)));
+            const unsigned long long ck = pack3(static_cast<int>(floor_div(x - mn[0], pr.ce)),
+                                                static_cast<int>(floor_div(y - mn[1], pr.ce)),
+                                                static_cast<int>(floor_div(z - mn[2], pr.ce)));
             spt[q] = make_double4(x, y, z, __longlong_as_double(static_cast<long long>(ck)));
             sorig[q] = static_cast<short>(i);
             spos[i] = static_cast<short>(q);
@@ -1933,7 +1809,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) {
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
-                lds_eps_pairs<N, MC_BP_FUSED_UNION != 0>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
+                lds_eps_pairs<N, true>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
                                                           spar);
             }
             sync_global();  // the lists hold other waves' stores
@@ -1949,13 +1825,13 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         bar();
         BP_STAMP(21);
         if constexpr (MC_DBG_CHECK) bp_dbg_lists<N>(g, sflag, nbw, n, pr, s);
-        // 6. connected core points.  Where the pair pass already united every pair (MC_BP_FUSED_UNION)
+        // 6. connected core points.  Where the pair pass already united every pair
         //    that union is the core-point union unless a non-core point has neighbours (every pair then
         //    joins two core points; an isolated point joins nothing), so only such slots run the pass
         //    below, from a fresh forest.  The pass: list points first; points with more than nbcap
         //    neighbours are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
         bool need_union = true;
-        if constexpr (!kBpLean2<N> && MC_BP_FUSED_UNION != 0) {
+        if constexpr (!kBpLean2<N>) {
             if (t == 0) s_ndef = 0;
             bar();
             for (int q = t; q < n; q += T) {
@@ -1974,7 +1850,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
         bar();
         for (int q = t; q < n; q += T) {
             const int fl = sflag[q], cnt = nb_cnt(fl);
-            if (MC_ABLATE_BP == 2 || cnt < pr.minpts) continue;
+            if (cnt < pr.minpts) continue;
             if (cnt > pr.nbcap) {
                 sX[atomicAdd(&s_ndef, 1)] = q;
                 continue;
@@ -2134,10 +2010,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const int fl = sflag[q];
             if (!(fl & (1 << 30))) continue;
             const int r = spar[q];
-#if MC_ABLATE_BP == 1
-            mavg[r] = 1.0;
-            continue;
-#endif
             const int cnt = nb_cnt(fl);
             if (kk != kBpKnnMax) {
                 sfb[atomicAdd(&sfb[kFbCount], 1)] = r;
@@ -2148,7 +2020,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 continue;
             }
             double best[kBpKnnMax];
-#if !MC_BP_KNN_LATE_INIT
             const double4 a = spt[q];
             auto d2of = [&](const double4 &p) {
                 const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
@@ -2156,7 +2027,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             };
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-#endif
             // selection pass: the kept candidates inside three radii (bit k of m1 / m2 / m3 = slot k),
             // from the entries' radius classes; if >= k of them lie inside radius i, the k nearest are
             // among those (every other kept candidate is farther than >= k others), so only they are
@@ -2176,15 +2046,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     });
             const int found = __popcll(mall);
             unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
-#if MC_BP_KNN_LATE_INIT  // (the point and the k best only from here: not live across the list walk)
-            const double4 a = spt[q];
-            auto d2of = [&](const double4 &p) {
-                const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                return ((ex * ex) + (ey * ey)) + (ez * ez);
-            };
-#pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-#endif
             if (found >= kk) {
                 const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
                 auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)] & kNbPos); };
@@ -2239,10 +2100,14 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int i = t; i < n; i += T) gr[i] = spt[i];
             int *gb = gbs + 2 * static_cast<size_t>(base) + s;
             for (int b = t; b <= NBK * n; b += T) gb[b] = sA[b];
-            // the class's queue region holds one entry per voxel of its slots (k_bp_classify), so it cannot fill
-            if (t == 0) s_slot = *dq_base + atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
+            // the queue holds at most one entry per voxel of the batch, so a pixel-sized array cannot
+            // fill; a region past its end is an internal error, reported (BS_DNERR) instead of written
+            if (t == 0) s_slot = atomicAdd(dq_cnt, nd);  // (s_slot is read again only after the next ticket)
             bar();
             const int e0 = s_slot;
+            if (e0 > dq_cap - nd) {
+                if (t == 0) atomicOr(err, 2);
+            } else
             for (int f = t; f < nd; f += T) {
                 const int q = sring[f];
                 dq[e0 + f] = s;
@@ -2279,14 +2144,14 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 // distance skipped: a's offsets in its cell, gaps shrunk by 1e-9 ce so the bound stays below every
 // point's computed distance); a point the rings cannot settle (sparse) scans every kept point.
 __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_cnt, const int *__restrict__ dq,
-                                                     const int *__restrict__ slot_pix, BpDev pr,
-                                                     const double4 *__restrict__ grec, const int *__restrict__ gbs,
-                                                     const int *__restrict__ gitem, const double *__restrict__ slot_grid,
-                                                     double *__restrict__ gavg, const int *__restrict__ dq_base)
+                                                     const int *__restrict__ slot_pix, const int *__restrict__ slot_m,
+                                                     BpDev pr, const double4 *__restrict__ grec,
+                                                     const int *__restrict__ gbs, const int *__restrict__ gitem,
+                                                     const double *__restrict__ slot_grid, double *__restrict__ gavg,
+                                                     int *__restrict__ err)
 {
-    const int ne = *dq_cnt, e0 = *dq_base;  // this queue's entries: [e0, e0 + ne)
-    for (int f0 = blockIdx.x * 256 + threadIdx.x; f0 < ne; f0 += gridDim.x * 256) {
-        const int f = e0 + f0;
+    const int ne = *dq_cnt;
+    for (int f = blockIdx.x * 256 + threadIdx.x; f < ne; f += gridDim.x * 256) {
         const int s = dq[f];
         const int base = slot_pix[s];
         const double *gm = slot_grid + 8 * static_cast<size_t>(s);
@@ -2301,6 +2166,11 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
         {
             const int item = gitem[f];
             const int q = item & 0x3FFF, r = item >> 14;
+            // an entry outside its slot (a broken hand-off from the class kernel) is reported, not followed
+            if (q >= n || r < 0 || r >= slot_m[s]) {
+                atomicOr(err, 1);
+                continue;
+            }
             const double4 a = g.pt[q];
             double best[kBpKnnMax];
 #pragma unroll
@@ -2326,7 +2196,7 @@ __global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_
                         const int step = (edge || R == 0) ? 1 : 2 * R;
                         const double gyz = gap(dy, oy) * gap(dy, oy) + gap(dz, oz) * gap(dz, oz);
                         for (int dx = -R; dx <= R; dx += step) {
-                            if (MC_KNN_CULL && gyz + gap(dx, ox) * gap(dx, ox) >= best[kBpKnnMax - 1]) continue;
+                            if (gyz + gap(dx, ox) * gap(dx, ox) >= best[kBpKnnMax - 1]) continue;
                             lds_cell(g, x + dx, y + dy, z + dz, kKeptBit, a.x, a.y, a.z, take);
                         }
                     }
@@ -2907,17 +2777,6 @@ __global__ __launch_bounds__(256) void k_bp_emit(const int *__restrict__ dNS, co
 // instead of a pageable host-to-device copy at every batch start)
 // ring-search queue regions: class c's entries start at the voxels of the classes before it
 // (per_class 0: one region for every class, at 0)
-__global__ __launch_bounds__(64) void k_bp_dq_bases(const int *__restrict__ cls_vox, int *__restrict__ dq_base, int per_class)
-{
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int c = 0; c < kBpClasses; c++) {
-            dq_base[c] = per_class ? acc : 0;
-            acc += cls_vox[c];
-        }
-    }
-}
-
 __global__ __launch_bounds__(64) void k_bp_stat_init(int *__restrict__ st, int n)
 {
     for (int i = threadIdx.x; i < n; i += 64) st[i] = i == 0 ? INT_MAX : 0;

@@ -165,36 +165,41 @@ def test_end_to_end_matches_oracle(ctx):
     assert_matches(run.canonical(), want)
 
 
-@pytest.mark.parametrize("min_cls", [1, 2, 3, 4, 5, 6])
-def test_denoise_size_classes_agree(ctx, monkeypatch, min_cls):
-    """Every denoise size class (LDS 512/1024/2048 points, the lean 3072- and 4096-point classes,
-    the 16384-point class with every array in global scratch, the global-memory kernel) gives the
-    same masks: all slots forced into class >= min_cls."""
+def _check_golden(ctx, name):
+    """the reference's own glue output (tests/golden/make_s1_golden.py) for fixture `name`"""
+    z = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    col, lab, off, pts = _run(ctx, z["in_scene"], z["in_depth"], z["in_seg"], z["in_intrinsics"], z["in_poses"])
+    fo = z["out_frame_off"]
+    np.testing.assert_array_equal(lab, z["out_labels"], err_msg=name)
+    np.testing.assert_array_equal(np.diff(fo), np.bincount(col, minlength=len(fo) - 1), err_msg=name)
+    np.testing.assert_array_equal(off, z["out_off"], err_msg=name)
+    np.testing.assert_array_equal(pts, z["out_pts"], err_msg=name)
+
+
+def _check_dense(ctx):
+    """the dense inputs against their references: the s1_dense fixture against the reference's glue,
+    the 360x480 frames against the CPU restatement (every statistics column and every mask)"""
     from maskclustering_amd.synthetic_frames import make_frames_shape
-    fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
-    a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
-    sa = ctx.bp_candidates()
+    _check_golden(ctx, "s1_dense")
+    _check_against_oracle(ctx, make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3))
+
+
+@pytest.mark.parametrize("min_cls", [1, 2, 3, 4, 5, 6])
+def test_denoise_size_classes_match_oracle(ctx, monkeypatch, min_cls):
+    """Every denoise size class (LDS 512/1024/2048 points, the lean 3072- and 4096-point classes,
+    the 16384-point class with every array in global scratch, the global-memory kernel), all slots
+    forced into class >= min_cls, against the oracle and the reference's glue fixture."""
     monkeypatch.setenv("MC_BP_MIN_CLASS", str(min_cls))
-    b = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
-    np.testing.assert_array_equal(sa, ctx.bp_candidates())
-    for x, y in zip(a, b):
-        np.testing.assert_array_equal(x, y)
+    _check_dense(ctx)
 
 
 @pytest.mark.parametrize("tier", [1, 2])
-def test_voxel_kernels_agree(ctx, monkeypatch, tier):
+def test_voxel_kernels_match_oracle(ctx, monkeypatch, tier):
     """voxel_down_sample's kernels (the LDS tier every slot starts in; the larger LDS tier and the
-    global-hash kernel it hands overflowing slots to) give the same voxels: every slot forced onto
-    the global kernel (tier 1) or the second LDS tier (tier 2)."""
-    from maskclustering_amd.synthetic_frames import make_frames_shape
-    fr = make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3)
-    a = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
-    sa = ctx.bp_candidates()
+    global-hash kernel it hands overflowing slots to), every slot forced onto the global kernel
+    (tier 1) or the second LDS tier (tier 2), against the oracle and the reference's glue fixture."""
     monkeypatch.setenv("MC_VX_GLOBAL", str(tier))
-    b = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
-    np.testing.assert_array_equal(sa, ctx.bp_candidates())
-    for x, y in zip(a, b):
-        np.testing.assert_array_equal(x, y)
+    _check_dense(ctx)
 
 
 def test_high_resolution_frame_matches_oracle(ctx):
@@ -247,49 +252,22 @@ def _dense_inputs():
 
 
 @pytest.mark.parametrize("nbcap", [1, 8, 24, 63])
-def test_list_overflow_paths_agree(ctx, monkeypatch, nbcap):
+def test_list_overflow_paths_match_oracle(ctx, monkeypatch, nbcap):
     """The eps-neighbour lists are read only for counts <= nbcap; every longer list takes the cell-walk
     paths of the union, the border labels and the k-NN ring search.  Forcing the cap down sends most
-    points (nbcap 1, 8) or the dense ones (24, 63) down those paths, in every size class: the masks must
-    not change.  (A list whose count passed the cap holds an atomic-order-dependent subset, so a
-    consumer reading one would show here as a run-dependent difference.)"""
-    for inp in _dense_inputs():
-        want = _run(ctx, *inp)
-        sa = ctx.bp_candidates()
-        for min_cls in ("0", "2", "5"):
-            monkeypatch.setenv("MC_BP_NBCAP", str(nbcap))
-            monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
-            got = _run(ctx, *inp)
-            np.testing.assert_array_equal(sa, ctx.bp_candidates(), err_msg=f"nbcap {nbcap} class {min_cls}")
-            for x, y in zip(want, got):
-                np.testing.assert_array_equal(x, y)
-            monkeypatch.delenv("MC_BP_NBCAP")
-            monkeypatch.delenv("MC_BP_MIN_CLASS")
-
-
-@pytest.mark.parametrize("env", [("MC_BP_TAIL_PER_CLASS", "1"), ("MC_BP_TAIL_PER_CLASS", "0")])
-def test_ring_queue_modes_agree(ctx, monkeypatch, env):
-    """The k-NN ring-search queue: one joined queue (default) and per class (MC_BP_TAIL_PER_CLASS=1:
-    each class's ring search and statistics queued behind its class kernel, in a region sized by the
-    class's voxels) give the same masks, in every size class."""
-    for inp in _dense_inputs():
-        want = _run(ctx, *inp)
-        sa = ctx.bp_candidates()
-        for min_cls in ("0", "2", "5"):
-            monkeypatch.setenv(*env)
-            monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
-            got = _run(ctx, *inp)
-            np.testing.assert_array_equal(sa, ctx.bp_candidates(), err_msg=f"{env} class {min_cls}")
-            for x, y in zip(want, got):
-                np.testing.assert_array_equal(x, y)
-            monkeypatch.delenv(env[0])
-            monkeypatch.delenv("MC_BP_MIN_CLASS")
+    points (nbcap 1, 8) or the dense ones (24, 63) down those paths, in every size class: the results
+    must still equal the oracle and the reference's glue fixture."""
+    for min_cls in ("0", "2", "5"):
+        monkeypatch.setenv("MC_BP_NBCAP", str(nbcap))
+        monkeypatch.setenv("MC_BP_MIN_CLASS", min_cls)
+        _check_dense(ctx)
 
 
 def test_repeated_runs_identical(ctx):
     """Run-to-run determinism of the concurrent size classes (their lists are built with LDS-atomic
     slots, so any read of a slot before its store lands would vary between runs): the dense inputs
-    six times each, every run bit-identical to the first."""
+    against their references, then six more times each, every run bit-identical to the first."""
+    _check_dense(ctx)
     for inp in _dense_inputs():
         want = _run(ctx, *inp)
         sa = ctx.bp_candidates()
