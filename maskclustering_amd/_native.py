@@ -286,7 +286,7 @@ class SetOrder:
         finally:
             self.close()
         if rc != MC_OK:
-            raise McError(rc, "mc_setorder_finish: inconsistent levels / edges")
+            raise McError(rc, "mc_setorder_finish: inconsistent levels / edges, or a negative point id")
         k = K.value
         out = dict(mask_off=mo[:k + 1], mask_order=mord[:N0], pt_off=oo[:k + 1], pts=opts[:int(oo[k])],
                    son_off=so[:k + 1], son_order=sord[:NL])

@@ -32,6 +32,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 namespace mcso {
 
 constexpr size_t kLinearProbes = 9;
@@ -345,10 +347,30 @@ class SharedPool {
     std::unique_ptr<Pool> pool_;
     int n_ = 0;
 };
+// One per process: a forked child inherits the parent's pool object (its n_ matching, its mutex
+// possibly held by a parent thread) but none of its worker threads, so a child that finds the
+// creating process's pid replaces it with a fresh pool and leaks the inherited one (joining threads
+// that do not exist, or waiting on a mutex no thread will release, would hang).
 inline SharedPool &shared_pool()
 {
-    static SharedPool *p = new SharedPool;  // never destroyed: idle workers end with the process
-    return *p;
+    static std::atomic<SharedPool *> p{nullptr};
+    static std::atomic<pid_t> owner{0};
+    static std::mutex mk;
+    const pid_t me = getpid();
+    SharedPool *cur = p.load(std::memory_order_acquire);
+    if (cur && owner.load(std::memory_order_acquire) == me) return *cur;
+    // first use, or the first use in a forked child: only the forking thread runs in the child, so
+    // the inherited creation mutex may be held; a new one is taken instead of it
+    static std::mutex *mkp = &mk;
+    if (cur && owner.load() != me) mkp = new std::mutex;  // (leaked: the child's first use only)
+    std::lock_guard<std::mutex> g(*mkp);
+    cur = p.load(std::memory_order_acquire);
+    if (!cur || owner.load() != me) {
+        cur = new SharedPool;  // never destroyed: idle workers end with the process
+        owner.store(me, std::memory_order_release);
+        p.store(cur, std::memory_order_release);
+    }
+    return *cur;
 }
 
 }  // namespace mcso
@@ -388,13 +410,24 @@ inline void build_level0(mc_setorder *h, const int64_t *node_start, const int64_
 {
     try {
         const int N0 = h->n0;
-        std::atomic<int> next{0};
+        std::atomic<int> next{0}, bad{0};
         auto work = [&]() {
-            // chunks of 64 nodes: fewer shared-counter round trips than one node at a time
+            // chunks of 64 nodes: fewer shared-counter round trips than one node at a time; each node's
+            // ids are checked by the worker that builds it (a negative id is not a scene point)
             for (int c = next.fetch_add(64); c < N0; c = next.fetch_add(64))
-                for (int i = c; i < std::min(N0, c + 64); i++) h->sets[i] = from_sequence(pts + node_start[i], node_len[i]);
+                for (int i = c; i < std::min(N0, c + 64); i++) {
+                    const int32_t *q = pts + node_start[i];
+                    bool ok = true;
+                    for (int64_t k = 0; k < node_len[i]; k++) ok &= q[k] >= 0;
+                    if (!ok) {
+                        bad.store(1, std::memory_order_relaxed);
+                        continue;
+                    }
+                    h->sets[i] = from_sequence(q, node_len[i]);
+                }
         };
         shared_pool().run(h->nth, work);
+        if (bad.load()) h->rc = MC_ERR_INVALID;
     } catch (const std::bad_alloc &) {
         h->rc = MC_ERR_HIP;
     }
@@ -407,11 +440,10 @@ extern "C" int mc_setorder_begin(int32_t num_nodes, const int64_t *node_start, c
 {
     if (!out || num_nodes < 0 || (num_nodes && (!node_start || !node_len))) return MC_ERR_INVALID;
     *out = nullptr;
-    for (int i = 0; i < num_nodes; i++) {
+    // O(num_nodes) range checks here; the ids themselves are checked by build_level0's workers (an
+    // O(total points) loop on the caller's thread would sit on the critical path the async build hides)
+    for (int i = 0; i < num_nodes; i++)
         if (node_start[i] < 0 || node_len[i] < 0 || (node_len[i] && !pts)) return MC_ERR_INVALID;
-        for (int64_t k = 0; k < node_len[i]; k++)
-            if (pts[node_start[i] + k] < 0) return MC_ERR_INVALID;
-    }
     try {
         auto *h = new mc_setorder;
         h->n0 = num_nodes;

@@ -125,15 +125,54 @@ class ShardedGraph:
     # ---- edges of the clustering run (for the reference's container orders) -----------------
     def set_edge_capture(self, capacity):
         self.ctx.set_edge_capture(capacity)
+        self._edge_cap = int(capacity)
 
-    def edges(self):
+    def _local_edges(self):
+        """this rank's capture, or None when it overflowed the capacity (MC_ERR_UNSUPPORTED)"""
+        from ._native import McError, MC_ERR_UNSUPPORTED
+        try:
+            return self.ctx.edges()
+        except McError as e:
+            if e.code != MC_ERR_UNSUPPORTED:
+                raise
+            return None
+
+    def _any_rank(self, flag):
+        """max of an int over the ranks (every rank must call it)"""
+        t = torch.tensor([int(flag)], dtype=torch.int64, device=self.comm_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def cluster_with_edges(self, connect_threshold, thresholds=None, capacity=1 << 20):
+        """cluster() with every iteration's edges captured: a rank whose capture overflowed makes every
+        rank grow the capacity (to the edges found, all-reduced) and re-run S6 on the same level-0
+        nodes, so no rank enters edges()' collectives with a failed capture.  Returns edges()."""
+        cap = int(capacity)
+        while True:
+            self.set_edge_capture(cap)
+            self.cluster(connect_threshold, thresholds)
+            local = self._local_edges()
+            need = self._any_rank(0 if local is not None else 2 * cap)
+            if need == 0:
+                return self.edges(_local=local)
+            cap = need
+
+    def edges(self, _local=None):
         """Every iteration's edges as (t, a, b) int64 arrays sorted by (t, a, b), the same on every
         rank: iteration 0's come from the ranks' pair rows (each rank captured its own rows' edges,
-        all-gathered here), the later iterations ran replicated (this rank's capture)."""
+        all-gathered here), the later iterations ran replicated (this rank's capture).  A rank whose
+        capture overflowed its capacity makes every rank raise (checked before any exchange, so no
+        rank waits in a collective the failed one never joins); cluster_with_edges grows instead."""
         import numpy as np
-        tt, aa, bb = self.ctx.edges()
+        from ._native import McError, MC_ERR_UNSUPPORTED
+        local = _local if _local is not None else self._local_edges()
         if self.world == 1:
-            return tt, aa, bb
+            if local is None:
+                raise McError(MC_ERR_UNSUPPORTED, "edge capture overflowed its capacity")
+            return local
+        if self._any_rank(local is None):
+            raise McError(MC_ERR_UNSUPPORTED, "edge capture overflowed its capacity on a rank")
+        tt, aa, bb = local
         z = tt == 0
         key = ((aa[z] << 24) | bb[z]).astype(np.int64)
         n = torch.tensor([len(key)], dtype=torch.int64, device=self.comm_dev)

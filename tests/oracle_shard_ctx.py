@@ -54,6 +54,9 @@ class OracleShardCtx:
         a0, b0 = self.e0 >> 32, self.e0 & 0xffffffff
         k = self.later
         key = np.sort(np.concatenate([(a0.astype(np.uint64) << np.uint64(24)) | b0.astype(np.uint64), k]))
+        if getattr(self, "ovf", False) or len(key) > self.cap:  # an overflowed capture (mc_cluster_get_edges)
+            from maskclustering_amd._native import McError, MC_ERR_UNSUPPORTED
+            raise McError(MC_ERR_UNSUPPORTED, "edge capture overflowed its capacity")
         return ((key >> np.uint64(48)).astype(np.int64), ((key >> np.uint64(24)) & np.uint64(0xFFFFFF)).astype(np.int64),
                 (key & np.uint64(0xFFFFFF)).astype(np.int64))
 
@@ -230,8 +233,8 @@ class OracleShardCtx:
             n = L.orcs_edge_sink_count() if self.cap else 0
         finally:
             L.orcs_set_edge_sink(None, 0)
-        assert n <= self.cap or not self.cap, "edge capture overflow"
-        k = sink[:n]   # iteration t of this call is iteration t + 1 of the run
+        self.ovf = bool(self.cap) and n > self.cap  # (the library keeps the first cap edges and reports it)
+        k = sink[:min(n, self.cap)]   # iteration t of this call is iteration t + 1 of the run
         self.later = ((((k >> np.uint64(48)) + np.uint64(1)) << np.uint64(48)) | (k & np.uint64((1 << 48) - 1))).astype(np.uint64)
         self.parts = [lab0] + [labels[t, :sizes1[t]].copy() for t in range(T1)]
         self.sizes = np.concatenate([[N0], sizes1]).astype(np.int32)

@@ -114,6 +114,29 @@ def main():
             po, seqs = c.level0_sequences()
             o = _native.setorder_replay(c.sizes[:T], eo, aa, bb, po, seqs, labels=True)
             np.savez(out, **o)
+        elif mode.startswith("overflow:"):
+            # a capture too small on some rank: edges() must raise on every rank (checked before any
+            # exchange), not leave the other ranks waiting in a collective; then the grow-and-rerun path
+            from maskclustering_amd._native import McError
+            from maskclustering_amd.synthetic import make_shape
+            _, shape, seed, cfg = mode.split(":")
+            s = make_shape(shape, seed=int(seed))
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+            run = OracleRun()
+            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            sh.graph.set_edge_capture(2 if rank == 0 else 1 << 20)
+            sh.set_local_masks(col, lab, off, torch.from_numpy(pts))
+            sh.step(**CFGS[cfg])
+            raised = 0
+            try:
+                sh.graph.edges()
+            except McError:
+                raised = 1
+            sh.graph.set_edge_capture(1 << 20)  # grown on every rank, and the run repeated
+            sh.step(**CFGS[cfg])
+            tt, aa, bb = sh.graph.edges()
+            np.savez(out, raised=np.array([raised]), tt=tt, aa=aa, bb=bb)
         elif mode.startswith("skew:"):
             from maskclustering_amd.synthetic import make_shape
             _, shape, seed = mode.split(":")

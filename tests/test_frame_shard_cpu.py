@@ -149,3 +149,14 @@ def test_sharded_reference_orders_equal_single_process(tmp_path, world, shape, s
         got = np.load(out)
         for k in ref:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_sharded_edges_overflow_raises_on_every_rank(tmp_path):
+    """Rank 0's edge capture overflows (capacity 2): edges() must raise on every rank before any
+    exchange (the other ranks would otherwise wait in the all-gather rank 0 never joins), and with the
+    capacity grown every rank gets the same gathered edges."""
+    outs = [np.load(o) for o in run_ranks("overflow:c1:1:scannet", 2, tmp_path)]
+    assert [int(o["raised"][0]) for o in outs] == [1, 1]
+    for k in ("tt", "aa", "bb"):
+        np.testing.assert_array_equal(outs[0][k], outs[1][k])
+    assert len(outs[0]["tt"]) > 2

@@ -205,7 +205,39 @@ def test_begin_finish_on_csr_rows(async_build):
 def test_begin_rejects_bad_ranges_and_frees_unfinished():
     with pytest.raises(ValueError):
         _native.SetOrder([0], [5], np.arange(3, dtype=np.int32))
-    with pytest.raises(_native.McError):
-        _native.SetOrder([0], [2], np.array([1, -1], np.int32))
+    with pytest.raises(_native.McError):  # a negative id: found by the build's workers, reported by finish
+        _native.SetOrder([0], [2], np.array([1, -1], np.int32)).finish([1], np.zeros(2, np.int64),
+                                                                       np.zeros(0, np.int32), np.zeros(0, np.int32))
     so = _native.SetOrder([0, 2], [2, 1], np.arange(3, dtype=np.int32))
     so.close()  # never finished: the background build is joined and released
+
+
+def test_replay_in_forked_child():
+    """The process-wide worker pool after fork(): a child inherits the pool object but not its threads;
+    a replay in the child must build its own pool and finish (it hung in done_.wait before)."""
+    import os
+    rng = np.random.default_rng(11)
+    seqs = [np.unique(rng.choice(5000, int(rng.integers(1, 60)), replace=False)).astype(np.int32) for _ in range(300)]
+    levels = _levels(rng, len(seqs), 3, 0.9)
+    want = _native_run(levels, seqs, threads=4)  # the parent's pool now exists, with live workers
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # child: same replay, exit status = equal or not
+        os.close(r)
+        code = 1
+        try:
+            got = _native_run(levels, seqs, threads=4)
+            code = 0 if all(np.array_equal(want[k], got[k]) for k in want) else 2
+        finally:
+            os.write(w, bytes([code]))
+            os._exit(code)
+    os.close(w)
+    import select
+    ready, _, _ = select.select([r], [], [], 60)
+    if not ready:
+        os.kill(pid, 9)
+        os.waitpid(pid, 0)
+        pytest.fail("replay in the forked child did not finish within 60 s")
+    code = os.read(r, 1)
+    os.waitpid(pid, 0)
+    assert code == bytes([0]), code
