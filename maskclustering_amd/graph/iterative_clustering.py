@@ -153,8 +153,14 @@ def _level0_sequences(h):
     rows = np.fromiter((row_of[src.keys[g]] for g in node0.tolist()), np.int64, count=len(node0))
     lens = off[rows + 1] - off[rows]
     made = getattr(mpc, "_made", {})
-    for k, v in made.items():                     # a set read and changed in place by the caller
-        if len(v) != off[row_of[k] + 1] - off[row_of[k]]:
+    for k, v in made.items():                     # a set read (and maybe changed in place) by the caller
+        r = row_of[k]
+        row = pts[off[r]:off[r + 1]]
+        if len(v) != len(row):
+            return None
+        # same length: the same ids in the same iteration order as the set(ascending ids) the replay
+        # builds, else the caller's history (a remove and an add, say) decides the order: Python replay
+        if list(v) != list(set(np.asarray(row).tolist())):
             return None
     return off[rows], lens, np.asarray(pts)
 

@@ -115,3 +115,25 @@ def test_merged_node_points_made_on_first_read():
     assert "_point_ids" not in n.__dict__
     assert n.point_ids == {5, 9, 11} and n.point_ids is n.point_ids
     assert n.mask_list == [(0, 1), (10, 2)] and n.node_info == (3, 0) and n.son_node_info == {(2, 0)}
+
+
+def test_level0_sequences_detects_same_length_edits():
+    """A materialised level-0 set changed in place to the same length (one id removed, another added)
+    must send iterative_clustering to the Python replay (the native one would rebuild the set from the
+    CSR row and ignore the edit); untouched and read-only sets keep the native path."""
+    import types
+    from maskclustering_amd.graph.iterative_clustering import _level0_sequences
+    pts = np.array([1, 4, 9, 2, 3, 7, 8], np.int32)
+    off = np.array([0, 3, 7], np.int64)
+    row_of = {"a": 0, "b": 1}
+    mpc = types.SimpleNamespace(csr=(row_of, off, pts), _made={})
+    h = types.SimpleNamespace(src=types.SimpleNamespace(mpc=mpc, keys=["a", "b"]), node0=np.array([0, 1]))
+    st, ln, pp = _level0_sequences(h)
+    np.testing.assert_array_equal(st, [0, 3])
+    np.testing.assert_array_equal(ln, [3, 4])
+    mpc._made["b"] = {2, 3, 7, 8}                 # read, unchanged
+    assert _level0_sequences(h) is not None
+    mpc._made["b"] = {2, 3, 7, 100}               # same length, one id replaced
+    assert _level0_sequences(h) is None
+    mpc._made["b"] = {2, 3, 7}                    # shorter
+    assert _level0_sequences(h) is None
