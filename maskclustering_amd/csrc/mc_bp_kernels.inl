@@ -1174,6 +1174,7 @@ constexpr int kBpLdsN = 16384;  // largest class of the LDS-kernel template
 constexpr int kBpClasses = 6;   // classes 512, 1024, 2048, 3072, 4096, 16384; class kBpClasses = k_bp_denoise
 constexpr int kBpStreamClasses = 5;  // classes with a stream of their own (the 16384 class shares the side stream)
 constexpr int kBpNbCap = 64;  // eps-neighbour list entries per point (self included); more -> cell walk
+constexpr int kBpKnnBatch = 4;  // k-NN list pass: selected entries fetched per batch
 template <int N>
 struct BpLdsClass;
 #ifndef MC_BP_WG512
@@ -1339,7 +1340,8 @@ __device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
 // last slot (the list is unused then: the point walks its cells).  Returns the count.
 template <int N>
 __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
-                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q)
+                                            const BpDev &pr, unsigned short *__restrict__ nbw, int q, int &farA,
+                                            int &farB)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
@@ -1354,7 +1356,10 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
         if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
-            nb_put<N>(nbw, q, min(cnt, kBpNbCap - 1), static_cast<unsigned>(q2) | (nb_class(d2, pr) << 14));
+            const unsigned c = nb_class(d2, pr);
+            nb_put<N>(nbw, q, min(cnt, kBpNbCap - 1), static_cast<unsigned>(q2) | (c << 14));
+            if (c == 3u) farA = q2;  // far neighbours: the sampled links of the union (step 6)
+            if (c == 2u) farB = q2;
             cnt++;
         }
     };
@@ -1383,10 +1388,10 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 // counter returns (sflag[] holds the counts, self entries already in slot 0).  Half the candidate
 // records of lds_eps_list; the slot order within a list is arbitrary, which no consumer depends on
 // (the union and the border labels are order-free, the k-NN sorts).
-template <int N, bool kUnite>
+template <int N>
 __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
                                               const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag,
-                                              int *spar)
+                                              int *farA, int *farB)
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
@@ -1396,7 +1401,7 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
     };
     const double eps2 = pr.eps2;
-    int ra = kUnite ? uf_find_s(spar, q) : 0;
+    int fa = q, fb = q;
     auto visit = [&](const double4 &p, int q2, unsigned long long key) {
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
@@ -1405,16 +1410,10 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
             const int o1 = atomicAdd(&sflag[q], 1), o2 = atomicAdd(&sflag[q2], 1);
             if (o1 < kBpNbCap) nb_put<N>(nbw, q, o1, static_cast<unsigned>(q2) | c);
             if (o2 < kBpNbCap) nb_put<N>(nbw, q2, o2, static_cast<unsigned>(q) | c);
-            if constexpr (kUnite) {  // speculative: every pair, as if both points were core
-                const int p2 = ld_wg(spar + q2);
-                if (p2 != ra) {
-                    const int rb = uf_find_s(spar, p2);
-                    if (rb != ra) {
-                        uf_unite_s(spar, ra, rb);
-                        ra = uf_find_s(spar, ra);
-                    }
-                }
-            }
+            // far neighbours of this point's forward walk (radius classes 3 and 2): the union's sampled
+            // links (step 6), stored once after the walk
+            fa = c == (3u << 14) ? q2 : fa;
+            fb = c == (2u << 14) ? q2 : fb;
         }
     };
     unsigned long long nkey = 0;
@@ -1433,6 +1432,8 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         }
         if (q2 < e) visit(g.pt[q2], q2, key);
     }
+    farA[q] = fa;
+    farB[q] = fb;
 }
 
 // the uint4 words of sorted position q's first cnt slots, all issued together; the others zero
@@ -1497,7 +1498,8 @@ __device__ __forceinline__ void unpack3(unsigned long long k, int &x, int &y, in
 #define MC_DBG_CHECK 0
 #endif
 #ifndef MC_DBG_NOINLINE
-#define MC_DBG_NOINLINE 0  // 1: the checks as calls (their spills misplaced by the compiler: DESIGN.md §4)
+#define MC_DBG_NOINLINE 1  // 0: the checks inlined (which of the two builds clean depends on the source:
+                           //    scripts/build_variant.sh rejects one with misplaced spills)
 #endif
 #ifndef MC_DBG_PRINT
 #define MC_DBG_PRINT 1     // 0: failures counted only (no device printf)
@@ -1809,8 +1811,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             for (int q = t; q < n; q += T) {
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
-                lds_eps_pairs<N, true>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag,
-                                                          spar);
+                lds_eps_pairs<N>(g, x, y, z, spt[q].x, spt[q].y, spt[q].z, pr, nbw, q, sflag, sX, slab);
             }
             sync_global();  // the lists hold other waves' stores
         } else {
@@ -1818,62 +1819,89 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                 int x, y, z;
                 unpack3(keyof(q), x, y, z);
                 const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
-                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q);
+                int fa = q, fb = q;
+                sflag[q] = lds_eps_list<N>(g, x, y, z, ax, ay, az, pr, nbw, q, fa, fb);
                 spar[q] = q;
+                sX[q] = fa;
+                slab[q] = fb;
             }
         }
         bar();
         BP_STAMP(21);
         if constexpr (MC_DBG_CHECK) bp_dbg_lists<N>(g, sflag, nbw, n, pr, s);
-        // 6. connected core points.  Where the pair pass already united every pair
-        //    that union is the core-point union unless a non-core point has neighbours (every pair then
-        //    joins two core points; an isolated point joins nothing), so only such slots run the pass
-        //    below, from a fresh forest.  The pass: list points first; points with more than nbcap
-        //    neighbours are deferred (into sX, free here) and walk their cells afterwards, all lanes busy
-        bool need_union = true;
-        if constexpr (!kBpLean2<N>) {
-            if (t == 0) s_ndef = 0;
-            bar();
-            for (int q = t; q < n; q += T) {
-                const int cnt = nb_cnt(sflag[q]);
-                if (cnt >= 2 && cnt < pr.minpts) s_ndef = 1;
-            }
-            bar();
-            need_union = s_ndef != 0;
-            if (need_union) {
-                for (int q = t; q < n; q += T) spar[q] = q;
-                bar();
+        // 6. connected core points, Afforest-style (Sutton et al., SC'18): (a) every core point links to
+        //    three sampled core neighbours: its first list entry and two far ones of its own list walk
+        //    (radius classes 3 and 2, kept in sX / slab, free between the scatter and the labels: links
+        //    that span the eps ball percolate where the nearest few stay in clumps; sampling the first
+        //    two entries left most points outside the giant, 63 us per C3 slot against 12);
+        //    (b) the component most of a sample of core points
+        //    fell into (a slot is mostly one surface patch: ~98 % of its points) is taken as the giant;
+        //    (c) only core points outside it unite with all their core neighbours (list, or the 27 cells
+        //    for a list past nbcap).  Every core-core edge is then covered: one with an end outside the
+        //    giant is processed by that end (the lists are symmetric), one inside joins nothing new.
+        //    The partition is the core-point connectivity whatever the union order (union-find, min
+        //    roots); the pair pass measured 58 of its 131 us per slot uniting every pair speculatively.
+        if (t == 0) s_ndef = 0;
+        for (int q = t; q < n; q += T) {
+            if (nb_cnt(sflag[q]) < pr.minpts) continue;
+            const uint4 w0 = reinterpret_cast<const uint4 *>(nbw)[q];  // slots 0..7 (slot 0: self in pair lists)
+            const int cand[3] = {static_cast<int>(((w0.x >> 16) & 0xFFFFu) & kNbPos), sX[q], slab[q]};
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const int q2 = cand[r];
+                if (q2 != q && q2 < n && nb_cnt(sflag[q2]) >= pr.minpts) uf_unite_s(spar, q, q2);
             }
         }
-        if (need_union) {
-        if (t == 0) s_ndef = 0;
         bar();
-        for (int q = t; q < n; q += T) {
-            const int fl = sflag[q], cnt = nb_cnt(fl);
-            if (cnt < pr.minpts) continue;
-            if (cnt > pr.nbcap) {
-                sX[atomicAdd(&s_ndef, 1)] = q;
-                continue;
+        if (t < 64) {  // wave 0: the most frequent root among 64 core points spread over the slot
+            const int q = static_cast<int>((static_cast<long long>(t) * n) >> 6);
+            const int r = (q < n && nb_cnt(sflag[q]) >= pr.minpts) ? uf_find_s(spar, q) : -1;
+            int best = -1, bestc = 0;
+            unsigned long long act = __ballot(r >= 0);
+            while (act) {
+                const int L = __ffsll(static_cast<long long>(act)) - 1;
+                const int rr = __shfl(r, L, 64);
+                const unsigned long long m = __ballot(r == rr);
+                const int c = __popcll(m);
+                if (c > bestc) {
+                    bestc = c;
+                    best = rr;
+                }
+                act &= ~m;
             }
-            int ra = uf_find_s(spar, q);
-            nb_load<N>(nbw, q, cnt, w);
-            // the next entry's count and union-find parent are loaded before this one's find (a parent
-            // read early is still a node of q2's component, so it is a valid place to start the find)
-            nb_walk(w, cnt,
-                    [&](unsigned e) {  // only the entries the union takes (q2 < q) are loaded
-                        const int q2 = static_cast<int>(e & kNbPos);
-                        return q2 < q ? make_int2(sflag[q2], ld_wg(spar + q2)) : make_int2(0, 0);
-                    },
-                    [&](int, unsigned e, int2 fp) {
-                        const int q2 = static_cast<int>(e & kNbPos);
-                        if (q2 < q && nb_cnt(fp.x) >= pr.minpts && fp.y != ra) {  // parent == root: joined already
-                            const int rb = uf_find_s(spar, fp.y);
-                            if (rb != ra) {  // most edges of a dense cluster are already joined
-                                uf_unite_s(spar, ra, rb);
-                                ra = uf_find_s(spar, ra);
+            if (t == 0) s_slot = best;  // (s_slot is free until the next ticket)
+        }
+        bar();
+        {
+            const int giant = s_slot;
+            for (int q = t; q < n; q += T) {
+                const int cnt = nb_cnt(sflag[q]);
+                if (cnt < pr.minpts) continue;
+                int ra = uf_find_s(spar, q);
+                if (giant >= 0 && ra == uf_find_s(spar, giant)) continue;
+                if (cnt > pr.nbcap) {
+                    sX[atomicAdd(&s_ndef, 1)] = q;
+                    continue;
+                }
+                nb_load<N>(nbw, q, cnt, w);
+                // the next entry's count and union-find parent are loaded before this one's find (a parent
+                // read early is still a node of q2's component, so it is a valid place to start the find)
+                nb_walk(w, cnt,
+                        [&](unsigned e) {
+                            const int q2 = static_cast<int>(e & kNbPos);
+                            return make_int2(sflag[q2], ld_wg(spar + q2));
+                        },
+                        [&](int, unsigned e, int2 fp) {
+                            const int q2 = static_cast<int>(e & kNbPos);
+                            if (q2 != q && nb_cnt(fp.x) >= pr.minpts && fp.y != ra) {  // parent == root: joined already
+                                const int rb = uf_find_s(spar, fp.y);
+                                if (rb != ra) {
+                                    uf_unite_s(spar, ra, rb);
+                                    ra = uf_find_s(spar, ra);
+                                }
                             }
-                        }
-                    });
+                        });
+            }
         }
         bar();
         for (int f = t; f < s_ndef; f += T) {
@@ -1883,7 +1911,7 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const double ax = spt[q].x, ay = spt[q].y, az = spt[q].z;
             int ra = uf_find_s(spar, q);
             lds_cells27(g, x, y, z, 0ull, ax, ay, az, [&](int q2, double d2) {
-                if (d2 < pr.eps2 && q2 < q && nb_cnt(sflag[q2]) >= pr.minpts) {
+                if (d2 < pr.eps2 && q2 != q && nb_cnt(sflag[q2]) >= pr.minpts) {
                     const int rb = uf_find_s(spar, q2);
                     if (rb != ra) {
                         uf_unite_s(spar, ra, rb);
@@ -1893,7 +1921,6 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             });
         }
         bar();
-        }  // need_union
         BP_STAMP(22);
         // 7. roots; every component keyed by its smallest original index; clusters ranked by it
         {
@@ -2048,13 +2075,30 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
             if (found >= kk) {
                 const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
-                auto entry = [&](int k) { return static_cast<int>(lst[static_cast<size_t>(k >> 3) * 8 * N + (k & 7)] & kNbPos); };
-                double4 nxt = pm ? spt[entry(__ffsll(static_cast<long long>(pm)) - 1)] : make_double4(0.0, 0.0, 0.0, 0.0);
-                while (pm) {
-                    pm &= pm - 1;
-                    const double4 p = nxt;
-                    if (pm) nxt = spt[entry(__ffsll(static_cast<long long>(pm)) - 1)];
-                    sorted_insert(best, d2of(p));
+                // the selected entries' positions are reloaded from the list (a lane-varying slot index
+                // cannot read the register copy), kBpKnnBatch at a time, the next batch's loads in flight
+                // while this batch's points are inserted: the lists live past the L2 (one region per
+                // workgroup), and one load in flight per lane left the pass waiting on every entry
+                auto fetch = [&](int (&e)[kBpKnnBatch]) {
+#pragma unroll
+                    for (int u = 0; u < kBpKnnBatch; u++) {
+                        const int b = pm ? __ffsll(static_cast<long long>(pm)) - 1 : -1;
+                        pm &= pm - 1;
+                        e[u] = b >= 0 ? static_cast<int>(lst[static_cast<size_t>(b >> 3) * 8 * N + (b & 7)]) : -1;
+                    }
+                };
+                int en[kBpKnnBatch];
+                fetch(en);
+                while (en[0] >= 0) {
+                    double d2[kBpKnnBatch];
+#pragma unroll
+                    for (int u = 0; u < kBpKnnBatch; u++) {
+                        const double4 p = spt[en[u] >= 0 ? en[u] & kNbPos : q];
+                        d2[u] = en[u] >= 0 ? d2of(p) : DBL_MAX;
+                    }
+                    fetch(en);
+#pragma unroll
+                    for (int u = 0; u < kBpKnnBatch; u++) sorted_insert(best, d2[u]);
                 }
             }
 #ifdef MC_BP_STAMPS

@@ -9,4 +9,12 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -Wall "$@" \
     -o "maskclustering_amd/libmcgraph_${name}.so" maskclustering_amd/csrc/mc_api.hip
+# the same flags' device code must hold no spill store before an EXEC restore (such a
+# build computes wrong results); a failing variant is removed rather than left to be run
+if ! python3 scripts/spill_exec_check.py --build "$@" k_ > "/tmp/spill_check_${name}.txt"; then
+    cat "/tmp/spill_check_${name}.txt" >&2
+    rm -f "maskclustering_amd/libmcgraph_${name}.so"
+    echo "spill placement check failed for ${name}: try other flags (e.g. -DMC_DBG_NOINLINE=0/1, -DMC_DBG_PRINT=0)" >&2
+    exit 1
+fi
 echo "maskclustering_amd/libmcgraph_${name}.so"

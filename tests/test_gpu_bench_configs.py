@@ -10,8 +10,8 @@ the C-ABI against the CPU oracle, bit for bit:
   frame's S1 against the oracle's, then S2-S6 against the sparse oracle (oracle/graph_sparse.c) on
   that mask set.
 * ``c4``: the Matterport-region-shaped scene (BASELINE configs[3]: 2000 frames of 1280x1024, depth in
-  1/4000 m units, ~120k masks): three 16-frame windows' S1 against the oracle, then the whole scene
-  S1 -> S6 on the device with S2-S6 against the sparse oracle on the device's mask set.
+  1/4000 m units, ~120k masks): the whole scene S1 -> S6 on the device, every frame's S1 against the
+  oracle's (100 frames at a time), then S2-S6 against the sparse oracle on the device's mask set.
 
 The oracle is pinned to the reference's own outputs by tests/test_s1_oracle.py and
 tests/test_oracle_golden.py; the Open3D / pytorch3d arithmetic inside S1 is parity unpinned
@@ -73,6 +73,24 @@ def test_c2_e2e_matches_oracle():
     assert_matches(run.canonical(), want)
 
 
+def _compare_every_frame(fr, masks, stats, chunk=100):
+    """S1 of every frame of a device-resident scene (torch frames) against the oracle's, `chunk`
+    frames at a time through the host"""
+    F = fr.depth.shape[0]
+    scene = fr.scene_points.astype(np.float32)
+    col_all = masks[0]
+    for f0 in range(0, F, chunk):
+        f1 = min(F, f0 + chunk)
+        want = oracle.s1_frames(scene, fr.depth[f0:f1].cpu().numpy(), fr.seg[f0:f1].cpu().numpy(),
+                                fr.intrinsics[f0:f1], fr.poses[f0:f1])
+        g0, g1 = np.searchsorted(col_all, [f0, f1])
+        o0 = masks[2][g0]
+        sub = (col_all[g0:g1] - f0, masks[1][g0:g1], masks[2][g0:g1 + 1] - o0, masks[3][o0:masks[2][g1]])
+        st = stats[(stats[:, 0] >= f0) & (stats[:, 0] < f1)].copy()
+        st[:, 0] -= f0
+        _compare_s1(sub, st, want, range(f0, f1))
+
+
 def test_c3_s1_windows_match_oracle():
     from maskclustering_amd import _native
     from maskclustering_amd.synthetic_frames import FRAME_SHAPES, make_frames_shape
@@ -107,20 +125,7 @@ def test_c3_e2e_matches_oracle():
     ctx.backproject(None, None, None, None, _native.bp_params(), shape=(F, H, W),
                     device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), t_K.data_ptr(), t_T.data_ptr()))
     masks = ctx.bp_masks()
-    stats = ctx.bp_candidates()
-    # S1 of every frame against the oracle, 100 frames at a time through the host
-    scene = fr.scene_points.astype(np.float32)
-    col_all = masks[0]
-    for f0 in range(0, F, 100):
-        f1 = min(F, f0 + 100)
-        want = oracle.s1_frames(scene, fr.depth[f0:f1].cpu().numpy(), fr.seg[f0:f1].cpu().numpy(),
-                                fr.intrinsics[f0:f1], fr.poses[f0:f1])
-        g0, g1 = np.searchsorted(col_all, [f0, f1])
-        o0 = masks[2][g0]
-        sub = (col_all[g0:g1] - f0, masks[1][g0:g1], masks[2][g0:g1 + 1] - o0, masks[3][o0:masks[2][g1]])
-        st = stats[(stats[:, 0] >= f0) & (stats[:, 0] < f1)].copy()
-        st[:, 0] -= f0
-        _compare_s1(sub, st, want, range(f0, f1))
+    _compare_every_frame(fr, masks, ctx.bp_candidates())
     col, lab, off, pts = masks
     del fr
     torch.cuda.empty_cache()
@@ -161,8 +166,8 @@ def test_c4_s1_windows_match_oracle():
 
 
 def test_c4_e2e_matches_oracle():
-    """the whole C4 scene S1 -> S6 on the device (frames resident in HBM); the device's S1 of the
-    windows is checked above, S2-S6 here against the sparse oracle on the device's mask set"""
+    """the whole C4 scene S1 -> S6 on the device (frames resident in HBM): every frame's S1 against the
+    oracle, then S2-S6 against the sparse oracle on the device's mask set"""
     import torch
     from maskclustering_amd import _native
     from maskclustering_amd.pipeline import GraphRun
@@ -179,19 +184,11 @@ def test_c4_e2e_matches_oracle():
     F, H, W = fr.depth.shape
     ctx.backproject(None, None, None, None, _native.bp_params(), shape=(F, H, W),
                     device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), t_K.data_ptr(), t_T.data_ptr()))
-    col, lab, off, pts = ctx.bp_masks()
-    # the windows' masks equal a run over the windows alone (S1 is per frame)
-    win = _c4_frames_window()
-    sub = _native.Context(0)
-    sub.set_points(fr.scene_points.astype(np.float32))
-    idx = torch.as_tensor(win, device=dev)
-    sub.backproject(fr.depth[idx].cpu().numpy(), fr.seg[idx].cpu().numpy(), fr.intrinsics[win], fr.poses[win])
-    scol, slab, soff, spts = sub.bp_masks()
-    rows = np.nonzero(np.isin(col, win))[0]
-    np.testing.assert_array_equal(np.asarray(win)[scol], col[rows])
-    np.testing.assert_array_equal(slab, lab[rows])
-    np.testing.assert_array_equal(np.concatenate([pts[off[r]:off[r + 1]] for r in rows]), spts)
-    del fr, sub
+    masks = ctx.bp_masks()
+    # S1 of every one of the 2000 frames (1280x1024, depth in 1/4000 m) against the oracle's
+    _compare_every_frame(fr, masks, ctx.bp_candidates())
+    col, lab, off, pts = masks
+    del fr
     torch.cuda.empty_cache()
     assert len(col) > 100_000
     run.P, run.F = len(t_scene), F
