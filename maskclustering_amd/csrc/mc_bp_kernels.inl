@@ -41,6 +41,24 @@ struct BpDev {
     int vec4;  // W % 4 == 0 with a 16-byte aligned depth and a 4-byte aligned seg pointer: 4 pixels per lane
 };
 
+// Diagnostic build only (-DMC_BP_STAMPS): per-step real-time-clock (100 MHz) totals of the S1 kernels' steps, summed
+// over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
+#ifdef MC_BP_STAMPS
+__device__ unsigned long long g_bp_stamps[40];
+__device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks), last batch
+#define BP_STAMP(k)                                                                      \
+    do {                                                                                 \
+        __syncthreads();                                                                 \
+        if (threadIdx.x == 0) {                                                          \
+            const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                \
+            atomicAdd(&g_bp_stamps[k], now_ - stamp_prev);                               \
+            stamp_prev = now_;                                                           \
+        }                                                                                \
+    } while (0)
+#else
+#define BP_STAMP(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ unsigned bp_hash3(int x, int y, int z)
 {
     unsigned h = static_cast<unsigned>(x) * 0x9E3779B1u;
@@ -597,7 +615,11 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
+#ifdef MC_BP_STAMPS
+    unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
+        BP_STAMP(39);  // (the previous slot's sums, 4.)
         const int s = order[idx];
         if (force_fb) {  // test knob: every slot to the global-hash kernel
             if (t == 0) fb_list[atomicAdd(fb_cnt, 1)] = s;
@@ -641,6 +663,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the points are read by any wave in 4.
         block_minmax3_nw<NW>(mn, mx, red);
+        BP_STAMP(36);  // 0. world points + min bound
         double vmin[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
@@ -704,6 +727,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             __syncthreads();
             continue;
         }
+        BP_STAMP(37);  // 1. voxel ids, counts
         // 2. counts -> exclusive offsets
         {
             int carry = 0;
@@ -747,6 +771,7 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
             if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
         }
         sync_global();  // 4. reads the lists other waves wrote
+        BP_STAMP(38);  // 2. + 3. offsets, ordered scatter
         // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
         for (int v = t; v < nv; v += kVxT) {
             const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
@@ -1129,23 +1154,6 @@ __device__ __forceinline__ void bp_knn(const BpCells &g, const double *__restric
     }
 }
 
-// Diagnostic build only (-DMC_BP_STAMPS): per-step real-time-clock (100 MHz) totals of k_bp_denoise, summed
-// over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
-#ifdef MC_BP_STAMPS
-__device__ unsigned long long g_bp_stamps[40];
-__device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks), last batch
-#define BP_STAMP(k)                                                                      \
-    do {                                                                                 \
-        __syncthreads();                                                                 \
-        if (threadIdx.x == 0) {                                                          \
-            const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                \
-            atomicAdd(&g_bp_stamps[k], now_ - stamp_prev);                               \
-            stamp_prev = now_;                                                           \
-        }                                                                                \
-    } while (0)
-#else
-#define BP_STAMP(k) do { } while (0)
-#endif
 
 // acc + v(lane 0) + v(lane 1) + ... + v(lane 63), in lane order, skipping lanes with v <= 0 (a
 // std::accumulate step over 64 values); the lane values are read as scalars

@@ -53,6 +53,11 @@ print("k-NN points deferred to the ring search", int(buf[30]), "(list overflow",
       int(buf[33]), ")", "near-tied keys redone exactly", int(buf[31]))
 print("knn points", int(buf[13]), "candidates/point", round(float(buf[29]) / max(int(buf[13]), 1), 1),
       "fallbacks", int(buf[31]))
+vt = [float(buf[k]) for k in (36, 37, 38, 39)]
+vtot = max(sum(vt), 1.0)
+print("k_bp_voxel_lds workgroup-busy shares:", {n: f"{100 * v / vtot:.1f} %" for n, v in
+      zip(("0 world+min", "1 ids+counts", "2+3 offsets+scatter", "4 sums"), vt)},
+      "total ms", round(vtot / 1e5, 2))
 st = ctx.bp_candidates()
 for c, n in ((2, "npix"), (3, "nvox"), (4, "ndbscan"), (5, "nsor")):
     v = st[:, c]
