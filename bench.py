@@ -422,19 +422,43 @@ class ShardedEndToEndStep(EndToEndStep):
         _, H, W = fr.depth.shape
         self.F_total = F
         self.shape = (hi - lo, H, W)
+        # the scene pipeline (default; MC_BENCH_PIPELINE=1 turns it on): S1 on its own context
+        # and stream in a producer thread, S1 of scene k + 1 under the graph stages of scene k
+        # (maskclustering_amd.frame_shard.ScenePipeline); each step is still one whole scene
+        self.pipe = None
+        self.timing_ctxs = [self.ctx]
+        self.s1ctx = self.ctx
+        if os.environ.get("MC_BENCH_PIPELINE", "0") != "0":
+            from maskclustering_amd.frame_shard import ScenePipeline
+            self.s1ctx = _native.Context(local)
+            self.s1ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+            own_device_budget(self.s1ctx, 0.6 / (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
+            self.pipe = ScenePipeline(self.sh, self.s1ctx, self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
+            self.timing_ctxs = [self.ctx, self.s1ctx]
         log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
         self.workload = (f"{shape}: synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
                          f"S1-S6, frames sharded over {self.sh.world} GPU(s)")
 
     def step(self):
+        if self.pipe is not None:
+            self.pipe.run(1, **CFG)
+            return
         self.sh.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
         self.sh.step(**CFG)
+
+    def run_steps(self, n):
+        """n scenes; with the pipeline, S1 of scene k + 1 runs under the graph stages of scene k"""
+        if self.pipe is not None:
+            self.pipe.run(n, **CFG)
+            return
+        for _ in range(n):
+            self.step()
 
     def work(self):
         F, H, W = self.shape
         pts = self.sh.pts.cpu().numpy()
         w = graph_work(self.ctx, pts, self.fr.num_points, self.F_total)
-        w.update(bp_work(self.ctx, F, H, W))
+        w.update(bp_work(self.s1ctx, F, H, W))
         return w
 
     def cpu_baseline(self):
@@ -870,6 +894,11 @@ def main():
     else:  # every rank its own scene (weak scaling)
         runner = (GraphStep if args.variant == "g" else EndToEndStep)(args.shape, args.seed + rank, local)
     ctx = runner.run.ctx
+    # contexts whose group timers the line reads (the scene pipeline runs S1 on a context of its own)
+    tctxs = getattr(runner, "timing_ctxs", [ctx])
+
+    def ktime(g):  # (ms, launches) of group g from the context that ran it
+        return max((c.kernel_time(g) for c in tctxs), key=lambda v: v[1])
 
     for _ in range(args.warmup):
         runner.step()
@@ -879,12 +908,15 @@ def main():
     pairs_per_step = int(np.sum(sizes[:-1].astype(np.int64) ** 2))
 
     # calibration pass with per-group event timing: find the dominant kernel group
-    ctx.reset_kernel_times()
-    ctx.set_timing(True)
+    for c in tctxs:
+        c.reset_kernel_times()
+        c.set_timing(True)
     runner.step()
-    ctx.synchronize()
-    calib = {g: ctx.kernel_time(g) for g in runner.groups}
-    ctx.set_timing(False)
+    for c in tctxs:
+        c.synchronize()
+    calib = {g: ktime(g) for g in runner.groups}
+    for c in tctxs:
+        c.set_timing(False)
     work = runner.work()
     for g in BP_GROUPS:  # S1 models are scene totals: per launch = total / the group's launches per scene
         if g in work and calib.get(g, (0, 0))[1]:
@@ -895,21 +927,26 @@ def main():
 
     # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant
     # group only (one event pair per launch of the group, on the context stream)
-    ctx.reset_kernel_times()
-    ctx.set_timing_filter(dominant)
-    ctx.set_timing(True)
+    for c in tctxs:
+        c.reset_kernel_times()
+        c.set_timing_filter(dominant)
+        c.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner.step()
+    if hasattr(runner, "run_steps"):
+        runner.run_steps(args.steps)
+    else:
+        for _ in range(args.steps):
+            runner.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    dom_ms, dom_n = ctx.kernel_time(dominant)
+    for c in tctxs:
+        c.set_timing(False)
+    dom_ms, dom_n = ktime(dominant)
     t = torch.tensor([elapsed], dtype=torch.float64,
                      device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
@@ -1001,7 +1038,8 @@ def main():
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
                        "stage_ms": {k: round(v[0], 4) for k, v in calib.items()},
-                       "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}"},
+                       "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}",
+                       "scene_pipeline": getattr(runner, "pipe", None) is not None},
             # SURVEY.md §8(d)'s own definition of the pair metric: the same pairs over S6's time only
             "pairs_per_s_s6": round(pairs_per_step / max(s6_ms / 1e3, 1e-12), 1),
             "pairs_per_s_s6_def": "sum_t N_t^2 / sum_t (S6 iteration t's device time: s6_columns + s6_pairs + "

@@ -321,3 +321,92 @@ class FrameShardedScene:
         runner = self.graph if self.graph is not None else self.run
         runner.step(mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
                     contained_threshold)
+
+
+class ScenePipeline:
+    """A stream of scenes through one :class:`FrameShardedScene`, S1 of scene k + 1 overlapping the
+    graph stages of scene k.
+
+    S1 (this rank's frame slice) runs on its own context ``s1_ctx`` and stream, in a producer thread
+    (the library's calls release the GIL); the calling thread takes each scene's masks, gathers
+    them over the ranks (the only collectives, all issued by this thread, in the same order on every
+    rank), hands them to the graph context and runs S2-S6 there.  Per scene the work is exactly the
+    sequential path's (``FrameShardedScene.backproject`` + ``step``, the same results); only the
+    order in time changes, so that the graph stages, which run serially on every rank after the
+    gather and do not shrink with the rank count, hide under the next scene's S1.
+    The producer runs at most two scenes ahead (a bounded queue of mask sets).
+    """
+
+    def __init__(self, sh: FrameShardedScene, s1_ctx, depth: torch.Tensor, seg: torch.Tensor,
+                 intrinsics: torch.Tensor, poses: torch.Tensor, params=None):
+        n = sh.hi - sh.lo
+        if depth.shape[0] != n:
+            raise ValueError(f"rank {sh.rank} owns {n} frames [{sh.lo}, {sh.hi})")
+        self.sh, self.s1 = sh, s1_ctx
+        self.frames = (depth, seg, intrinsics, poses)
+        self.params = params
+
+    def _s1_scene(self):
+        """S1 of this rank's slice on the S1 context: (col, lab, off, point ids on the device)."""
+        depth, seg, K, T = self.frames
+        n, H, W = depth.shape
+        if n == 0:
+            return (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64),
+                    torch.zeros(1, dtype=torch.int32, device=depth.device))
+        self.s1.backproject(None, None, None, None, self.params, shape=(n, H, W),
+                            device_ptrs=(depth.data_ptr(), seg.data_ptr(), K.data_ptr(), T.data_ptr()))
+        col, lab, off = self.s1.bp_mask_index()
+        pts = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=depth.device)
+        self.s1.bp_points_to_device(pts.data_ptr())
+        self.s1.synchronize()  # the ids are complete before another stream reads them
+        return col, lab, off, pts
+
+    def run(self, num_scenes: int, on_scene=None, **step_kwargs):
+        """num_scenes scenes (each S1 -> gather -> S2-S6); on_scene(k) after scene k's graph stages
+        were issued.  Returns when the last scene's graph stages have been issued on the graph
+        context's stream (synchronize it to wait for them)."""
+        import queue
+        import threading
+        q: queue.Queue = queue.Queue(maxsize=1)
+        stop = threading.Event()
+
+        def produce():
+            try:
+                for _ in range(num_scenes):
+                    item = self._s1_scene()
+                    while not stop.is_set():
+                        try:
+                            q.put(item, timeout=0.5)
+                            break
+                        except queue.Full:
+                            continue
+                    if stop.is_set():
+                        return
+            except BaseException as e:  # handed to the consumer, which raises it
+                q.put(e)
+
+        th = threading.Thread(target=produce, name="s1-producer", daemon=True)
+        th.start()
+        sh = self.sh
+        try:
+            for k in range(num_scenes):
+                item = q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                col, lab, off, pts = item
+                if sh.world == 1:
+                    g_col, g_lab, g_off, g_pts = col, lab, off, pts
+                else:
+                    g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks)
+                sh.mask_index = (g_col, g_lab, g_off)
+                sh.pts = g_pts
+                if g_pts.device.type == "cuda":
+                    sh.run.set_masks(sh.P, sh.F, g_col, g_lab, g_off, pts_device_ptr=g_pts.data_ptr())
+                else:
+                    sh.run.set_masks(sh.P, sh.F, g_col, g_lab, g_off, g_pts.numpy())
+                sh.step(**step_kwargs)
+                if on_scene is not None:
+                    on_scene(k)
+        finally:
+            stop.set()
+            th.join()

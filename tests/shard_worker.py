@@ -114,6 +114,45 @@ def main():
             po, seqs = c.level0_sequences()
             o = _native.setorder_replay(c.sizes[:T], eo, aa, bb, po, seqs, labels=True)
             np.savez(out, **o)
+        elif mode.startswith("pipeline:"):
+            # the scene pipeline (frame_shard.ScenePipeline): S1 in a producer thread on a stand-in S1
+            # context that serves this rank's slice masks, gather + sharded S2-S6 on the oracle-backed
+            # context in this thread; three scenes, every scene's canonical outputs saved
+            import ctypes
+            from maskclustering_amd.frame_shard import ScenePipeline
+            from maskclustering_amd.synthetic import make_shape
+            _, shape, seed, cfg = mode.split(":")
+            s = make_shape(shape, seed=int(seed))
+            lo, hi = frame_slice(s.num_frames, world, rank)
+            col, lab, off, pts = local_masks(s, lo, hi)
+
+            class S1Ctx:  # the Context surface ScenePipeline reads after a back-projection
+                calls = 0
+
+                def backproject(self, *a, **kw):
+                    S1Ctx.calls += 1
+
+                def bp_mask_index(self):
+                    return col.copy(), lab.copy(), off.copy()
+
+                def bp_points_to_device(self, dst):
+                    if len(pts):
+                        ctypes.memmove(dst, pts.ctypes.data, pts.nbytes)
+
+                def synchronize(self):
+                    pass
+
+            run = OracleRun()
+            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            n = hi - lo
+            z = torch.zeros((n, 1, 1))
+            pipe = ScenePipeline(sh, S1Ctx(), z, z.to(torch.uint8), torch.zeros((n, 4), dtype=torch.float64),
+                                 torch.zeros((n, 16), dtype=torch.float64))
+            outs = {}
+            pipe.run(3, on_scene=lambda k: outs.update({f"{k}/{a}": np.asarray(b) for a, b in
+                                                        run.ctx.canonical().items()}), **CFGS[cfg])
+            outs["s1_calls"] = np.array([S1Ctx.calls])
+            np.savez(out, **outs)
         elif mode.startswith("overflow:"):
             # a capture too small on some rank: edges() must raise on every rank (checked before any
             # exchange), not leave the other ranks waiting in a collective; then the grow-and-rerun path

@@ -160,3 +160,21 @@ def test_sharded_edges_overflow_raises_on_every_rank(tmp_path):
     for k in ("tt", "aa", "bb"):
         np.testing.assert_array_equal(outs[0][k], outs[1][k])
     assert len(outs[0]["tt"]) > 2
+
+
+@pytest.mark.parametrize("world,shape,seed,cfg", [(1, "c1", 1, "scannet"), (2, "c1", 1, "scannet"),
+                                                  (4, "tiny", 5, "scannetpp")])
+def test_scene_pipeline_equals_single_process(tmp_path, world, shape, seed, cfg):
+    """The scene pipeline (S1 in a producer thread, gather + sharded S2-S6 in the calling thread, three
+    scenes): every scene on every rank ends with exactly the single-process S2-S6 outputs, and S1 ran
+    once per scene."""
+    from maskclustering_amd.synthetic import make_shape
+    from oracle import oracle
+    s = make_shape(shape, seed=seed)
+    want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, **KW[cfg])
+    for out in run_ranks(f"pipeline:{shape}:{seed}:{cfg}", world, tmp_path):
+        got = np.load(out)
+        assert int(got["s1_calls"][0]) == 3
+        for k in range(3):
+            for name in want:
+                np.testing.assert_array_equal(got[f"{k}/{name}"], np.asarray(want[name]), err_msg=f"scene {k} {name}")
