@@ -422,13 +422,14 @@ class ShardedEndToEndStep(EndToEndStep):
         _, H, W = fr.depth.shape
         self.F_total = F
         self.shape = (hi - lo, H, W)
-        # the scene pipeline (default; MC_BENCH_PIPELINE=1 turns it on): S1 on its own context
+        # the scene pipeline (default; MC_BENCH_PIPELINE=0 turns it off): S1 on its own context
         # and stream in a producer thread, S1 of scene k + 1 under the graph stages of scene k
-        # (maskclustering_amd.frame_shard.ScenePipeline); each step is still one whole scene
+        # (maskclustering_amd.frame_shard.ScenePipeline); each step is still one whole scene, and
+        # the K timed steps process K whole scenes inside the timed region
         self.pipe = None
         self.timing_ctxs = [self.ctx]
         self.s1ctx = self.ctx
-        if os.environ.get("MC_BENCH_PIPELINE", "0") != "0":
+        if os.environ.get("MC_BENCH_PIPELINE", "1") != "0":
             from maskclustering_amd.frame_shard import ScenePipeline
             self.s1ctx = _native.Context(local)
             self.s1ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)

@@ -400,6 +400,9 @@ class ScenePipeline:
                     g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks)
                 sh.mask_index = (g_col, g_lab, g_off)
                 sh.pts = g_pts
+                # set_masks copies the ids into the graph context and synchronises its stream before
+                # it returns (mc_scene_set_masks validates them on the host), so the producer's
+                # tensors, allocated on its thread's stream, are free to be reused afterwards
                 if g_pts.device.type == "cuda":
                     sh.run.set_masks(sh.P, sh.F, g_col, g_lab, g_off, pts_device_ptr=g_pts.data_ptr())
                 else:
