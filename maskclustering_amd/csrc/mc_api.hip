@@ -129,7 +129,7 @@ struct mc_ctx {
     DevBuf d_bpbm, d_tmp, d_kflag, d_ksize, d_midx, d_moff, d_out_col, d_out_label, d_out_off, d_out_pts, d_bp_pts;
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
-    DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_vx_ppt, d_bppack;
+    DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_bppack;
     DevBuf d_slot_grid;  // denoise: grid origin / extent of the slots with points queued for the k-NN ring search
     int num_cu = 256;
     int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
@@ -382,7 +382,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_kflag, &ctx->d_ksize, &ctx->d_midx, &ctx->d_moff, &ctx->d_out_col,
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
-                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_vx_ppt, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid,
+                         &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid,
                          &ctx->d_slot_grid};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy), (void)hipStreamDestroy(ctx->copy);
@@ -1760,9 +1760,9 @@ enum BpStat : int {
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
-// HBM of the per-batch S1 arrays per pixel of the batch (bp_reserve: the per-pixel arrays sum to 219 B;
+// HBM of the per-batch S1 arrays per pixel of the batch (bp_reserve: the per-pixel arrays sum to 195 B;
 // the per-slot and per-frame ones are small against them)
-constexpr size_t kBpBytesPerPixel = 224;
+constexpr size_t kBpBytesPerPixel = 200;
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
 // Workgroups per resident slot of a denoise class (the classes take slots from tickets): the extra
@@ -1836,7 +1836,6 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
         fill_u32(s, ctx->d_hfirst.ptr, 2 * px, 0x7FFFFFFFu);  // INT_MAX
         ctx->d_acc.reserve(px * 4 * 8);
         ctx->d_vx_pvid.reserve(px * 4);
-        ctx->d_vx_ppt.reserve(px * 3 * 8);
         ctx->d_vx_list.reserve(px * 4);
         ctx->d_vox_entry.reserve(px * 4);
         ctx->d_vpts.reserve(px * 3 * 8);
@@ -2331,16 +2330,16 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
                                    ctx->d_vox_order.as<int>());
                 int *fb1 = ctx->d_vx_fb.as<int>(), *fb2 = fb1 + slots_cap(FB);
-                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH, mc::kVxV>), dim3(ctx->num_cu * 2), dim3(mc::kVxT), 0, s,
+                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxT, mc::kVxH, mc::kVxV>), dim3(ctx->num_cu * 4), dim3(mc::kVxT), 0, s,
                                    st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
                                    ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
-                                   KB, TB, dv, ctx->d_vx_ppt.as<double>(), ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(), ctx->d_vpts.as<double>(),
+                                   KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(),
                                    ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
-                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxH2, mc::kVxV2>), dim3(ctx->num_cu), dim3(mc::kVxT), 0, s,
+                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxT2, mc::kVxH2, mc::kVxV2>), dim3(ctx->num_cu), dim3(mc::kVxT2), 0, s,
                                    st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
-                                   ctx->d_vx_ppt.as<double>(), ctx->d_vx_pvid.as<int>(), ctx->d_vx_list.as<int>(),
-                                   ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2, st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                                   ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2,
+                                   st + BS_VXFB2, vx_global == 1 ? 1 : 0);
                 hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB2,
                                    fb2, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
@@ -2529,9 +2528,9 @@ int mc_debug_bp_slot_times(unsigned *out, int n)
 }
 int mc_debug_bp_stamps(unsigned long long *out32)
 {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 40 * 8) != hipSuccess) return MC_ERR_HIP;
-    static const unsigned long long zero[40] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_stamps), zero, 40 * 8) == hipSuccess ? MC_OK : MC_ERR_HIP;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mc::g_bp_stamps), 48 * 8) != hipSuccess) return MC_ERR_HIP;
+    static const unsigned long long zero[48] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mc::g_bp_stamps), zero, 48 * 8) == hipSuccess ? MC_OK : MC_ERR_HIP;
 }
 #endif
 

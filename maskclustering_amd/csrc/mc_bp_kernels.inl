@@ -44,7 +44,7 @@ struct BpDev {
 // Diagnostic build only (-DMC_BP_STAMPS): per-step real-time-clock (100 MHz) totals of the S1 kernels' steps, summed
 // over slots by thread 0 of every workgroup (shares, not durations: DESIGN.md §4).
 #ifdef MC_BP_STAMPS
-__device__ unsigned long long g_bp_stamps[40];
+__device__ unsigned long long g_bp_stamps[48];
 __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks), last batch
 #define BP_STAMP(k)                                                                      \
     do {                                                                                 \
@@ -531,18 +531,23 @@ __global__ __launch_bounds__(256) void k_bp_compact(const unsigned char *__restr
 // ---------------------------------------------------------------------------------------------
 // Open3D: min bound - voxel/2, index = floor((p - vmin) / voxel), per-voxel sum in input order,
 // mean = sum / count.  Output order (u2): first occurrence in pixel order.
-// k_bp_voxel_lds (every slot, largest first): the slot's voxel hash and per-voxel counters in LDS.
-//   0. min bound (order-free block reduction)
-//   1. chunks of kVxT pixels in list order: relative voxel key (10 bits per axis) -> LDS hash; a
-//      new voxel's id = rank of its first pixel (LDS atomicMin of the lane, ordered block scan);
-//      per pixel its voxel id (global scratch), per voxel its pixel count
-//   2. counts -> list offsets (block scan)
-//   3. chunks again: every pixel to its voxel's list at a stable position (ranks within a wave by
-//      ballot groups, waves in order), so each voxel's list is in pixel order
-//   4. a thread per voxel adds its list's points in order; mean
-// Only LDS between the chunk barriers: no global atomics, no global read-modify-write chains.
-// A slot whose voxel coordinates span >= 1024 voxels on an axis or that has more than kVxV voxels
-// is listed for the next tier (the larger LDS tables, then k_bp_voxel, the global-hash kernel below).
+// k_bp_voxel_lds (every slot, largest first), one workgroup per slot, the voxel hash in LDS:
+//   0. min bound of the slot's world points (order-free block reduction; the points are not stored)
+//   1. chunks of T pixels in list order, the next chunk's pixel and depth loads in flight under this
+//      one; each pixel's world point is recomputed (bit for bit the one of 0.) and staged in LDS.
+//      Runs of consecutive pixels with the same voxel key (within a wave) are found by comparing
+//      every lane's key with the previous lane's: only a run's first pixel probes the hash.  The
+//      chunk's first pixel of every voxel it touches is found by an LDS atomicMin of the thread id in
+//      the voxel's hash entry; each run ORs its lanes into that thread's per-wave lane masks; new
+//      voxels get ids in order of their first pixel (wave counts + prefix).  Then the chunk-first
+//      thread of each voxel adds the voxel's pixels of this chunk, in pixel order (mask words in
+//      wave order, bits ascending), to the voxel's running sum (global, loaded under the masks'
+//      barrier).  Chunks run in order, so every voxel's sum is the left fold in input order that
+//      Open3D's AccumulatedPoint makes, exactly.
+//   2. a thread per voxel: mean = sum / count
+// Three barriers per chunk, no per-pixel global stores.  A slot whose voxel coordinates span >= 1024
+// voxels on an axis or that has more than V voxels is listed for the next tier (the larger LDS
+// table, then k_bp_voxel, the global-hash kernel below).
 // Largest slots first (their per-slot time grows with the pixel count): slots binned by
 // floor(4 log2(pixels)) (the top three bits of the count), bins in descending order.  One workgroup.
 __device__ __forceinline__ int vox_order_bin(int np)
@@ -573,53 +578,41 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
     for (int s = t; s < NS; s += 1024) order[atomicAdd(&cnt[vox_order_bin(slot_np[s])], 1)] = s;
 }
 
-// Workgroup barrier that orders LDS only: this wave's LDS operations complete (lgkmcnt 0), global
-// loads stay in flight (vmcnt not waited, unlike __syncthreads' fence), then s_barrier; the empty
-// asm statements keep the compiler from moving memory operations across it.  For steps whose only
-// cross-wave traffic is LDS.
-__device__ __forceinline__ void lds_barrier()
-{
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt 63 (no wait), expcnt 7, lgkmcnt 0
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
-constexpr int kVxT = 512;        // threads (= pixels per chunk) of k_bp_voxel_lds
-// tiers: <6144, 4096> (hash + counters 64 KB, two workgroups per CU) for every slot; <12288, 8192>
-// (128 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
-constexpr int kVxH = 6144, kVxV = 4096;      // first tier: LDS hash entries (load <= 2/3), voxels
-constexpr int kVxH2 = 12288, kVxV2 = 8192;   // second tier
+// tiers: <256, 3072, 2048> (32 KB of LDS, four workgroups per CU) for every slot; <512, 12288, 8192>
+// (140 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
+constexpr int kVxT = 256, kVxH = 3072, kVxV = 2048;    // first tier: threads (pixels per chunk), hash entries (load <= 2/3), voxels
+constexpr int kVxT2 = 512, kVxH2 = 12288, kVxV2 = 8192;  // second tier
 constexpr unsigned kVxEmpty = ~0u;
 
-
-template <int kVxH, int kVxV>
-__global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
-                                                       const int *__restrict__ slot_frame, const int *__restrict__ slot_np,
-                                                       const int *__restrict__ slot_pix,
-                                                       const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
-                                                       const double *__restrict__ intr, const double *__restrict__ pose,
-                                                       BpDev pr, double *__restrict__ ppt, int *__restrict__ pvid,
-                                                       int *__restrict__ vlist,
-                                                       double *__restrict__ vpts, int *__restrict__ slot_nv,
-                                                       int *__restrict__ fb_list, int *__restrict__ fb_cnt, int force_fb)
+template <int T, int H, int V>
+__global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
+                                                    const int *__restrict__ slot_frame, const int *__restrict__ slot_np,
+                                                    const int *__restrict__ slot_pix,
+                                                    const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
+                                                    const double *__restrict__ intr, const double *__restrict__ pose,
+                                                    BpDev pr, int *__restrict__ vcnt, double *__restrict__ vpts,
+                                                    int *__restrict__ slot_nv, int *__restrict__ fb_list,
+                                                    int *__restrict__ fb_cnt, int force_fb)
 {
-    constexpr int NW = kVxT / 64;
-    __shared__ unsigned hkey[kVxH];
-    __shared__ unsigned hval[kVxH];  // (voxel id << 16) | lowest lane of the chunk; 0xFFFF: none yet
-    __shared__ int vcur[kVxV];       // counts, then list cursors (end of each voxel's list after 3.)
-    __shared__ int gb[NW][64];
+    static_assert(T % 64 == 0 && T <= 1024 && V <= 0xFFFF, "chunk-first thread ids and voxel ids share 16 bits");
+    constexpr int NW = T / 64;
+    __shared__ unsigned hkey[H];
+    __shared__ unsigned hval[H];                   // (voxel id << 16) | chunk-first thread (0xFFFF: none yet)
+    __shared__ unsigned long long msk[T][NW];     // per chunk-first thread: its voxel's lanes of the chunk, by wave
+    __shared__ double psx[T], psy[T], psz[T];     // the chunk's world points
     __shared__ double red[6 * NW];
-    __shared__ int ws[NW];
+    __shared__ int wsn[NW];
     __shared__ int s_flag;
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
+    const unsigned long long below = (1ull << lane) - 1ull;
 #ifdef MC_BP_STAMPS
     unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int idx = blockIdx.x; idx < NS; idx += gridDim.x) {
-        BP_STAMP(39);  // (the previous slot's sums, 4.)
+        BP_STAMP(39);  // (the previous slot's means, 2.)
         const int s = order[idx];
         if (force_fb) {  // test knob: every slot to the global-hash kernel
             if (t == 0) fb_list[atomicAdd(fb_cnt, 1)] = s;
@@ -627,179 +620,190 @@ __global__ __launch_bounds__(kVxT) void k_bp_voxel_lds(const int *__restrict__ d
         }
         const int f = slot_frame[s], n = slot_np[s], base = slot_pix[s];
         const double *K = intr + 4 * static_cast<size_t>(f);
-        const double *T = pose + 16 * static_cast<size_t>(f);
+        const double *Tp = pose + 16 * static_cast<size_t>(f);
         const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
         const unsigned *pl = pix_list + base;
-        for (int i = t; i < kVxH; i += kVxT) {
+        for (int i = t; i < H; i += T) {
             hkey[i] = kVxEmpty;
             hval[i] = ~0u;
         }
-        for (int i = t; i < kVxV; i += kVxT) vcur[i] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) msk[t][w] = 0ull;
         if (t == 0) s_flag = 0;
-        // 0. world points (stored at the list position for 1. and 4.) and the min bound; four pixels'
-        //    loads per thread in flight
+        // 0. min bound; four pixels' loads per thread in flight
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        double *pp = ppt + 3 * static_cast<size_t>(base);
-        for (int k0 = t; k0 < n; k0 += 4 * kVxT) {
+        for (int k0 = t; k0 < n; k0 += 4 * T) {
             unsigned iv[4];
             float dv[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) iv[u] = k0 + u * kVxT < n ? pl[k0 + u * kVxT] : 0u;
+            for (int u = 0; u < 4; u++) iv[u] = k0 + u * T < n ? pl[k0 + u * T] : 0u;
 #pragma unroll
-            for (int u = 0; u < 4; u++) dv[u] = k0 + u * kVxT < n ? dep[iv[u]] : 0.f;
+            for (int u = 0; u < 4; u++) dv[u] = k0 + u * T < n ? dep[iv[u]] : 0.f;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const int k = k0 + u * kVxT;
-                if (k < n) {
+                if (k0 + u * T < n) {
                     double p[3];
-                    bp_world(K, T, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
+                    bp_world(K, Tp, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
 #pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        pp[3 * k + c] = p[c];
-                        mn[c] = fmin(mn[c], p[c]);
-                    }
+                    for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
                 }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the points are read by any wave in 4.
         block_minmax3_nw<NW>(mn, mx, red);
-        BP_STAMP(36);  // 0. world points + min bound
+        BP_STAMP(36);  // 0. min bound
         double vmin[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
-        // 1. voxel ids in first-occurrence order, per-pixel ids, per-voxel counts
+        // 1. chunks in list order: voxel ids in first-occurrence order and the running sums
         int nv = 0;
-        for (int c0 = 0; c0 < n; c0 += kVxT) {
+        unsigned ivA = t < n ? pl[t] : 0u;              // this chunk's pixel
+        unsigned ivB = T + t < n ? pl[T + t] : 0u;      // the next chunk's
+        float dA = t < n ? dep[ivA] : 0.f;
+        asm volatile("" ::"v"(ivA), "v"(dA), "v"(ivB));  // (loaded before the loop: no wait at its head)
+        for (int c0 = 0; c0 < n; c0 += T) {
             const int k = c0 + t;
-            int h = -1;
-            if (k < n) {
-                const double p[3] = {pp[3 * k], pp[3 * k + 1], pp[3 * k + 2]};
-                unsigned key = 0;
+            const bool valid = k < n;
+            const unsigned iv = ivA;
+            const float d = dA;
+            unsigned key = kVxEmpty;
+            if (valid) {
+                double p[3];
+                bp_world(K, Tp, static_cast<int>(iv % W), static_cast<int>(iv / W), d, p[0], p[1], p[2]);
+                unsigned kk = 0;
                 bool fits = true;
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
                     const double r = floor_div(p[c] - vmin[c], pr.vs);
                     fits = fits && r >= 0.0 && r < 1024.0;
-                    key = (key << 10) | (fits ? static_cast<unsigned>(r) : 0u);
+                    kk = (kk << 10) | (fits ? static_cast<unsigned>(r) : 0u);
                 }
-                if (!fits) {
-                    s_flag = 1;
-                } else {
-                    unsigned e = mod_mul(key * 0x9E3779B1u, kVxH);
-                    for (int probe = 0; probe < kVxH; probe++) {
-                        unsigned cur = hkey[e];
-                        if (cur == kVxEmpty) {
-                            cur = atomicCAS(&hkey[e], kVxEmpty, key);
-                            if (cur == kVxEmpty) cur = key;
-                        }
-                        if (cur == key) {
-                            h = static_cast<int>(e);
-                            break;
-                        }
-                        e = e + 1 == kVxH ? 0u : e + 1;
-                    }
-                    if (h < 0) s_flag = 1;
-                    else if ((hval[h] >> 16) == 0xFFFFu) atomicMin(&hval[h], 0xFFFF0000u | static_cast<unsigned>(t));
-                }
-            }
-            __syncthreads();
-            const bool first = h >= 0 && hval[h] == (0xFFFF0000u | static_cast<unsigned>(t));
-            int tot;
-            const int ex = block_excl_scan<kVxT>(first ? 1 : 0, ws, tot);
-            if (first) {
-                const int v = nv + ex;
-                if (v < kVxV) hval[h] = (static_cast<unsigned>(v) << 16) | 0xFFFFu;
+                if (fits) key = kk;
                 else s_flag = 1;
+                psx[t] = p[0];
+                psy[t] = p[1];
+                psz[t] = p[2];
             }
-            __syncthreads();
-            if (h >= 0) {
-                const unsigned v = hval[h] >> 16;
-                if (v < static_cast<unsigned>(kVxV)) {
-                    pvid[base + k] = static_cast<int>(v);
-                    atomicAdd(&vcur[v], 1);
+            // runs: a lane whose key differs from the previous lane's starts one (invalid lanes, at
+            // the end of the last chunk, and lanes that do not fit, which abandon the slot, start none)
+            const unsigned prev = static_cast<unsigned>(__shfl_up(static_cast<int>(key), 1, 64));
+            const bool head = key != kVxEmpty && (lane == 0 || prev != key);
+            const unsigned long long ends = __ballot(head) | ~__ballot(key != kVxEmpty);
+            int h = -1;
+            unsigned long long run = 0ull;
+            if (head) {
+                const unsigned long long after = ends & ~(below | (1ull << lane));
+                run = (after ? (after & (0ull - after)) - 1ull : ~0ull) & ~below;  // this lane .. the next run's first - 1
+                unsigned e = mod_mul(key * 0x9E3779B1u, H);
+                for (int probe = 0; probe < H; probe++) {
+                    unsigned cur = hkey[e];
+                    if (cur == kVxEmpty) {
+                        cur = atomicCAS(&hkey[e], kVxEmpty, key);
+                        if (cur == kVxEmpty) cur = key;
+                    }
+                    if (cur == key) {
+                        h = static_cast<int>(e);
+                        break;
+                    }
+                    e = e + 1 == static_cast<unsigned>(H) ? 0u : e + 1;
                 }
+                if (h < 0) s_flag = 1;
+                else atomicMin(&hval[h], (hval[h] & 0xFFFF0000u) | static_cast<unsigned>(t));  // (the id half is stable here)
+            }
+            // the previous chunk's sums are stored before any thread loads them after the barrier (their
+            // latency under this chunk's points and probes)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // (the compiler's own wait for the next chunk's pixel lands here, where nothing is in flight,
+            // not after the sums' loads below, where it would wait for them)
+            asm volatile("" ::"v"(ivB));
+            BP_STAMP(38);  // 1a. points, keys, runs, probes
+            __syncthreads();  // hash entries, chunk-first threads, staged points
+            if (s_flag) break;  // (uniform) overflow: the next tier takes the slot
+            bool first = false, isnew = false;
+            unsigned v = 0;
+            if (h >= 0) {
+                const unsigned hv = hval[h];
+                const int tf = static_cast<int>(hv & 0xFFFFu);
+                v = hv >> 16;
+                first = tf == t;
+                isnew = first && v == 0xFFFFu;
+                atomicOr(&msk[tf][wv], run);
+            }
+            double ax = 0.0, ay = 0.0, az = 0.0;
+            int cnt = 0;
+            if (first && !isnew) {  // the running sum so far, loaded under the barrier
+                const double *o = vpts + 3 * (static_cast<size_t>(base) + v);
+                ax = o[0];
+                ay = o[1];
+                az = o[2];
+                cnt = vcnt[base + v];
+            }
+            // the next chunk's depths and the one after's pixels, behind the sums' loads (a wave's
+            // memory operations complete in issue order: the fold waits for the sums only).  The
+            // addresses are clamped rather than the loads skipped, so that both are always issued and
+            // the compiler counts them (a conditional load makes its waits for the sums vmcnt(0)).
+            ivA = ivB;
+            dA = dep[k + T < n ? ivA : 0u];
+            ivB = pl[min(k + 2 * T, n - 1)];
+            const unsigned long long nm = __ballot(isnew);
+            if (lane == 0) wsn[wv] = __popcll(nm);
+            __syncthreads();  // every run's lanes in the masks, new voxels per wave
+            // the prefetched depth and pixel (issued after the sums' loads, so this is the fold's wait
+            // as well) arrive before the sums are stored: the stores, the chunk's last memory
+            // operations, are then waited for only before the next barrier A, under the next chunk's
+            // points and probes
+            asm volatile("" ::"v"(dA), "v"(ivB));
+            int tot = 0, before = 0;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const int c = wsn[w];
+                before += w < wv ? c : 0;
+                tot += c;
+            }
+            if (isnew) {
+                v = static_cast<unsigned>(nv + before + __popcll(nm & below));
+                if (v >= static_cast<unsigned>(V)) s_flag = 1;
+            }
+            if (first && v < static_cast<unsigned>(V)) {
+                // this chunk's pixels of voxel v, in pixel order
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    unsigned long long m = msk[t][w];
+                    if (!m) continue;
+                    msk[t][w] = 0ull;
+                    cnt += __popcll(m);
+                    while (m) {
+                        const int i = 64 * w + __ffsll(static_cast<long long>(m)) - 1;
+                        m &= m - 1ull;
+                        ax = ax + psx[i];
+                        ay = ay + psy[i];
+                        az = az + psz[i];
+                    }
+                }
+                double *o = vpts + 3 * (static_cast<size_t>(base) + v);
+                o[0] = ax;
+                o[1] = ay;
+                o[2] = az;
+                vcnt[base + v] = cnt;
+                hval[h] = (v << 16) | 0xFFFFu;
             }
             nv += tot;
+            BP_STAMP(40);  // 1b. masks, ids, ordered sums
+            __syncthreads();  // staged points, masks and hash entries free for the next chunk
         }
-        __syncthreads();
-        if (s_flag) {  // (uniform) overflow: the global-hash kernel takes the slot
+        sync_global();  // the last chunk's sums, read by other threads in 2.
+        if (s_flag) {  // (uniform) the global-hash kernel or the next tier takes the slot
             if (t == 0) fb_list[atomicAdd(fb_cnt, 1)] = s;
             __syncthreads();
             continue;
         }
-        BP_STAMP(37);  // 1. voxel ids, counts
-        // 2. counts -> exclusive offsets
-        {
-            int carry = 0;
-            for (int v0 = 0; v0 < nv; v0 += kVxT) {
-                const int v = v0 + t;
-                const int c = v < nv ? vcur[v] : 0;
-                int tot;
-                const int ex = block_excl_scan<kVxT>(c, ws, tot);
-                if (v < nv) vcur[v] = carry + ex;
-                carry += tot;
-            }
-        }
-        __syncthreads();
-        // 3. stable scatter: list positions in pixel order within every voxel
-        int vnext = t < n ? pvid[base + t] : -1;  // the next chunk's ids stay in flight across the LDS-only barriers
-        for (int c0 = 0; c0 < n; c0 += kVxT) {
-            const int k = c0 + t;
-            const int v = vnext;
-            vnext = k + kVxT < n ? pvid[base + k + kVxT] : -1;
-            int rank = 0, leader = 0, cnt = 0;
-            unsigned long long act = __ballot(v >= 0);
-            while (act) {
-                const int L = __ffsll(static_cast<long long>(act)) - 1;
-                const int vv = __shfl(v, L, 64);
-                const unsigned long long m = __ballot(v == vv);
-                if (v == vv) {
-                    rank = __popcll(m & ((1ull << lane) - 1ull));
-                    leader = L;
-                    cnt = __popcll(m);
-                }
-                act &= ~m;
-            }
-#pragma unroll
-            for (int w = 0; w < NW; w++) {
-                if (wv == w && v >= 0 && lane == leader) {
-                    gb[w][lane] = vcur[v];
-                    vcur[v] += cnt;
-                }
-                lds_barrier();
-            }
-            if (v >= 0) vlist[base + gb[wv][leader] + rank] = k;
-        }
-        sync_global();  // 4. reads the lists other waves wrote
-        BP_STAMP(38);  // 2. + 3. offsets, ordered scatter
-        // 4. per-voxel sums in pixel order (vcur[v] = end of voxel v's list now)
-        for (int v = t; v < nv; v += kVxT) {
-            const int b0 = v ? vcur[v - 1] : 0, b1 = vcur[v];
-            const int *vl = vlist + base;
-            double ax = 0.0, ay = 0.0, az = 0.0;
-            int j = b0;
-            for (; j + 4 <= b1; j += 4) {
-                const double *q[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) q[u] = pp + 3 * vl[j + u];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    ax = ax + q[u][0];
-                    ay = ay + q[u][1];
-                    az = az + q[u][2];
-                }
-            }
-            for (; j < b1; j++) {
-                const double *q = pp + 3 * vl[j];
-                ax = ax + q[0];
-                ay = ay + q[1];
-                az = az + q[2];
-            }
-            const double dn = static_cast<double>(b1 - b0);
+        BP_STAMP(37);  // 1. ids and running sums
+        // 2. means
+        for (int v = t; v < nv; v += T) {
             double *o = vpts + 3 * (static_cast<size_t>(base) + v);
-            o[0] = ax / dn;
-            o[1] = ay / dn;
-            o[2] = az / dn;
+            const double dn = static_cast<double>(vcnt[base + v]);
+            o[0] = o[0] / dn;
+            o[1] = o[1] / dn;
+            o[2] = o[2] / dn;
         }
         if (t == 0) slot_nv[s] = nv;
         __syncthreads();

@@ -24,7 +24,7 @@ L = _native.load()
 L.mc_debug_bp_stamps.restype = ctypes.c_int
 L.mc_debug_bp_stamps.argtypes = [ctypes.c_void_p]
 ctx.set_points(fr.scene_points.astype(np.float32))
-buf = np.zeros(40, np.uint64)
+buf = np.zeros(48, np.uint64)
 for rep in range(3):
     L.mc_debug_bp_stamps(buf.ctypes.data)
     ctx.set_timing(True)
@@ -53,10 +53,10 @@ print("k-NN points deferred to the ring search", int(buf[30]), "(list overflow",
       int(buf[33]), ")", "near-tied keys redone exactly", int(buf[31]))
 print("knn points", int(buf[13]), "candidates/point", round(float(buf[29]) / max(int(buf[13]), 1), 1),
       "fallbacks", int(buf[31]))
-vt = [float(buf[k]) for k in (36, 37, 38, 39)]
+vt = [float(buf[k]) for k in (36, 38, 40, 37, 39)]
 vtot = max(sum(vt), 1.0)
 print("k_bp_voxel_lds workgroup-busy shares:", {n: f"{100 * v / vtot:.1f} %" for n, v in
-      zip(("0 world+min", "1 ids+counts", "2+3 offsets+scatter", "4 sums"), vt)},
+      zip(("0 min bound", "1a points+keys+probes", "1b masks+ids+sums", "1 exit", "2 means + slot set-up"), vt)},
       "total ms", round(vtot / 1e5, 2))
 st = ctx.bp_candidates()
 for c, n in ((2, "npix"), (3, "nvox"), (4, "ndbscan"), (5, "nsor")):

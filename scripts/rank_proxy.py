@@ -1,0 +1,131 @@
+"""One rank's share of an N-GPU frame-sharded C3 scene, measured on one GPU.
+
+The bench's default at N ranks: each rank back-projects its frame slice (S1), the mask CSRs are
+all-gathered, and every rank runs the graph stages on the whole scene's masks; with the scene
+pipeline (frame_shard.ScenePipeline) the graph stages of scene k run beside S1 of scene k + 1.
+Without N GPUs this script runs what one rank's device does: S1 of the rank's cost-balanced slice
+in a producer thread on its own context, and the graph stages over the WHOLE scene's masks (made
+once up front, handed to the graph context as the gather would) in the calling thread, scene after
+scene.  The graph stages run unsharded here (the bench shards S3 / S4 / S6 level 0 N ways): an
+upper bound on the rank's graph work.  Not included: the all-gather of the mask CSRs (issued by the
+consumer thread, under the producer's S1).  Prints one JSON line per N.
+
+    python scripts/rank_proxy.py [shape] [scenes] [N ...]
+"""
+import json
+import os
+import queue
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from maskclustering_amd import _native  # noqa: E402
+from maskclustering_amd.frame_shard import FrameShardedScene, balanced_frame_slices, frame_costs  # noqa: E402
+from maskclustering_amd.pipeline import GraphRun  # noqa: E402
+from maskclustering_amd.synthetic_frames import make_frames_shape  # noqa: E402
+
+CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
+           contained_threshold=0.8)
+
+
+def main():
+    shape = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    Ns = [1] + [n for n in ([int(x) for x in sys.argv[3:]] or [8]) if n != 1]
+    dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
+    fr = make_frames_shape(shape, seed=0, device="cuda:0", out="torch")
+    F = fr.depth.shape[0]
+    print(f"{shape}: {F} frames rendered in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)
+    K_t = torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev)
+    T_t = torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)
+    prm = _native.bp_params()
+    run = GraphRun(0)
+    run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    run.ctx.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)
+    s1 = _native.Context(0)
+    s1.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)
+    free, _ = torch.cuda.mem_get_info()
+    s1.set_memory_budget(int(free * 0.5))
+    sh = FrameShardedScene(run, fr.num_points, F)
+
+    def s1_masks(lo, hi):
+        s1.backproject(None, None, None, None, prm, shape=(hi - lo, fr.depth.shape[1], fr.depth.shape[2]),
+                       device_ptrs=(fr.depth[lo:hi].data_ptr(), fr.seg[lo:hi].data_ptr(), K_t[lo:hi].data_ptr(),
+                                    T_t[lo:hi].data_ptr()))
+        col, lab, off = s1.bp_mask_index()
+        pts = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=dev)
+        s1.bp_points_to_device(pts.data_ptr())
+        s1.synchronize()
+        return col, lab, off, pts
+
+    full = s1_masks(0, F)  # the gathered masks every rank's graph stages read
+
+    def graph():
+        col, lab, off, pts = full
+        run.set_masks(fr.num_points, F, col, lab, off, pts_device_ptr=pts.data_ptr())
+        sh.step(**CFG)
+        return run.ctx.cluster_info().num_objects
+
+    def timed(fn, n):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / n * 1e3
+
+    objects = graph()
+    g_ms = timed(graph, K)
+    one_ms = timed(lambda: (s1_masks(0, F), graph()), max(2, K // 2))
+    base_pipe = None
+    costs = frame_costs(fr.depth, fr.seg, K_t).cpu().numpy()
+    for N in Ns:
+        slices = balanced_frame_slices(costs, N)
+        s1_ms = [timed(lambda: s1_masks(lo, hi), max(2, K // 2)) for lo, hi in slices]
+        r = int(np.argmax(s1_ms))
+        lo, hi = slices[r]
+
+        def pipelined(n):
+            q: queue.Queue = queue.Queue(maxsize=1)
+
+            def produce():
+                for _ in range(n):
+                    q.put(s1_masks(lo, hi))
+
+            th = threading.Thread(target=produce, daemon=True)
+            th.start()
+            for _ in range(n):
+                q.get()
+                graph()
+            th.join()
+
+        pipelined(1)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        pipelined(K)
+        torch.cuda.synchronize()
+        pipe_ms = (time.perf_counter() - t) / K * 1e3
+        base_pipe = base_pipe or pipe_ms
+        print(json.dumps({
+            "shape": shape, "N": N, "objects": int(objects), "scenes": K,
+            "one_gpu_sequential_ms": round(one_ms, 3),
+            "graph_stages_full_scene_ms": round(g_ms, 3),
+            "s1_slice_ms": [round(x, 3) for x in s1_ms], "slowest_slice": [int(lo), int(hi)],
+            "rank_pipelined_ms": round(pipe_ms, 3),
+            "rank_sequential_ms": round(s1_ms[r] + g_ms, 3),
+            "projected_speedup": round(base_pipe / pipe_ms, 2),
+            "note": "rank_pipelined_ms: S1 of the slowest slice beside the unsharded graph stages of the previous "
+                    "scene; projected_speedup: the N = 1 line's rank_pipelined_ms over this one; the mask all-gather "
+                    "is not included (issued under the next S1 by the consumer thread)"}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
