@@ -295,6 +295,31 @@ def test_in_kernel_invariants(ctx, monkeypatch):
                 assert not bad.any(), f"class >= {min_cls}, nbcap {nbcap}: failures per kind {bad.tolist()}"
 
 
+def test_diagnostics_build_invariants(ctx, tmp_path):
+    """The in-kernel invariant checks on every driver run: the -DMC_DBG_CHECK=1 build of the same
+    source (maskclustering_amd/libmcgraph_dbg.so, built by __graft_entry__.build() behind the spill
+    gate) in a worker process of its own (tests/dbg_invariants_worker.py): no check fails in any size
+    class, lists full or capped, and its masks equal this (release) build's."""
+    import subprocess
+    import sys
+    from maskclustering_amd import _native
+    lib = os.path.join(os.path.dirname(_native.LIB_PATH), "libmcgraph_dbg.so")
+    if not os.path.exists(lib):
+        pytest.fail(f"{lib} missing: __graft_entry__.build() makes it")
+    want = {}
+    for i, inp in enumerate(_dense_inputs()):
+        for k, x in enumerate(_run(ctx, *inp)):
+            want[f"in{i}_{k}"] = np.asarray(x)
+    path = tmp_path / "release_masks.npz"
+    np.savez(path, **want)
+    env = dict(os.environ, MCGRAPH_LIB=lib)
+    env.pop("MC_BP_MIN_CLASS", None)
+    env.pop("MC_BP_NBCAP", None)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "dbg_invariants_worker.py"), str(path)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 def test_two_contexts_share_a_device_under_budgets():
     """Two live contexts on one device, each within its own HBM budget (mc_ctx_set_memory_budget;
     no MC_BP_BATCH_PIXELS): a budget that admits only a few frames per batch gives the same masks as
