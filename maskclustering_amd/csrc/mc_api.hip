@@ -133,8 +133,10 @@ struct mc_ctx {
     DevBuf d_slot_grid;  // denoise: grid origin / extent of the slots with points queued for the k-NN ring search
     int num_cu = 256;
     int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
-    size_t bp_px_cap = 0;  // pixel capacity of the per-batch arrays
+    size_t bp_px_cap = 0;  // mask-pixel capacity of the per-batch arrays (pixel-list positions)
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
+    size_t bp_fpx_cap = 0; // frame-pixel capacity (the valid-id map)
+    double bp_mfrac = 1.0; // mask pixels per frame pixel a batch is sized for (the largest seen, + margin)
     int bp_bm_blocks = 0;
     int bp_F = 0, bp_err_frame = -1;
     int64_t bp_nnz = 0;
@@ -1756,13 +1758,18 @@ enum BpStat : int {
     BS_VXFB2,                             // slots the second voxel tier hands to k_bp_voxel
     BS_DQ,                                // points queued for the k-NN ring search
     BS_DNERR,                             // denoise internal-error bits (queue entry / region out of range)
+    BS_PXOVF,                             // the batch's mask pixels exceed the capacity: grown, batch redone
     BS_COUNT
 };
 
 size_t slots_cap(int fb) { return static_cast<size_t>(fb) * 256 + 1; }  // (frame, id) slots of a batch
-// HBM of the per-batch S1 arrays per pixel of the batch (bp_reserve: the per-pixel arrays sum to 195 B;
-// the per-slot and per-frame ones are small against them)
-constexpr size_t kBpBytesPerPixel = 200;
+// HBM of the per-batch S1 arrays (bp_reserve): per mask pixel (the arrays indexed by pixel-list position,
+// voxel and point arrays included: 195 B) and per frame pixel (the valid-id map); the per-slot and
+// per-frame ones are small against them.  A batch's frames are sized for its mask pixels: the share of
+// mask pixels among frame pixels seen so far (bp_mfrac, 1 before any batch) decides the frames per batch,
+// and a batch with more mask pixels than its capacity grows the arrays and is redone.
+constexpr size_t kBpBytesPerMaskPixel = 196;
+constexpr size_t kBpBytesPerFramePixel = 2;
 
 // (re)allocate the per-batch arrays for fb frames of H x W (pixel capacity fb*H*W)
 // Workgroups per resident slot of a denoise class (the classes take slots from tickets): the extra
@@ -1798,12 +1805,13 @@ inline size_t lean_offset(const mc_ctx *ctx, int cls)
     return o * static_cast<size_t>(ctx->num_cu) * kBpOversub;
 }
 
-void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, hipStream_t s)
+void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, size_t mask_px, hipStream_t s)
 {
-    const size_t px = static_cast<size_t>(fb) * H * W + 1;
+    const size_t px = mask_px + 1;
     const size_t slots = slots_cap(fb);
     ctx->d_band.reserve(static_cast<size_t>(fb) * nbands * mc::kBpWaves * 256 * 4);
     ctx->d_bpvid.reserve(static_cast<size_t>(fb) * H * W + 16);
+    ctx->bp_fpx_cap = std::max(ctx->bp_fpx_cap, static_cast<size_t>(fb) * H * W);
     ctx->d_present.reserve(static_cast<size_t>(fb) * 8 * 4);
     ctx->d_fflags.reserve(static_cast<size_t>(fb) * 4);
     ctx->d_cand.reserve(slots * 4);
@@ -2167,9 +2175,15 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // default 40 % of the device or 65 % of what is free (plus what this context already holds),
         // whichever is less, so a caller's own allocator keeps room (a fresh 288 GB MI355X: ~115 GB,
         // ~530 M pixels per batch); a caller that owns the device (bench.py) sets a larger one.
-        size_t budget = static_cast<size_t>(1) << 30;
+        // frame pixels per batch: below 2^31 (int positions), and within the byte budget at the
+        // expected mask-pixel share (C3: 0.23 of the frame pixels, so two batches instead of six; the
+        // per-batch tails and syncs cost ~3 ms each, profiles/r05/r5s_*)
+        size_t budget = (static_cast<size_t>(1) << 31) - 1;
+        // test knob: MC_BP_MASK_FRAC sets the expected share (a small one forces the grow-and-redo path)
+        if (const char *e = getenv("MC_BP_MASK_FRAC")) ctx->bp_mfrac = atof(e);
+        const double mfrac = std::min(1.0, std::max(ctx->bp_mfrac, 1e-4));
         {
-            const size_t held = ctx->bp_px_cap * kBpBytesPerPixel;
+            const size_t held = ctx->bp_px_cap * kBpBytesPerMaskPixel + ctx->bp_fpx_cap * kBpBytesPerFramePixel;
             size_t bytes = static_cast<size_t>(ctx->mem_budget);
             if (ctx->mem_budget <= 0) {
                 size_t free_b = 0, total_b = 0;
@@ -2177,7 +2191,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b)
                     bytes = std::min(total_b / 100 * 40, (free_b + held) / 100 * 65);
             }
-            budget = std::max<size_t>(HW, std::min(budget, bytes / kBpBytesPerPixel));  // >= one frame
+            const double per_px = static_cast<double>(kBpBytesPerFramePixel) + mfrac * kBpBytesPerMaskPixel;
+            budget = std::max<size_t>(HW, std::min(budget, static_cast<size_t>(static_cast<double>(bytes) / per_px)));
         }
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         BpUpload *const up = on_device ? ctx->bp_up : nullptr;
@@ -2215,7 +2230,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             MC_HIP(hipEventRecord(ctx->ev_up, ctx->copy));
             up->staged = f_hi;
         };
-        bp_reserve(ctx, FB, H, W, nbands, s);
+        // mask-pixel capacity for a batch of FB frames at the expected share (+ 1/16 and a frame's worth)
+        auto mask_cap = [&](double frac) {
+            const double fpx = static_cast<double>(FB) * static_cast<double>(HW);
+            return static_cast<size_t>(std::min(fpx, frac * fpx * 1.0625 + static_cast<double>(HW))) + 1024;
+        };
+        bp_reserve(ctx, FB, H, W, nbands, mask_cap(mfrac), s);
+        double mfrac_seen = 0.0;
         const int PW = static_cast<int>((ctx->P_scene + 63) / 64) + 1;
         if (ctx->d_bpbm.bytes < static_cast<size_t>(kBpGrid) * PW * 8) {
             ctx->d_bpbm.reserve(static_cast<size_t>(kBpGrid) * PW * 8);
@@ -2318,7 +2339,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_slots, grid_for(nslot), dim3(256), 0, s, ctx->d_cand.as<int>(),
                                    ctx->d_csidx.as<int>(), ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), nslot,
                                    ctx->d_slot_of.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>());
+                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), st + BS_NPX,
+                                   static_cast<int>(std::min<size_t>(ctx->bp_px_cap, INT_MAX)), st + BS_NS, st + BS_PXOVF);
                 hipLaunchKernelGGL(mc::k_bp_compact, dim3(nbands, fb), dim3(256), 0, s, ctx->d_bpvid.as<unsigned char>(),
                                    ctx->d_band.as<int>(),
                                    ctx->d_slot_of.as<int>(), ctx->d_slot_pix.as<int>(), dv,
@@ -2419,6 +2441,13 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                        "denoise: k-NN ring-search queue " + std::string(hs[BS_DNERR] & 1 ? "entry" : "region") +
                            " out of range (internal error)");
             MC_REQUIRE(hs[BS_VOXERR] == 0, MC_ERR_UNSUPPORTED, "voxel index beyond 2^21 per axis");
+            if (hs[BS_PXOVF]) {  // more mask pixels than the capacity (nothing past the pixel lists ran): grow, redo
+                const double frac = static_cast<double>(hs[BS_NPX]) / (static_cast<double>(fb) * HW);
+                ctx->bp_mfrac = std::max(ctx->bp_mfrac, frac);
+                bp_reserve(ctx, FB, H, W, nbands, std::max(mask_cap(frac), static_cast<size_t>(hs[BS_NPX]) + 1024), s);
+                continue;
+            }
+            mfrac_seen = std::max(mfrac_seen, static_cast<double>(hs[BS_NPX]) / (static_cast<double>(fb) * HW));
             if (hs[BS_OVF]) {  // neighbour sets overflowed tmp: grow and redo the batch
                 tmp_cap = static_cast<size_t>(hs[BS_TOP]) + (static_cast<size_t>(hs[BS_TOP]) >> 1) + 1024;
                 ctx->d_tmp.reserve(tmp_cap * 4);
@@ -2468,6 +2497,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             ctx->bp_nnz += nnzb;
             b0 += fb;
         }
+        if (mfrac_seen > 0.0) ctx->bp_mfrac = mfrac_seen;  // the next call's batches are sized for it
         unpack();
         MC_HIP(hipStreamSynchronize(s));
         ctx->have_bp = true;

@@ -383,10 +383,18 @@ __global__ __launch_bounds__(256) void k_bp_slots(const int *__restrict__ cand, 
                                                   const int *__restrict__ npix, const int *__restrict__ poff, int n,
                                                   int *__restrict__ slot_of, int *__restrict__ slot_frame,
                                                   int *__restrict__ slot_id, int *__restrict__ slot_np,
-                                                  int *__restrict__ slot_pix)
+                                                  int *__restrict__ slot_pix, const int *__restrict__ npx, int px_cap,
+                                                  int *__restrict__ dNS, int *__restrict__ ovf)
 {
+    // more mask pixels than the pixel-list capacity: no slot (the compaction writes nothing, every later
+    // kernel sees zero slots); the host grows the arrays and redoes the batch
+    const bool over = *npx >= px_cap;
+    if (over && blockIdx.x == 0 && threadIdx.x == 0) {
+        *dNS = 0;
+        *ovf = 1;
+    }
     for (int x = blockIdx.x * 256 + threadIdx.x; x < n; x += gridDim.x * 256) {
-        if (cand[x]) {
+        if (cand[x] && !over) {
             const int s = sidx[x];
             slot_frame[s] = x >> 8;
             slot_id[s] = x & 255;

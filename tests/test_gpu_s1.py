@@ -109,6 +109,37 @@ def test_backproject_batched_equals_single(ctx, monkeypatch):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("frac", ["0.0001", "0.02"])
+def test_mask_pixel_capacity_grow_and_redo(ctx, monkeypatch, frac):
+    """Batches are sized for the expected share of mask pixels among frame pixels; a batch with more
+    mask pixels than that capacity runs no slot, grows the pixel-list arrays and is redone.  Forcing
+    a tiny expected share (MC_BP_MASK_FRAC) sends the first batch (of one or of several) down that
+    path: the masks and statistics equal the default run's and the oracle's."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=6)
+    want = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    sw = ctx.bp_candidates()
+    for batch in (None, str(4 * fr.depth.shape[1] * fr.depth.shape[2])):
+        fresh = _native_ctx()
+        monkeypatch.setenv("MC_BP_MASK_FRAC", frac)
+        if batch:
+            monkeypatch.setenv("MC_BP_BATCH_PIXELS", batch)
+        got = _run(fresh, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+        for x, y in zip(want, got):
+            np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(sw, fresh.bp_candidates())
+        monkeypatch.delenv("MC_BP_MASK_FRAC")
+        again = _run(fresh, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)  # sized from the seen share
+        for x, y in zip(want, again):
+            np.testing.assert_array_equal(x, y)
+    _check_against_oracle(ctx, fr)
+
+
+def _native_ctx():
+    from maskclustering_amd import _native
+    return _native.Context(0)
+
+
 @pytest.mark.parametrize("nb", ["1", "3", "16"])
 def test_backproject_frames_staged_per_batch(ctx, monkeypatch, nb):
     """mc_backproject_frames (per-frame host arrays, batch b + 1 staged on the copy stream while
