@@ -135,9 +135,9 @@ def roofline_entry(w, avg_s, pmc_group=None):
 
 
 # the SQ counter passes of the benched build (scripts/gpu_r4final.sh); the round-3 file only as a fallback
-SQ_DENOISE = next((p for p in (os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"),
-                               os.path.join(REPO, "profiles", "r03", "denoise_sq_counters_c3_v13.json"))
-                   if os.path.exists(p)), os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"))
+SQ_DENOISE = next((p for p in (os.path.join(REPO, "profiles", "r05", "denoise_sq_counters_c3.json"),
+                               os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"))
+                   if os.path.exists(p)), os.path.join(REPO, "profiles", "r05", "denoise_sq_counters_c3.json"))
 SQ_DENOISE_FRAMES = 100     # the counter pass: C3 frames 600-699 (scripts/pmc_kernel.py over scripts/bp_profile.py)
 CLOCK_GHZ = 2.4             # MI355X engine clock (MI355X_MICROARCH.md)
 
@@ -981,6 +981,13 @@ def main():
             for k in ("alt_frac", "traffic_frac_hbm"):
                 if k in e:
                     stages[g][k] = e[k]
+            if "dense-equivalent" in e["model"]:
+                # the reference's dense work over this sparse kernel's time: a ratio, not a roofline
+                # fraction (it exceeds 1); frac is then the kernel's own bytes model (alt_frac) where
+                # one is defined, else absent
+                stages[g]["dense_equiv_ratio"] = stages[g].pop("frac")
+                if "alt_frac" in stages[g]:
+                    stages[g]["frac"] = stages[g].pop("alt_frac")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
