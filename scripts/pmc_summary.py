@@ -32,7 +32,7 @@ GROUPS = {
     "s6_merge": (["mc::k6_merge"], ["mc::k6_merge"]),
     "s7_points": (["mc::k7"], ["mc::k7_words", "mc::k7_count"]),
     "bp_pixels": (["mc::k_bp_count", "mc::k_bp_frames", "mc::k_bp_slots", "mc::k_bp_compact"], ["mc::k_bp_count"]),
-    "bp_voxel": (["mc::k_bp_voxel", "mc::k_bp_vox_order"], ["mc::k_bp_voxel_lds<6144"]),
+    "bp_voxel": (["mc::k_bp_voxel", "mc::k_bp_vox_order"], ["mc::k_bp_voxel_lds<256"]),
     "bp_denoise": (["mc::k_bp_denoise", "mc::k_bp_classify", "mc::k_bp_knn_ring", "mc::k_bp_vox_order"],
                    ["mc::k_bp_classify"]),
     "bp_query": (["mc::k_bp_query", "mc::k_bp_keepflags", "mc::k_bp_emit"], ["mc::k_bp_query", "mc::k_bp_emit"]),
