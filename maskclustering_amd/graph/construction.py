@@ -66,6 +66,8 @@ class GraphHandle:
         self.num_points = num_points
         self.src = src      # Level0Source of the level-0 nodes
         self.node0 = node0  # global mask of every level-0 node
+        self.nodes = ()     # the level-0 Node objects, in order (the fast path checks identity)
+        self.touched = False  # set by a node's visible_frame / contained_mask setter
 
 
 _current = {"token": None}
@@ -251,8 +253,9 @@ for _n in ("update", "pop", "popitem", "clear", "setdefault"):
 
 def _mask_sets(ctx, frame_list):
     col, lab, off, pts = ctx.bp_masks()
-    gl = [(frame_list[c], np.uint8(m)) for c, m in zip(col.tolist(), lab.tolist())]
-    keys = [f"{fid}_{mid}" for fid, mid in gl]
+    fl = [frame_list[c] for c in col.tolist()]
+    gl = list(zip(fl, np.asarray(lab).astype(np.uint8)))          # (frame id, np.uint8 mask id)
+    keys = [f"{f}_{m}" for f, m in zip(fl, np.asarray(lab).tolist())]  # ints format as the uint8s do
     return gl, keys, MaskPointClouds.from_csr(keys, np.asarray(off, np.int64), np.asarray(pts))
 
 
@@ -296,8 +299,8 @@ def _mask_graph_construction(args, scene_points, frame_list, dataset):
     _current["token"] = token
     src = Level0Source(gl, keys, vf, c_off, c_idx, M, mpc)
     handle = GraphHandle(token, len(node0), F, M, P, src, node0)
-    level0 = Node.level0
-    nodes = [level0(src, i, g, handle) for i, g in enumerate(node0.tolist())]
+    nodes = Node.level0_list(src, node0.tolist(), handle)
+    handle.nodes = tuple(nodes)
     return nodes, _thresholds(thr, isint), mpc, pfm
 
 

@@ -31,6 +31,7 @@ the chained ``set.union``, graph/node.py:31-36), and post_process numbers its DB
 """
 from __future__ import annotations
 
+import operator
 import os
 
 import numpy as np
@@ -48,11 +49,10 @@ def _fast_path(nodes):
     h = getattr(nodes[0], "_graph", None)
     if h is None or h.token != construction._current["token"] or len(nodes) != h.num_nodes:
         return None
-    for i, n in enumerate(nodes):
-        d = getattr(n, "__dict__", None)   # (an untouched level-0 node has only its graph identity)
-        if d is None or d.get("_graph") is not h or d.get("_level0") != i or d.get("_vf", 0) is None \
-                or d.get("_cids", 0) is None:
-            return None
+    # the same level-0 Node objects in the same order (a C-speed identity scan), none of them with a
+    # replaced visible_frame / contained_mask (the setters mark the handle touched)
+    if h.touched or not all(map(operator.is_, nodes, h.nodes)):
+        return None
     return h
 
 

@@ -51,6 +51,29 @@ def _visible(node) -> np.ndarray:
     return _host(node.visible_frame) > 0
 
 
+def _order(n):
+    """np.int64 ids in list(n.point_ids) order (node.py:45)"""
+    po = getattr(n, "point_order", None)
+    return po() if po is not None else np.fromiter(n.point_ids, np.int64, count=len(n.point_ids))
+
+
+def _bulk_columns(nodes, vfs, fcol, F):
+    """(frame column of every mask of every node, the (frame, mask) pairs), flattened in node order,
+    when each mask's frame is visible to its node (the usual case, :67-69 then picks that column); None
+    when any is not, for the per-node walk"""
+    if not nodes or any(len(v) != F for v in vfs):
+        return None
+    mls = [n.mask_list for n in nodes]
+    flat = [t for ml in mls for t in ml]
+    cols = np.array([fcol.get(f, -1) for f, _ in flat], np.int64)
+    if len(cols) and cols.min() < 0:
+        return None
+    owner = np.repeat(np.arange(len(mls)), np.fromiter(map(len, mls), np.int64, count=len(mls)))
+    if not np.stack(vfs)[owner, cols].all():
+        return None
+    return cols, flat
+
+
 def post_process_objects(node_list, mask_point_clouds, scene_points, point_frame_matrix, frame_list,
                          point_filter_threshold, dbscan_eps=0.1, dbscan_min_points=4, overlapping_ratio=0.8):
     """post_process.py:180-194 on the device: returns (total_point_ids_list, total_mask_list) as the
@@ -91,8 +114,15 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
         table[key] = len(mask_arrays)
         mask_arrays.append(pts)
 
-    for n in nodes:
-        vf = _visible(n)
+    vfs = [_visible(n) for n in nodes]
+    bulk = _bulk_columns(nodes, vfs, fcol, F) if direct and unique_frames else None
+    if bulk is not None:        # every mask's frame visible to its node: one pass, in node order
+        cols, q_key = bulk
+        q_rows = [row_of[f"{f}_{m}"] for f, m in q_key]         # KeyError as at :70
+        q_col = cols.tolist()
+        vf_rows = vfs
+        orders = [_order(n) for n in nodes]
+    for n, vf in zip(nodes if bulk is None else (), vfs):
         ml = n.mask_list
         cols = np.array([fcol.get(f, -1) for f, _ in ml], np.int64) if unique_frames else None
         if cols is not None and (cols >= 0).all() and vf[cols].all():
@@ -125,8 +155,7 @@ def _post_process_objects(node_list, mask_point_clouds, scene_points, point_fram
                 q_col.append(c)
                 q_key.append((f, m))
         vf_rows.append(vf)
-        po = getattr(n, "point_order", None)                      # list(point_ids), node.py:45
-        orders.append(po() if po is not None else np.fromiter(n.point_ids, np.int64, count=len(n.point_ids)))
+        orders.append(_order(n))
     if not nodes:
         return [], []
     scene = np.ascontiguousarray(_host(scene_points), np.float64).reshape(-1, 3)

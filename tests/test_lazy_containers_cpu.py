@@ -137,3 +137,26 @@ def test_level0_sequences_detects_same_length_edits():
     assert _level0_sequences(h) is None
     mpc._made["b"] = {2, 3, 7}                    # shorter
     assert _level0_sequences(h) is None
+
+
+def test_fast_path_needs_the_untouched_level0_list():
+    """iterative_clustering takes the device-graph path only for the very level-0 Node objects the
+    construction returned, in order, none with a replaced visible_frame / contained_mask."""
+    from maskclustering_amd.graph import construction
+    from maskclustering_amd.graph.iterative_clustering import _fast_path
+    saved = construction._current["token"]
+    try:
+        h = construction.GraphHandle(12345, 3, 4, 5, 6)
+        nodes = [Node.level0(None, i, i, h) for i in range(3)]
+        h.nodes = tuple(nodes)
+        construction._current["token"] = 12345
+        assert _fast_path(nodes) is h and _fast_path(list(nodes)) is h
+        assert _fast_path(nodes[::-1]) is None and _fast_path(nodes[:2]) is None
+        assert _fast_path([nodes[0], nodes[1], Node.level0(None, 2, 2, h)]) is None
+        construction._current["token"] = 7            # another graph was built since
+        assert _fast_path(nodes) is None
+        construction._current["token"] = 12345
+        nodes[1].contained_mask = None                # a caller-replaced containment row
+        assert _fast_path(nodes) is None
+    finally:
+        construction._current["token"] = saved
