@@ -411,7 +411,13 @@ class ShardedEndToEndStep(EndToEndStep):
         # MC_BENCH_NATIVE_COMM=1: the sharded graph stages exchange over the library's own RCCL
         # communicator (mc_ctx_comm_init) instead of torch.distributed between calls
         native = os.environ.get("MC_BENCH_NATIVE_COMM", "0") == "1" and world > 1
-        self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs, native_comm=native)
+        # scene-owner graph stages (default with the pipeline at N > 1; MC_BENCH_SCENE_OWNER=0: the
+        # row-block sharded ones): every rank back-projects its slice of every scene, scene k's masks go
+        # to rank k mod N alone, which runs S2-S6 for it (frame_shard.ScenePipeline)
+        pipelined = os.environ.get("MC_BENCH_PIPELINE", "1") != "0"
+        self.scene_owner = pipelined and world > 1 and os.environ.get("MC_BENCH_SCENE_OWNER", "1") != "0"
+        self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs, native_comm=native,
+                                    shard_graph=not self.scene_owner)
         assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.t_depth, self.t_seg = fr.depth, fr.seg
@@ -429,28 +435,32 @@ class ShardedEndToEndStep(EndToEndStep):
         self.pipe = None
         self.timing_ctxs = [self.ctx]
         self.s1ctx = self.ctx
-        if os.environ.get("MC_BENCH_PIPELINE", "1") != "0":
+        if pipelined:
             from maskclustering_amd.frame_shard import ScenePipeline
             self.s1ctx = _native.Context(local)
             self.s1ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
             own_device_budget(self.s1ctx, 0.6 / (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
-            self.pipe = ScenePipeline(self.sh, self.s1ctx, self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
+            self.pipe = ScenePipeline(self.sh, self.s1ctx, self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm,
+                                      scene_owner=self.scene_owner)
             self.timing_ctxs = [self.ctx, self.s1ctx]
         log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
         self.workload = (f"{shape}: synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
                          f"S1-S6, frames sharded over {self.sh.world} GPU(s)")
 
     def step(self):
+        # (scene-owner mode: the single scene is rank 0's, so rank 0's graph context holds the warmup's
+        # result and the calibration's stage times)
         if self.pipe is not None:
-            self.pipe.run(1, **CFG)
+            self.pipe.run(1, first_owner=0, **CFG)
             return
         self.sh.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
         self.sh.step(**CFG)
 
     def run_steps(self, n):
-        """n scenes; with the pipeline, S1 of scene k + 1 runs under the graph stages of scene k"""
+        """n scenes; with the pipeline, S1 of scene k + 1 runs under the graph stages of scene k (in
+        scene-owner mode scene k's graph stages run on rank k mod N only)"""
         if self.pipe is not None:
-            self.pipe.run(n, **CFG)
+            self.pipe.run(n, first_owner=0, **CFG)
             return
         for _ in range(n):
             self.step()
@@ -904,9 +914,14 @@ def main():
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize()
-    ci = ctx.cluster_info()
-    sizes = ctx.level_sizes(ci.num_iterations)
-    pairs_per_step = int(np.sum(sizes[:-1].astype(np.int64) ** 2))
+    # (scene-owner mode: the warmup and calibration scenes are rank 0's, the other ranks hold no graph
+    # result; they only time their share and join the max-reduce)
+    has_graph = rank == 0 or not getattr(runner, "scene_owner", False)
+    pairs_per_step = 0
+    if has_graph:
+        ci = ctx.cluster_info()
+        sizes = ctx.level_sizes(ci.num_iterations)
+        pairs_per_step = int(np.sum(sizes[:-1].astype(np.int64) ** 2))
 
     # calibration pass with per-group event timing: find the dominant kernel group
     for c in tctxs:
@@ -918,12 +933,12 @@ def main():
     calib = {g: ktime(g) for g in runner.groups}
     for c in tctxs:
         c.set_timing(False)
-    work = runner.work()
+    work = runner.work() if has_graph else {}
     for g in BP_GROUPS:  # S1 models are scene totals: per launch = total / the group's launches per scene
         if g in work and calib.get(g, (0, 0))[1]:
             b, tot, model, alt = work[g]
             work[g] = (b, tot / calib[g][1], model + " per scene / launches per scene", alt)
-    dominant = max((g for g in calib if g in work), key=lambda g: calib[g][0])
+    dominant = max((g for g in calib if g in work), key=lambda g: calib[g][0]) if work else BP_GROUPS[0]
     log("calibration (ms):", json.dumps({k: round(v[0], 4) for k, v in calib.items()}), "dominant:", dominant)
 
     # timed region: barrier + synchronize on both sides; live HIP-event timing of the dominant
@@ -953,6 +968,9 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    if not has_graph:
+        dist.destroy_process_group()
+        return
 
     gi = ctx.graph_info()
     s6_ms = sum(calib.get(g, (0.0, 0))[0] for g in ("s6_columns", "s6_pairs", "s6_components", "s6_merge"))
@@ -1046,7 +1064,9 @@ def main():
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
                        "stage_ms": {k: round(v[0], 4) for k, v in calib.items()},
-                       "parallelism": f"frame-sharded x{world}" if frames else f"scene-parallel x{world}",
+                       "parallelism": (f"frame-sharded x{world}" + (", scene-owner graph stages"
+                                                                     if getattr(runner, "scene_owner", False) else "")
+                                       if frames else f"scene-parallel x{world}"),
                        "scene_pipeline": getattr(runner, "pipe", None) is not None},
             # SURVEY.md §8(d)'s own definition of the pair metric: the same pairs over S6's time only
             "pairs_per_s_s6": round(pairs_per_step / max(s6_ms / 1e3, 1e-12), 1),

@@ -119,8 +119,9 @@ def _comm_device(group, like: torch.device) -> torch.device:
 
 
 def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
-                 max_masks: int | None = None, points_ready=None):
-    """All-gather per-rank mask CSRs into the global one.
+                 max_masks: int | None = None, points_ready=None, dst: int | None = None):
+    """All-gather per-rank mask CSRs into the global one (dst: group rank that alone receives
+    the point ids; the others get None for them).
 
     mask_col / mask_label / mask_off: this rank's masks (numpy; mask_col relative to
     frame_lo); mask_pts: int32 tensor of their point ids (any device).  max_masks bounds any
@@ -133,7 +134,8 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
     Two collectives, one host read: (1) one packed int32 block per rank, [M, nnz, col[M],
     label[M], len[M]] at a fixed stride, whose copy to the host the caller needs anyway (the
     graph input's mask index is host metadata); (2) the point ids at the largest rank's nnz,
-    gathered on the device into one tensor and compacted there.  points_ready (optional) is
+    gathered on the device into one tensor and compacted there (with dst: gathered to that rank
+    only, 1/world of the all-gather's traffic; the scene-owner pipeline).  points_ready (optional) is
     called between the two: the metadata exchange runs while mask_pts is still being written
     (e.g. by a copy on another stream that points_ready then orders torch's stream behind).
     """
@@ -177,6 +179,14 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
         points_ready()
     buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
     buf[:nnz] = mask_pts[:nnz].to(dev)
+    if dst is not None:
+        me = dist.get_rank(group)
+        gdst = dst if group is None else dist.get_global_rank(group, dst)
+        parts = [torch.empty(nmax, dtype=torch.int32, device=dev) for _ in range(world)] if me == dst else None
+        dist.gather(buf, parts, dst=gdst, group=group)
+        if me != dst:
+            return g_col, g_lab, g_off, None
+        return g_col, g_lab, g_off, torch.cat([parts[r][:int(Ns[r])] for r in range(world)]).to(out_dev)
     allp = torch.empty(world * nmax, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(allp, buf, group=group)
     allp = allp.view(world, nmax).to(out_dev)
@@ -335,16 +345,27 @@ class ScenePipeline:
     order in time changes, so that the graph stages, which run serially on every rank after the
     gather and do not shrink with the rank count, hide under the next scene's S1.
     The producer runs at most two scenes ahead (a bounded queue of mask sets).
+
+    ``scene_owner=True`` (several ranks): every rank still back-projects its frame slice of every
+    scene, but scene k's masks are gathered to one rank only, its owner ``(first_owner + k) mod
+    world``, which alone runs S2-S6 for it, unsharded, on its graph context.  The graph stages then
+    cost each rank 1/world of their time per scene instead of all of it (sharding them row-block wise
+    leaves S2, S6 levels >= 1 and the object extraction replicated), and the point ids
+    cross the links once instead of world - 1 times.  Scenes are independent (the reference itself
+    runs one scene per process, ``run.py:33-50``), so each scene's result is the single-process one,
+    held by its owner (``owned``: the scene numbers this rank ran S2-S6 for).
     """
 
     def __init__(self, sh: FrameShardedScene, s1_ctx, depth: torch.Tensor, seg: torch.Tensor,
-                 intrinsics: torch.Tensor, poses: torch.Tensor, params=None):
+                 intrinsics: torch.Tensor, poses: torch.Tensor, params=None, scene_owner: bool = False):
         n = sh.hi - sh.lo
         if depth.shape[0] != n:
             raise ValueError(f"rank {sh.rank} owns {n} frames [{sh.lo}, {sh.hi})")
         self.sh, self.s1 = sh, s1_ctx
         self.frames = (depth, seg, intrinsics, poses)
         self.params = params
+        self.scene_owner = bool(scene_owner) and sh.world > 1
+        self.owned: list[int] = []
 
     def _s1_scene(self):
         """S1 of this rank's slice on the S1 context: (col, lab, off, point ids on the device)."""
@@ -361,10 +382,10 @@ class ScenePipeline:
         self.s1.synchronize()  # the ids are complete before another stream reads them
         return col, lab, off, pts
 
-    def run(self, num_scenes: int, on_scene=None, **step_kwargs):
+    def run(self, num_scenes: int, on_scene=None, first_owner: int = 0, **step_kwargs):
         """num_scenes scenes (each S1 -> gather -> S2-S6); on_scene(k) after scene k's graph stages
-        were issued.  Returns when the last scene's graph stages have been issued on the graph
-        context's stream (synchronize it to wait for them)."""
+        were issued (with scene_owner: on its owner only).  Returns when the last scene's graph
+        stages have been issued on the graph context's stream (synchronize it to wait for them)."""
         import queue
         import threading
         q: queue.Queue = queue.Queue(maxsize=1)
@@ -394,8 +415,14 @@ class ScenePipeline:
                 if isinstance(item, BaseException):
                     raise item
                 col, lab, off, pts = item
+                owner = (first_owner + k) % sh.world
                 if sh.world == 1:
                     g_col, g_lab, g_off, g_pts = col, lab, off, pts
+                elif self.scene_owner:
+                    g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks,
+                                                              dst=owner)
+                    if sh.rank != owner:
+                        continue
                 else:
                     g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks)
                 sh.mask_index = (g_col, g_lab, g_off)
@@ -407,7 +434,12 @@ class ScenePipeline:
                     sh.run.set_masks(sh.P, sh.F, g_col, g_lab, g_off, pts_device_ptr=g_pts.data_ptr())
                 else:
                     sh.run.set_masks(sh.P, sh.F, g_col, g_lab, g_off, g_pts.numpy())
-                sh.step(**step_kwargs)
+                if self.scene_owner:  # the whole scene on this rank: the unsharded graph stages
+                    sh.run.step(step_kwargs["mask_visible_threshold"], step_kwargs["undersegment_filter_threshold"],
+                                step_kwargs["view_consensus_threshold"], step_kwargs["contained_threshold"])
+                    self.owned.append(k)
+                else:
+                    sh.step(**step_kwargs)
                 if on_scene is not None:
                     on_scene(k)
         finally:

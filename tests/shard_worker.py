@@ -70,6 +70,11 @@ class OracleRun:  # the GraphRun surface FrameShardedScene / ShardedGraph use
     def set_masks(self, *a, **kw):
         self.ctx.set_masks(*a, **kw)
 
+    def step(self, mask_visible_threshold, undersegment_filter_threshold, view_consensus_threshold,
+             contained_threshold):  # GraphRun.step: the whole graph path on this process
+        self.ctx.build(mask_visible_threshold, contained_threshold, undersegment_filter_threshold)
+        self.ctx.cluster(None, view_consensus_threshold)
+
 
 def main():
     mode, rank, world, port, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
@@ -114,7 +119,7 @@ def main():
             po, seqs = c.level0_sequences()
             o = _native.setorder_replay(c.sizes[:T], eo, aa, bb, po, seqs, labels=True)
             np.savez(out, **o)
-        elif mode.startswith("pipeline:"):
+        elif mode.startswith("pipeline:") or mode.startswith("owner:"):
             # the scene pipeline (frame_shard.ScenePipeline): S1 in a producer thread on a stand-in S1
             # context that serves this rank's slice masks, gather + sharded S2-S6 on the oracle-backed
             # context in this thread; three scenes, every scene's canonical outputs saved
@@ -143,15 +148,27 @@ def main():
                     pass
 
             run = OracleRun()
-            sh = FrameShardedScene(run, s.num_points, s.num_frames)
+            owner = mode.startswith("owner:")
+            # scene-owner mode: the graph stages unsharded on each scene's owner
+            sh = FrameShardedScene(run, s.num_points, s.num_frames, shard_graph=not owner)
             n = hi - lo
             z = torch.zeros((n, 1, 1))
             pipe = ScenePipeline(sh, S1Ctx(), z, z.to(torch.uint8), torch.zeros((n, 4), dtype=torch.float64),
-                                 torch.zeros((n, 16), dtype=torch.float64))
+                                 torch.zeros((n, 16), dtype=torch.float64), scene_owner=owner)
             outs = {}
-            pipe.run(3, on_scene=lambda k: outs.update({f"{k}/{a}": np.asarray(b) for a, b in
-                                                        run.ctx.canonical().items()}), **CFGS[cfg])
+            nsc = 3 if not owner else 2 * world + 1
+            # scene-owner mode: two calls (one scene with owner 0, then the rest from owner 1), as the
+            # bench's warmup / timed steps make them
+            calls = [(nsc, 0)] if not owner else [(1, 0), (nsc - 1, 1)]
+            base = 0
+            for cnt, first in calls:
+                pipe.run(cnt, first_owner=first,
+                         on_scene=lambda k, b=base: outs.update({f"{b + k}/{a}": np.asarray(v) for a, v in
+                                                                 run.ctx.canonical().items()}), **CFGS[cfg])
+                base += cnt
             outs["s1_calls"] = np.array([S1Ctx.calls])
+            outs["owned"] = np.array(sorted(int(x.split("/")[0]) for x in outs if "/" in x and x.endswith("/num_iters")),
+                                     np.int64)
             np.savez(out, **outs)
         elif mode.startswith("overflow:"):
             # a capture too small on some rank: edges() must raise on every rank (checked before any
