@@ -437,12 +437,20 @@ class ShardedEndToEndStep(EndToEndStep):
         self.s1ctx = self.ctx
         if pipelined:
             from maskclustering_amd.frame_shard import ScenePipeline
-            self.s1ctx = _native.Context(local)
-            self.s1ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
-            own_device_budget(self.s1ctx, 0.6 / (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
-            self.pipe = ScenePipeline(self.sh, self.s1ctx, self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm,
-                                      scene_owner=self.scene_owner)
-            self.timing_ctxs = [self.ctx, self.s1ctx]
+            # S1 producers (contexts): two from N = 4 on, where a slice's arrays fit twice in the budget;
+            # one scene's S1 kernel tails are then filled by the next scene's
+            nprod = int(os.environ.get("MC_BENCH_S1_PRODUCERS", "2" if world >= 4 else "1"))
+            s1ctxs = []
+            for _ in range(max(1, nprod)):
+                c = _native.Context(local)
+                c.set_points(device_ptr=self.t_scene.data_ptr(), num_points=fr.num_points)
+                own_device_budget(c, 0.6 / max(1, nprod) /
+                                  (world if os.environ.get("MC_BENCH_DEVICE") is not None else 1))
+                s1ctxs.append(c)
+            self.s1ctx = s1ctxs[0]
+            self.pipe = ScenePipeline(self.sh, s1ctxs if len(s1ctxs) > 1 else self.s1ctx, self.t_depth, self.t_seg,
+                                      self.t_K, self.t_T, self.prm, scene_owner=self.scene_owner)
+            self.timing_ctxs = [self.ctx] + s1ctxs
         log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
         self.workload = (f"{shape}: synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
                          f"S1-S6, frames sharded over {self.sh.world} GPU(s)")
@@ -1067,7 +1075,8 @@ def main():
                        "parallelism": (f"frame-sharded x{world}" + (", scene-owner graph stages"
                                                                      if getattr(runner, "scene_owner", False) else "")
                                        if frames else f"scene-parallel x{world}"),
-                       "scene_pipeline": getattr(runner, "pipe", None) is not None},
+                       "scene_pipeline": getattr(runner, "pipe", None) is not None,
+                       "s1_producers": len(runner.pipe.s1s) if getattr(runner, "pipe", None) is not None else 0},
             # SURVEY.md §8(d)'s own definition of the pair metric: the same pairs over S6's time only
             "pairs_per_s_s6": round(pairs_per_step / max(s6_ms / 1e3, 1e-12), 1),
             "pairs_per_s_s6_def": "sum_t N_t^2 / sum_t (S6 iteration t's device time: s6_columns + s6_pairs + "

@@ -361,25 +361,32 @@ class ScenePipeline:
         n = sh.hi - sh.lo
         if depth.shape[0] != n:
             raise ValueError(f"rank {sh.rank} owns {n} frames [{sh.lo}, {sh.hi})")
-        self.sh, self.s1 = sh, s1_ctx
+        self.sh = sh
+        # one or more S1 contexts: with P of them, P producer threads take scenes k = i mod P each on
+        # its own context and stream, so that one scene's kernel tails (a persistent ticket kernel's
+        # last slots, a batch's host sync) are filled by the next scene's kernels; scenes are still
+        # handed over in order
+        self.s1s = list(s1_ctx) if isinstance(s1_ctx, (list, tuple)) else [s1_ctx]
+        self.s1 = self.s1s[0]
         self.frames = (depth, seg, intrinsics, poses)
         self.params = params
         self.scene_owner = bool(scene_owner) and sh.world > 1
         self.owned: list[int] = []
 
-    def _s1_scene(self):
-        """S1 of this rank's slice on the S1 context: (col, lab, off, point ids on the device)."""
+    def _s1_scene(self, s1=None):
+        """S1 of this rank's slice on an S1 context: (col, lab, off, point ids on the device)."""
+        s1 = self.s1 if s1 is None else s1
         depth, seg, K, T = self.frames
         n, H, W = depth.shape
         if n == 0:
             return (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64),
                     torch.zeros(1, dtype=torch.int32, device=depth.device))
-        self.s1.backproject(None, None, None, None, self.params, shape=(n, H, W),
-                            device_ptrs=(depth.data_ptr(), seg.data_ptr(), K.data_ptr(), T.data_ptr()))
-        col, lab, off = self.s1.bp_mask_index()
+        s1.backproject(None, None, None, None, self.params, shape=(n, H, W),
+                       device_ptrs=(depth.data_ptr(), seg.data_ptr(), K.data_ptr(), T.data_ptr()))
+        col, lab, off = s1.bp_mask_index()
         pts = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=depth.device)
-        self.s1.bp_points_to_device(pts.data_ptr())
-        self.s1.synchronize()  # the ids are complete before another stream reads them
+        s1.bp_points_to_device(pts.data_ptr())
+        s1.synchronize()  # the ids are complete before another stream reads them
         return col, lab, off, pts
 
     def run(self, num_scenes: int, on_scene=None, first_owner: int = 0, **step_kwargs):
@@ -388,13 +395,15 @@ class ScenePipeline:
         stages have been issued on the graph context's stream (synchronize it to wait for them)."""
         import queue
         import threading
-        q: queue.Queue = queue.Queue(maxsize=1)
+        NP = len(self.s1s)
+        qs = [queue.Queue(maxsize=1) for _ in range(NP)]
         stop = threading.Event()
 
-        def produce():
+        def produce(i):
+            q = qs[i]
             try:
-                for _ in range(num_scenes):
-                    item = self._s1_scene()
+                for _ in range(i, num_scenes, NP):
+                    item = self._s1_scene(self.s1s[i])
                     while not stop.is_set():
                         try:
                             q.put(item, timeout=0.5)
@@ -406,12 +415,13 @@ class ScenePipeline:
             except BaseException as e:  # handed to the consumer, which raises it
                 q.put(e)
 
-        th = threading.Thread(target=produce, name="s1-producer", daemon=True)
-        th.start()
+        ths = [threading.Thread(target=produce, args=(i,), name=f"s1-producer-{i}", daemon=True) for i in range(NP)]
+        for th in ths:
+            th.start()
         sh = self.sh
         try:
             for k in range(num_scenes):
-                item = q.get()
+                item = qs[k % NP].get()
                 if isinstance(item, BaseException):
                     raise item
                 col, lab, off, pts = item
@@ -444,4 +454,5 @@ class ScenePipeline:
                     on_scene(k)
         finally:
             stop.set()
-            th.join()
+            for th in ths:
+                th.join()

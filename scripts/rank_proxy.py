@@ -54,7 +54,13 @@ def main():
     s1.set_memory_budget(int(free * 0.5))
     sh = FrameShardedScene(run, fr.num_points, F)
 
-    def s1_masks(lo, hi):
+    s1b = None  # a second S1 context (two producers: one scene's kernel tails filled by the next's)
+    if os.environ.get("MC_PROXY_TWO_PRODUCERS", "1") != "0":
+        s1b = _native.Context(0)
+        s1b.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)
+        s1b.set_memory_budget(int(free * 0.3))
+
+    def s1_masks(lo, hi, s1=s1):
         s1.backproject(None, None, None, None, prm, shape=(hi - lo, fr.depth.shape[1], fr.depth.shape[2]),
                        device_ptrs=(fr.depth[lo:hi].data_ptr(), fr.seg[lo:hi].data_ptr(), K_t[lo:hi].data_ptr(),
                                     T_t[lo:hi].data_ptr()))
@@ -121,6 +127,32 @@ def main():
         # over N * ceil(K / N) scenes so that the share is exact
         Ko = N * max(1, -(-K // N))
         own_ms = timed_pipe(Ko, N)
+
+        def pipelined2(n, every):  # two producers on two S1 contexts, scenes alternating, taken in order
+            qs = [queue.Queue(maxsize=1), queue.Queue(maxsize=1)]
+
+            def produce(i, ctx):
+                for _ in range(i, n, 2):
+                    qs[i].put(s1_masks(lo, hi, ctx))
+
+            ths = [threading.Thread(target=produce, args=(i, c), daemon=True) for i, c in enumerate((s1, s1b))]
+            for th in ths:
+                th.start()
+            for k in range(n):
+                qs[k % 2].get()
+                if k % every == 0:
+                    graph()
+            for th in ths:
+                th.join()
+
+        own2_ms = None
+        if s1b is not None and N > 1:  # (a whole C3 scene twice does not fit beside the first context's arrays)
+            pipelined2(2, N)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            pipelined2(Ko, N)
+            torch.cuda.synchronize()
+            own2_ms = (time.perf_counter() - t) / Ko * 1e3
         print(json.dumps({
             "shape": shape, "N": N, "objects": int(objects), "scenes": K,
             "one_gpu_sequential_ms": round(one_ms, 3),
@@ -131,6 +163,8 @@ def main():
             "projected_speedup": round(base_pipe / pipe_ms, 2),
             "rank_pipelined_scene_owner_ms": round(own_ms, 3), "scene_owner_scenes": Ko,
             "projected_speedup_scene_owner": round(base_pipe / own_ms, 2),
+            "rank_two_producers_scene_owner_ms": own2_ms and round(own2_ms, 3),
+            "projected_speedup_two_producers": own2_ms and round(base_pipe / own2_ms, 2),
             "note": "rank_pipelined_ms: S1 of the slowest slice beside the unsharded graph stages of the previous "
                     "scene; projected_speedup: the N = 1 line's rank_pipelined_ms over this one; the mask all-gather "
                     "is not included (issued under the next S1 by the consumer thread); scene_owner: the graph "

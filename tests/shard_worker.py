@@ -119,7 +119,7 @@ def main():
             po, seqs = c.level0_sequences()
             o = _native.setorder_replay(c.sizes[:T], eo, aa, bb, po, seqs, labels=True)
             np.savez(out, **o)
-        elif mode.startswith("pipeline:") or mode.startswith("owner:"):
+        elif mode.startswith(("pipeline:", "owner:", "owner2:")):
             # the scene pipeline (frame_shard.ScenePipeline): S1 in a producer thread on a stand-in S1
             # context that serves this rank's slice masks, gather + sharded S2-S6 on the oracle-backed
             # context in this thread; three scenes, every scene's canonical outputs saved
@@ -148,12 +148,13 @@ def main():
                     pass
 
             run = OracleRun()
-            owner = mode.startswith("owner:")
+            owner = mode.startswith(("owner:", "owner2:"))
+            producers = 2 if mode.startswith("owner2:") else 1  # S1 contexts (producer threads)
             # scene-owner mode: the graph stages unsharded on each scene's owner
             sh = FrameShardedScene(run, s.num_points, s.num_frames, shard_graph=not owner)
             n = hi - lo
             z = torch.zeros((n, 1, 1))
-            pipe = ScenePipeline(sh, S1Ctx(), z, z.to(torch.uint8), torch.zeros((n, 4), dtype=torch.float64),
+            pipe = ScenePipeline(sh, [S1Ctx() for _ in range(producers)] if producers > 1 else S1Ctx(), z, z.to(torch.uint8), torch.zeros((n, 4), dtype=torch.float64),
                                  torch.zeros((n, 16), dtype=torch.float64), scene_owner=owner)
             outs = {}
             nsc = 3 if not owner else 2 * world + 1

@@ -180,21 +180,22 @@ def test_scene_pipeline_equals_single_process(tmp_path, world, shape, seed, cfg)
                 np.testing.assert_array_equal(got[f"{k}/{name}"], np.asarray(want[name]), err_msg=f"scene {k} {name}")
 
 
-@pytest.mark.parametrize("world,shape,seed,cfg", [(2, "c1", 1, "scannet"), (3, "tiny", 5, "scannetpp"),
-                                                  (4, "c1", 2, "scannet")])
-def test_scene_owner_pipeline_equals_single_process(tmp_path, world, shape, seed, cfg):
+@pytest.mark.parametrize("world,shape,seed,cfg,mode", [(2, "c1", 1, "scannet", "owner"), (3, "tiny", 5, "scannetpp", "owner"),
+                                                       (4, "c1", 2, "scannet", "owner"), (2, "c1", 1, "scannet", "owner2"),
+                                                       (3, "c1", 2, "scannet", "owner2")])
+def test_scene_owner_pipeline_equals_single_process(tmp_path, world, shape, seed, cfg, mode):
     """The scene-owner pipeline (every rank back-projects its slice of every scene; scene k's masks
     are gathered to rank k mod world alone, which runs S2-S6 unsharded): each scene is clustered by
     exactly one rank, its owner, with exactly the single-process outputs, and S1 ran on every rank
     for every scene.  Two run() calls, the first with one scene (the bench's warmup), the second
-    starting at owner 1."""
+    starting at owner 1.  owner2: two S1 producers on two contexts, scenes alternating."""
     from maskclustering_amd.synthetic import make_shape
     from oracle import oracle
     s = make_shape(shape, seed=seed)
     want = oracle.run_sparse(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, **KW[cfg])
     nsc = 2 * world + 1
     seen = []
-    for r, out in enumerate(run_ranks(f"owner:{shape}:{seed}:{cfg}", world, tmp_path)):
+    for r, out in enumerate(run_ranks(f"{mode}:{shape}:{seed}:{cfg}", world, tmp_path)):
         got = np.load(out)
         assert int(got["s1_calls"][0]) == nsc
         owned = [int(k) for k in got["owned"]]
