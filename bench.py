@@ -437,9 +437,10 @@ class ShardedEndToEndStep(EndToEndStep):
         self.s1ctx = self.ctx
         if pipelined:
             from maskclustering_amd.frame_shard import ScenePipeline
-            # S1 producers (contexts): two from N = 4 on, where a slice's arrays fit twice in the budget;
-            # one scene's S1 kernel tails are then filled by the next scene's
-            nprod = int(os.environ.get("MC_BENCH_S1_PRODUCERS", "2" if world >= 4 else "1"))
+            # S1 producers (contexts; MC_BENCH_S1_PRODUCERS, default one): with two, one scene's S1 kernel
+            # tails are filled by the next scene's; measured +3 % for one rank's share at N = 8 but 2.2x
+            # slower for whole C3 scenes on one GPU, so not the default
+            nprod = int(os.environ.get("MC_BENCH_S1_PRODUCERS", "1"))
             s1ctxs = []
             for _ in range(max(1, nprod)):
                 c = _native.Context(local)
@@ -451,6 +452,7 @@ class ShardedEndToEndStep(EndToEndStep):
             self.pipe = ScenePipeline(self.sh, s1ctxs if len(s1ctxs) > 1 else self.s1ctx, self.t_depth, self.t_seg,
                                       self.t_K, self.t_T, self.prm, scene_owner=self.scene_owner)
             self.timing_ctxs = [self.ctx] + s1ctxs
+            self.pipe.warm()  # the other producers' first calls, outside the timed region
         log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
         self.workload = (f"{shape}: synthetic RGB-D scene, {F} frames {W}x{H}, P={fr.num_points}, "
                          f"S1-S6, frames sharded over {self.sh.world} GPU(s)")

@@ -373,6 +373,12 @@ class ScenePipeline:
         self.scene_owner = bool(scene_owner) and sh.world > 1
         self.owned: list[int] = []
 
+    def warm(self):
+        """One S1 call on every context but the first (a context's first call sizes its batches for
+        the worst case and allocates; run(1), the bench's warmup step, only reaches the first)."""
+        for c in self.s1s[1:]:
+            self._s1_scene(c)
+
     def _s1_scene(self, s1=None):
         """S1 of this rank's slice on an S1 context: (col, lab, off, point ids on the device)."""
         s1 = self.s1 if s1 is None else s1
