@@ -130,6 +130,7 @@ struct mc_ctx {
     DevBuf d_cls_list, d_nbl, d_lean, d_vox_order;  // denoise size-class slot lists; per-workgroup eps-neighbour lists, lean scratch
     // voxel_down_sample: per-pixel voxel ids and voxel lists of k_bp_voxel_lds; its overflow slots
     DevBuf d_vx_pvid, d_vx_list, d_vx_fb, d_bppack;
+    DevBuf d_scanm;  // block sums of the per-batch multi-workgroup scans
     DevBuf d_slot_grid;  // denoise: grid origin / extent of the slots with points queued for the k-NN ring search
     int num_cu = 256;
     int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
@@ -385,7 +386,7 @@ void mc_ctx_destroy(mc_ctx *ctx)
                          &ctx->d_out_label, &ctx->d_out_off, &ctx->d_out_pts, &ctx->d_bp_pts,
                          &ctx->d_cls_list, &ctx->d_nbl, &ctx->d_lean, &ctx->d_vox_order,
                          &ctx->d_vx_pvid, &ctx->d_vx_list, &ctx->d_vx_fb, &ctx->d_bppack, &ctx->d_acc, &ctx->d_hvid,
-                         &ctx->d_slot_grid};
+                         &ctx->d_slot_grid, &ctx->d_scanm};
     for (DevBuf *b : bp_bufs) b->release();
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy), (void)hipStreamDestroy(ctx->copy);
     if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
@@ -1830,6 +1831,7 @@ void bp_reserve(mc_ctx *ctx, int fb, int H, int W, int nbands, size_t mask_px, h
     ctx->d_cls_list.reserve((mc::kBpClasses + 1) * slots * 4);
     ctx->d_vox_order.reserve(slots * 4);
     ctx->d_vx_fb.reserve(2 * slots * 4);  // the two tiers' overflow lists
+    ctx->d_scanm.reserve(4 * (slots / mc::kScanTile + 3) * 4);
     ctx->d_slot_grid.reserve(8 * slots * 8);
     // per-workgroup eps-neighbour lists, one region per size class (the classes run concurrently)
     ctx->d_nbl.reserve(nbl_offset(ctx, mc::kBpClasses) * 2);
@@ -2334,8 +2336,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_frames, dim3(fb), dim3(1024), 0, s, ctx->d_band.as<int>(),
                                    ctx->d_present.as<unsigned>(), ctx->d_fflags.as<int>(), dv, ctx->d_cand.as<int>(),
                                    ctx->d_npix.as<int>(), st + BS_ERRF);
-                mc::scan_device_n(s, ctx->d_cand.as<int>(), ctx->d_csidx.as<int>(), nullptr, nslot, st + BS_NS,
-                                  ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), st + BS_NPX);
+                mc::scan_device_multi(s, nullptr, nslot, ctx->d_scanm.as<int>(), ctx->d_cand.as<int>(),
+                                      ctx->d_csidx.as<int>(), st + BS_NS, ctx->d_npix.as<int>(), ctx->d_poff.as<int>(),
+                                      st + BS_NPX);
                 hipLaunchKernelGGL(mc::k_bp_slots, grid_for(nslot), dim3(256), 0, s, ctx->d_cand.as<int>(),
                                    ctx->d_csidx.as<int>(), ctx->d_npix.as<int>(), ctx->d_poff.as<int>(), nslot,
                                    ctx->d_slot_of.as<int>(), ctx->d_slot_frame.as<int>(), ctx->d_slot_id.as<int>(),
@@ -2421,8 +2424,9 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 bp_debug_sync(s, "k_bp_query");
                 hipLaunchKernelGGL(mc::k_bp_keepflags, grid_for(nslot), dim3(256), 0, s, st + BS_NS,
                                    ctx->d_slot_nn.as<int>(), ctx->d_kflag.as<int>(), ctx->d_ksize.as<int>());
-                mc::scan_device_n(s, ctx->d_kflag.as<int>(), ctx->d_midx.as<int>(), st + BS_NS, 0, st + BS_M,
-                                  ctx->d_ksize.as<int>(), ctx->d_moff.as<int>(), st + BS_NNZ);
+                mc::scan_device_multi(s, st + BS_NS, nslot, ctx->d_scanm.as<int>(), ctx->d_kflag.as<int>(),
+                                      ctx->d_midx.as<int>(), st + BS_M, ctx->d_ksize.as<int>(), ctx->d_moff.as<int>(),
+                                      st + BS_NNZ);
                 bp_debug_sync(s, "bp_query");
             }
             MC_HIP(hipMemcpyAsync(hs, st, BS_COUNT * 4, hipMemcpyDeviceToHost, s));

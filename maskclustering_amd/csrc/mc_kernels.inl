@@ -223,6 +223,77 @@ void scan_device_n(hipStream_t s, const int *in, int *out, const int *dn, int n_
     hipLaunchKernelGGL(k_scan1, dim3(1), dim3(1024), 0, s, in, out, dn, n_host, dtotal, in2, out2, dtotal2);
 }
 
+// The same by many workgroups with n read from the device (*dn, bounded by the host's n_cap): block
+// sums, one single-workgroup scan of them, each block's tile; up to two arrays (blockIdx.y), each
+// with out[n] = total and *dtotal = total.  For the per-batch S1 scans (~10^5 ints), which the
+// single-workgroup k_scan1 walks one 8192-int tile after another.
+struct ScanArrays {
+    const int *in[2];
+    int *out[2];
+    int *dtotal[2];
+};
+__global__ __launch_bounds__(256) void k_scanm_reduce(ScanArrays a, const int *dn, int n_host, int *__restrict__ partial)
+{
+    __shared__ int ws[4];
+    const int n = dn ? *dn : n_host;
+    const int *in = a.in[blockIdx.y];
+    const int i0 = blockIdx.x * kScanTile;
+    int s = 0;
+    if (i0 < n)  // (uniform in the block)
+        for (int k = threadIdx.x; k < kScanTile; k += 256) {
+            const int i = i0 + k;
+            s += i < n ? in[i] : 0;
+        }
+    s = block_sum<256>(s, ws);
+    if (threadIdx.x == 0) partial[blockIdx.y * (gridDim.x + 1) + blockIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void k_scanm_down(ScanArrays a, const int *dn, int n_host, const int *__restrict__ pscan)
+{
+    __shared__ int ws[4];
+    const int n = dn ? *dn : n_host;
+    const int y = blockIdx.y;
+    const int *ps = pscan + y * (gridDim.x + 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.out[y][n] = ps[gridDim.x];
+        if (a.dtotal[y]) *a.dtotal[y] = ps[gridDim.x];
+    }
+    if (static_cast<int>(blockIdx.x) * kScanTile >= n) return;  // (uniform in the block)
+    const int *in = a.in[y];
+    int *out = a.out[y];
+    const int i0 = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    int v[kScanItems];
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = (i0 + k < n) ? in[i0 + k] : 0;
+        s += v[k];
+    }
+    int tot;
+    int ex = block_excl_scan<256>(s, ws, tot) + ps[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        if (i0 + k < n) out[i0 + k] = ex;
+        ex += v[k];
+    }
+}
+// tmp: >= 4 * (n_cap / kScanTile + 2) ints
+void scan_device_multi(hipStream_t s, const int *dn, int n_cap, int *tmp, const int *in, int *out, int *dtotal,
+                       const int *in2 = nullptr, int *out2 = nullptr, int *dtotal2 = nullptr)
+{
+    const int nb = std::max(1, ceil_div(n_cap, kScanTile));
+    if (nb <= 2) {
+        scan_device_n(s, in, out, dn, n_cap, dtotal, in2, out2, dtotal2);
+        return;
+    }
+    const int ny = in2 ? 2 : 1;
+    const ScanArrays a{{in, in2}, {out, out2}, {dtotal, dtotal2}};
+    int *part = tmp, *pscan = tmp + 2 * (nb + 1);
+    hipLaunchKernelGGL(k_scanm_reduce, dim3(nb, ny), dim3(256), 0, s, a, dn, n_cap, part);
+    scan_device_n(s, part, pscan, nullptr, nb, nullptr, ny > 1 ? part + nb + 1 : nullptr,
+                  ny > 1 ? pscan + nb + 1 : nullptr, nullptr);
+    hipLaunchKernelGGL(k_scanm_down, dim3(nb, ny), dim3(256), 0, s, a, dn, n_cap, pscan);
+}
+
 void scan_large(hipStream_t s, const int *in, int *out, int n, int *tmp /* >= 2*(n/tile+2) */)
 {
     const int nb = ceil_div(n, kScanTile);
