@@ -118,6 +118,9 @@ def _comm_device(group, like: torch.device) -> torch.device:
     return like if like.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
 
 
+_GATHER_OK = [True]  # cleared if the backend refuses dist.gather (gather_masks then all-gathers)
+
+
 def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
                  max_masks: int | None = None, points_ready=None, dst: int | None = None):
     """All-gather per-rank mask CSRs into the global one (dst: group rank that alone receives
@@ -179,14 +182,22 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
         points_ready()
     buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
     buf[:nnz] = mask_pts[:nnz].to(dev)
-    if dst is not None:
+    if dst is not None and _GATHER_OK[0]:
         me = dist.get_rank(group)
         gdst = dst if group is None else dist.get_global_rank(group, dst)
         parts = [torch.empty(nmax, dtype=torch.int32, device=dev) for _ in range(world)] if me == dst else None
-        dist.gather(buf, parts, dst=gdst, group=group)
-        if me != dst:
-            return g_col, g_lab, g_off, None
-        return g_col, g_lab, g_off, torch.cat([parts[r][:int(Ns[r])] for r in range(world)]).to(out_dev)
+        try:
+            dist.gather(buf, parts, dst=gdst, group=group)
+        except (RuntimeError, NotImplementedError) as e:
+            # a backend without gather refuses it on every rank before any transfer: the all-gather
+            # below serves instead, from now on
+            if "support" not in str(e).lower():
+                raise
+            _GATHER_OK[0] = False
+        else:
+            if me != dst:
+                return g_col, g_lab, g_off, None
+            return g_col, g_lab, g_off, torch.cat([parts[r][:int(Ns[r])] for r in range(world)]).to(out_dev)
     allp = torch.empty(world * nmax, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(allp, buf, group=group)
     allp = allp.view(world, nmax).to(out_dev)
