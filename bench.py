@@ -38,8 +38,11 @@ import maskclustering_amd  # noqa: E402,F401  (HIP queue setting before the firs
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense)
-CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
-           contained_threshold=0.8)  # configs/scannet.json
+from maskclustering_amd.dataset_configs import DATASET_THRESHOLDS, shape_thresholds  # noqa: E402
+
+# the graph thresholds of the reference's configs/scannet.json (C2, the ScanNet-shaped scene); every
+# step runs under its shape's own dataset config (shape_thresholds: C3 = configs/scannetpp.json)
+CFG = shape_thresholds("c2")[1]
 G_GROUPS = ["s2_point_lists", "s3_masks", "s3_undo_s5", "s4_observer_hist", "s6_columns", "s6_pairs",
             "s6_components", "s6_merge", "s7_points"]
 BP_GROUPS = ["bp_pixels", "bp_voxel", "bp_denoise", "bp_query"]
@@ -214,20 +217,20 @@ def s1_cpu_rate(scene_f32, frame_at, F, n_all=64, n_one=8):
                 frames=F)
 
 
-def graph_cpu(P, F, col, lab, off, pts, threads, dense=False):
-    """the S2-S6 port on `threads` host threads: (seconds, timings)"""
+def graph_cpu(P, F, col, lab, off, pts, threads, dense=False, cfg=None):
+    """the S2-S6 port on `threads` host threads under thresholds `cfg` (default C2's): (seconds, timings)"""
     from oracle import oracle
     tm = {}
     with oracle.threads(threads):
-        (oracle.run if dense else oracle.run_sparse)(P, F, col, lab, off, pts, timings=tm, **CFG)
+        (oracle.run if dense else oracle.run_sparse)(P, F, col, lab, off, pts, timings=tm, **(cfg or CFG))
     return tm["s2"] + tm["s3"] + tm["s4"] + tm["s6"], tm
 
 
-def e2e_cpu_baseline(s1, P, F, col, lab, off, pts):
+def e2e_cpu_baseline(s1, P, F, col, lab, off, pts, cfg):
     """cpu_baseline of the E2E variants: S1 port (per-frame rates of s1_cpu_rate x F frames) + the
     S2-S6 port on the full mask set, on all host threads (value) and on one (single_thread)."""
-    g_all, tm = graph_cpu(P, F, col, lab, off, pts, s1["threads"])
-    g_one, _ = graph_cpu(P, F, col, lab, off, pts, 1)
+    g_all, tm = graph_cpu(P, F, col, lab, off, pts, s1["threads"], cfg=cfg)
+    g_one, _ = graph_cpu(P, F, col, lab, off, pts, 1, cfg=cfg)
     all_s, one_s = s1["all"] * F + g_all, s1["one"] * F + g_one
     pairs = tm["pairs"]
     return {"value": round(pairs / all_s, 1), "unit": "mask-pairs/s", "cores": s1["threads"], "kind": "port",
@@ -248,6 +251,7 @@ class GraphStep:
         from maskclustering_amd.pipeline import GraphRun
         from maskclustering_amd.synthetic import SHAPES, make_shape
         self.scene = make_shape(shape, seed=seed)
+        self.dataset, self.cfg = shape_thresholds(shape)
         self.run = GraphRun(local)
         self.run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.run.set_scene(self.scene)
@@ -257,7 +261,7 @@ class GraphStep:
                          f"F={sh['num_frames']}")
 
     def step(self):
-        self.run.step(**CFG)
+        self.run.step(**self.cfg)
 
     def work(self):
         s = self.scene
@@ -268,8 +272,9 @@ class GraphStep:
         s = self.scene
         dense = s.num_masks <= 30000  # dense matrices beyond C2 do not fit
         thr = oracle.default_threads()
-        cpu_s, tm = graph_cpu(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, thr, dense)
-        one_s, _ = graph_cpu(s.num_points, s.num_frames, s.mask_col, s.mask_label, s.mask_off, s.mask_pts, 1, dense)
+        masks = (s.mask_col, s.mask_label, s.mask_off, s.mask_pts)
+        cpu_s, tm = graph_cpu(s.num_points, s.num_frames, *masks, thr, dense, cfg=self.cfg)
+        one_s, _ = graph_cpu(s.num_points, s.num_frames, *masks, 1, dense, cfg=self.cfg)
         return {"value": round(tm["pairs"] / cpu_s, 1), "unit": "mask-pairs/s", "cores": thr, "kind": "port",
                 "sample": f"{'oracle/mcgraph_oracle.c' if dense else 'oracle/graph_sparse.c'} S2-S6 on "
                           f"the same scene (1 full scene, {thr} threads, {cpu_s:.2f} s: "
@@ -292,6 +297,7 @@ class EndToEndStep:
         log(f"rendered {fr.num_frames} frames {fr.depth.shape[1]}x{fr.depth.shape[2]} P={fr.num_points} "
             f"in {time.perf_counter() - t0:.1f} s")
         self.fr = fr
+        self.dataset, self.cfg = shape_thresholds(shape)
         dev = torch.device("cuda", local)
         self.t_scene = torch.tensor(fr.scene_points, dtype=torch.float32, device=dev)  # construction.py:37
         self.t_depth = fr.depth
@@ -315,7 +321,7 @@ class EndToEndStep:
                              device_ptrs=(self.t_depth.data_ptr(), self.t_seg.data_ptr(), self.t_K.data_ptr(),
                                           self.t_T.data_ptr()))
         self.ctx.use_backprojection()
-        self.run.step(**CFG)
+        self.run.step(**self.cfg)
 
     def work(self):
         F, H, W = self.shape
@@ -332,7 +338,7 @@ class EndToEndStep:
         at = lambda i: (fr.depth[i].cpu().numpy(), fr.seg[i].cpu().numpy(), fr.intrinsics[i], fr.poses[i])  # noqa: E731
         s1 = s1_cpu_rate(fr.scene_points.astype(np.float32), at, fr.num_frames)
         col, lab, off, pts = self.ctx.bp_masks()
-        return e2e_cpu_baseline(s1, fr.num_points, fr.num_frames, col, lab, off, pts)
+        return e2e_cpu_baseline(s1, fr.num_points, fr.num_frames, col, lab, off, pts, self.cfg)
 
 
 class ShardedGraphStep(GraphStep):
@@ -347,6 +353,7 @@ class ShardedGraphStep(GraphStep):
         from maskclustering_amd.pipeline import GraphRun
         from maskclustering_amd.synthetic import SHAPES, make_shape
         self.scene = s = make_shape(shape, seed=seed)
+        self.dataset, self.cfg = shape_thresholds(shape)
         self.run = GraphRun(local)
         self.run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         self.sh = FrameShardedScene(self.run, s.num_points, s.num_frames)
@@ -364,7 +371,7 @@ class ShardedGraphStep(GraphStep):
 
     def step(self):
         self.sh.set_local_masks(*self.local)
-        self.sh.step(**CFG)
+        self.sh.step(**self.cfg)
 
     def work(self):
         s = self.scene
@@ -401,6 +408,7 @@ class ShardedEndToEndStep(EndToEndStep):
                 lo, hi = blo, bhi
                 fr = make_frames_shape(shape, seed=seed, device=f"cuda:{local}", frames=range(lo, hi), out="torch")
         self.fr = fr
+        self.dataset, self.cfg = shape_thresholds(shape)
         self.run = GraphRun(local)
         self.ctx = self.run.ctx
         self.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -461,16 +469,16 @@ class ShardedEndToEndStep(EndToEndStep):
         # (scene-owner mode: the single scene is rank 0's, so rank 0's graph context holds the warmup's
         # result and the calibration's stage times)
         if self.pipe is not None:
-            self.pipe.run(1, first_owner=0, **CFG)
+            self.pipe.run(1, first_owner=0, **self.cfg)
             return
         self.sh.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
-        self.sh.step(**CFG)
+        self.sh.step(**self.cfg)
 
     def run_steps(self, n):
         """n scenes; with the pipeline, S1 of scene k + 1 runs under the graph stages of scene k (in
         scene-owner mode scene k's graph stages run on rank k mod N only)"""
         if self.pipe is not None:
-            self.pipe.run(n, first_owner=0, **CFG)
+            self.pipe.run(n, first_owner=0, **self.cfg)
             return
         for _ in range(n):
             self.step()
@@ -488,7 +496,8 @@ class ShardedEndToEndStep(EndToEndStep):
         at = lambda i: (fr.depth[i].cpu().numpy(), fr.seg[i].cpu().numpy(), fr.intrinsics[i], fr.poses[i])  # noqa: E731
         s1 = s1_cpu_rate(fr.scene_points.astype(np.float32), at, len(fr.depth))
         col, lab, off = self.sh.mask_index
-        return e2e_cpu_baseline(s1, fr.num_points, self.F_total, col, lab, off, self.sh.pts.cpu().numpy())
+        return e2e_cpu_baseline(s1, fr.num_points, self.F_total, col, lab, off, self.sh.pts.cpu().numpy(),
+                                self.cfg)
 
 
 def c2_record(local, steps, warmup):
@@ -628,7 +637,7 @@ def api_timing(shape, seed, steps, warmup, replay=None, with_pp=False, profile=F
         fr = make_frames_shape(shape, seed=seed, device="cuda:0")
         log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
     fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
-    args = SimpleNamespace(debug=False, point_filter_threshold=0.5, **CFG)
+    args = SimpleNamespace(debug=False, **DATASET_THRESHOLDS[shape_thresholds(shape)[0]])
     ds = FrameDataset(fr, fids, raw_depth=raw_depth)
     parts = {"graph": [], "cluster": [], "post_process": []}
 
@@ -708,8 +717,7 @@ def run_post_process(a):
     fr = make_frames_shape(a.shape, seed=0, device="cuda:0")
     fids = [int(x) for x in np.arange(0, 10 * fr.num_frames, 10)]
     log(f"frames {fr.depth.shape} P={fr.num_points} rendered in {time.perf_counter() - t0:.1f} s")
-    args = SimpleNamespace(debug=False, mask_visible_threshold=0.3, undersegment_filter_threshold=0.3,
-                           view_consensus_threshold=0.9, contained_threshold=0.8, point_filter_threshold=0.5)
+    args = SimpleNamespace(debug=False, **DATASET_THRESHOLDS[shape_thresholds(a.shape)[0]])
     t0 = time.perf_counter()
     nodes, thr, mpc, pfm = construction.mask_graph_construction(args, fr.scene_points, fids, FrameDataset(fr, fids))
     objects = iterative_clustering.iterative_clustering(nodes, thr, args.view_consensus_threshold, False)
@@ -817,6 +825,7 @@ def run_sweep(a):
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     prm = _native.bp_params()
     objects = []
+    cfg = shape_thresholds(a.shape)[1]
 
     def scene(j):
         fr, pts, K, T = pool[j % len(pool)]
@@ -824,7 +833,7 @@ def run_sweep(a):
         ctx.backproject(None, None, None, None, prm, shape=tuple(fr.depth.shape),
                         device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), K.data_ptr(), T.data_ptr()))
         ctx.use_backprojection()
-        run.step(**CFG)
+        run.step(**cfg)
         return int(ctx.cluster_info().num_objects)
 
     for j in range(min(len(pool), max(a.warmup, 1))):
@@ -1071,6 +1080,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {"workload": runner.workload + f" M={gi.num_masks}", "variant": args.variant,
+                       "dataset_config": f"configs/{runner.dataset}.json", "thresholds": runner.cfg,
                        "scene_ms": round(ms_per_step, 4), "pairs_per_scene": pairs_per_step,
                        "iterations": int(ci.num_iterations), "objects": int(ci.num_objects),
                        "stage_ms": {k: round(v[0], 4) for k, v in calib.items()},

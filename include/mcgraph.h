@@ -165,6 +165,10 @@ int mc_backproject_frames_raw(mc_ctx *ctx, int32_t num_frames, int32_t height, i
                               const uint8_t *const *seg_frames, const double *intrinsics, const double *poses,
                               const mc_bp_params *params);
 int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info);
+/* S1's batching (no reference counterpart; the library's HBM budget, mc_ctx_set_memory_budget):
+ * out4 = {frames per batch at the end of the last call, mask-pixel capacity of the per-batch
+ * arrays, bytes those arrays hold, batches redone after a mask-pixel overflow (all calls)}       */
+int mc_backproject_get_batching(mc_ctx *ctx, int64_t *out4);
 /* kept masks in frame order then id order: mask_col (frame index), mask_label
  * (id), mask_off [M+1], mask_pts = sorted unique scene ids (mask_info[id], :148) */
 int mc_backproject_get_masks(mc_ctx *ctx, int32_t *mask_col, int32_t *mask_label, int64_t *mask_off,

@@ -33,7 +33,7 @@ EXPORTED = [
     "mc_cluster_run", "mc_cluster_get_info", "mc_cluster_get_level_sizes", "mc_cluster_get_level_caps", "mc_cluster_get_partition",
     "mc_cluster_get_edge_counts", "mc_cluster_get_final_labels", "mc_cluster_get_objects",
     "mc_bp_params_default", "mc_scene_set_points", "mc_backproject", "mc_backproject_frames", "mc_backproject_frames_raw",
-    "mc_backproject_get_info",
+    "mc_backproject_get_info", "mc_backproject_get_batching",
     "mc_backproject_get_masks", "mc_backproject_get_candidates", "mc_scene_use_backprojection",
     "mc_backproject_copy_points_device",
     "mc_pp_run", "mc_pp_get_info", "mc_pp_get_results", "mc_eval_match_counts", "mc_frames_decode",
@@ -165,6 +165,7 @@ def load():
         "mc_backproject_frames": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, P(BpParams)]),
         "mc_backproject_frames_raw": (ctypes.c_int, [vp, i32, i32, i32, vp, ctypes.c_double, vp, vp, vp, P(BpParams)]),
         "mc_backproject_get_info": (ctypes.c_int, [vp, P(BpInfo)]),
+        "mc_backproject_get_batching": (ctypes.c_int, [vp, vp]),
         "mc_backproject_get_masks": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "mc_backproject_copy_points_device": (ctypes.c_int, [vp, vp]),
         "mc_backproject_get_candidates": (ctypes.c_int, [vp, vp]),
@@ -638,6 +639,14 @@ def _bp_methods():
         self._check(self.L.mc_backproject_get_info(self.h, ctypes.byref(info)))
         return info
 
+    def bp_batching(self) -> dict:
+        """mc_backproject_get_batching: S1's frames per batch (last call), mask-pixel capacity, the
+        bytes the per-batch arrays hold, and the batches redone after a mask-pixel overflow."""
+        out = np.zeros(4, np.int64)
+        self._check(self.L.mc_backproject_get_batching(self.h, _ptr(out)))
+        return dict(frames_per_batch=int(out[0]), mask_pixel_cap=int(out[1]), bytes_held=int(out[2]),
+                    redone=int(out[3]))
+
     def bp_masks(self):
         info = self.bp_info()
         M = info.num_masks
@@ -670,8 +679,8 @@ def _bp_methods():
     def use_backprojection(self):
         self._check(self.L.mc_scene_use_backprojection(self.h))
 
-    for f in (set_points, backproject, backproject_frames, bp_info, bp_masks, bp_mask_index, bp_points_to_device, bp_candidates,
-              use_backprojection):
+    for f in (set_points, backproject, backproject_frames, bp_info, bp_batching, bp_masks, bp_mask_index,
+              bp_points_to_device, bp_candidates, use_backprojection):
         setattr(Context, f.__name__, f)
 
 

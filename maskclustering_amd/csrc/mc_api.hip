@@ -135,6 +135,9 @@ struct mc_ctx {
     int num_cu = 256;
     int64_t mem_budget = 0;  // bytes the S1 per-batch arrays may take (0: the default share, mc_backproject)
     size_t bp_px_cap = 0;  // mask-pixel capacity of the per-batch arrays (pixel-list positions)
+    int bp_last_fb = 0;    // frames per batch at the end of the last mc_backproject
+    bool bp_mfrac_obs = false;  // bp_mfrac comes from an earlier call's batches (not the initial guess)
+    int64_t bp_redo = 0;   // batches redone after a mask-pixel overflow (all calls)
     int bp_f_cap = 0;      // frame capacity of the per-batch arrays
     size_t bp_fpx_cap = 0; // frame-pixel capacity (the valid-id map)
     double bp_mfrac = 1.0; // mask pixels per frame pixel a batch is sized for (the largest seen, + margin)
@@ -2184,6 +2187,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         // test knob: MC_BP_MASK_FRAC sets the expected share (a small one forces the grow-and-redo path)
         if (const char *e = getenv("MC_BP_MASK_FRAC")) ctx->bp_mfrac = atof(e);
         const double mfrac = std::min(1.0, std::max(ctx->bp_mfrac, 1e-4));
+        size_t bud_bytes = 0;  // the per-batch arrays' byte budget (also bounds the grow-and-redo below)
         {
             const size_t held = ctx->bp_px_cap * kBpBytesPerMaskPixel + ctx->bp_fpx_cap * kBpBytesPerFramePixel;
             size_t bytes = static_cast<size_t>(ctx->mem_budget);
@@ -2193,9 +2197,11 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b)
                     bytes = std::min(total_b / 100 * 40, (free_b + held) / 100 * 65);
             }
+            bud_bytes = bytes;
             const double per_px = static_cast<double>(kBpBytesPerFramePixel) + mfrac * kBpBytesPerMaskPixel;
             budget = std::max<size_t>(HW, std::min(budget, static_cast<size_t>(static_cast<double>(bytes) / per_px)));
         }
+        const bool fixed_batch = getenv("MC_BP_BATCH_PIXELS") != nullptr;
         if (const char *e = getenv("MC_BP_BATCH_PIXELS")) budget = std::max<size_t>(1, strtoull(e, nullptr, 10));
         BpUpload *const up = on_device ? ctx->bp_up : nullptr;
         int FB = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(F, 1), budget / HW)));
@@ -2448,7 +2454,20 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             if (hs[BS_PXOVF]) {  // more mask pixels than the capacity (nothing past the pixel lists ran): grow, redo
                 const double frac = static_cast<double>(hs[BS_NPX]) / (static_cast<double>(fb) * HW);
                 ctx->bp_mfrac = std::max(ctx->bp_mfrac, frac);
-                bp_reserve(ctx, FB, H, W, nbands, std::max(mask_cap(frac), static_cast<size_t>(hs[BS_NPX]) + 1024), s);
+                // within the byte budget: at the observed share the batch takes fewer frames (a denser
+                // scene than the share learned so far), instead of arrays up to 1 / share times the budget
+                const int fb_was = FB;
+                if (!fixed_batch) {
+                    const double per_px = static_cast<double>(kBpBytesPerFramePixel) +
+                                          std::min(1.0, frac * 1.0625 + 1.0 / FB) * kBpBytesPerMaskPixel;
+                    const double fit = std::floor(static_cast<double>(bud_bytes) / (per_px * static_cast<double>(HW)));
+                    FB = std::max(1, std::min(FB, static_cast<int>(std::min(fit, 1e9))));
+                }
+                // the same frames again: room for every pixel they listed; fewer frames: the share's room
+                // (another overflow shrinks the batch or grows the arrays again, so the redo terminates)
+                bp_reserve(ctx, FB, H, W, nbands,
+                           FB < fb_was ? mask_cap(frac) : std::max(mask_cap(frac), static_cast<size_t>(hs[BS_NPX]) + 1024), s);
+                ctx->bp_redo++;
                 continue;
             }
             mfrac_seen = std::max(mfrac_seen, static_cast<double>(hs[BS_NPX]) / (static_cast<double>(fb) * HW));
@@ -2501,7 +2520,14 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             ctx->bp_nnz += nnzb;
             b0 += fb;
         }
-        if (mfrac_seen > 0.0) ctx->bp_mfrac = mfrac_seen;  // the next call's batches are sized for it
+        // the next call's batches are sized for the share seen, decaying from the larger of earlier calls
+        // (a stream of scenes on one context: a sparse scene does not at once size batches a denser one
+        // after it overflows)
+        if (mfrac_seen > 0.0) {
+            ctx->bp_mfrac = ctx->bp_mfrac_obs ? std::max(mfrac_seen, 0.5 * (ctx->bp_mfrac + mfrac_seen)) : mfrac_seen;
+            ctx->bp_mfrac_obs = true;
+        }
+        ctx->bp_last_fb = FB;
         unpack();
         MC_HIP(hipStreamSynchronize(s));
         ctx->have_bp = true;
@@ -2517,6 +2543,17 @@ int mc_backproject_get_info(mc_ctx *ctx, mc_bp_info *info)
         info->num_masks = static_cast<int32_t>(ctx->bp_col.size());
         info->error_frame = ctx->bp_err_frame;
         info->num_mask_points = ctx->bp_nnz;
+    });
+}
+
+int mc_backproject_get_batching(mc_ctx *ctx, int64_t *out4)
+{
+    return guarded(ctx, [&] {
+        MC_REQUIRE(out4, MC_ERR_INVALID, "null output");
+        out4[0] = ctx->bp_last_fb;
+        out4[1] = static_cast<int64_t>(ctx->bp_px_cap);
+        out4[2] = static_cast<int64_t>(ctx->bp_px_cap * kBpBytesPerMaskPixel + ctx->bp_fpx_cap * kBpBytesPerFramePixel);
+        out4[3] = ctx->bp_redo;
     });
 }
 

@@ -118,7 +118,14 @@ def _comm_device(group, like: torch.device) -> torch.device:
     return like if like.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
 
 
-_GATHER_OK = [True]  # cleared if the backend refuses dist.gather (gather_masks then all-gathers)
+# backends whose torch.distributed gather the scene-owner path uses (RCCL "nccl" implements it over
+# point-to-point sends, gloo natively); any other backend all-gathers and keeps the owner's share.
+# Decided from the group's backend, which every rank reads the same, so all ranks take one branch.
+_GATHER_BACKENDS = ("nccl", "gloo")
+
+
+def _gather_supported(group=None) -> bool:
+    return str(dist.get_backend(group)) in _GATHER_BACKENDS
 
 
 def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_lo: int, group=None,
@@ -182,25 +189,19 @@ def gather_masks(mask_col, mask_label, mask_off, mask_pts: torch.Tensor, frame_l
         points_ready()
     buf = torch.zeros(nmax, dtype=torch.int32, device=dev)
     buf[:nnz] = mask_pts[:nnz].to(dev)
-    if dst is not None and _GATHER_OK[0]:
+    if dst is not None and _gather_supported(group):
         me = dist.get_rank(group)
         gdst = dst if group is None else dist.get_global_rank(group, dst)
         parts = [torch.empty(nmax, dtype=torch.int32, device=dev) for _ in range(world)] if me == dst else None
-        try:
-            dist.gather(buf, parts, dst=gdst, group=group)
-        except (RuntimeError, NotImplementedError) as e:
-            # a backend without gather refuses it on every rank before any transfer: the all-gather
-            # below serves instead, from now on
-            if "support" not in str(e).lower():
-                raise
-            _GATHER_OK[0] = False
-        else:
-            if me != dst:
-                return g_col, g_lab, g_off, None
-            return g_col, g_lab, g_off, torch.cat([parts[r][:int(Ns[r])] for r in range(world)]).to(out_dev)
+        dist.gather(buf, parts, dst=gdst, group=group)
+        if me != dst:
+            return g_col, g_lab, g_off, None
+        return g_col, g_lab, g_off, torch.cat([parts[r][:int(Ns[r])] for r in range(world)]).to(out_dev)
     allp = torch.empty(world * nmax, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(allp, buf, group=group)
     allp = allp.view(world, nmax).to(out_dev)
+    if dst is not None and dist.get_rank(group) != dst:
+        return g_col, g_lab, g_off, None
     g_pts = torch.cat([allp[r, :int(Ns[r])] for r in range(world)])
     return g_col, g_lab, g_off, g_pts
 
@@ -219,6 +220,17 @@ def _check_same_on_all_ranks(costs: np.ndarray, group=None):
     dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
     if int(lo.item()) != int(hi.item()):
         raise ValueError("the ranks hold different frame cost vectors: their frame slices would disagree")
+
+
+def _stream_wait(stream: int, cur, device):
+    """Make HIP stream `stream` (a library context's; 0 = the null stream) wait on torch stream
+    `cur` on the device: an event, no host wait (the null stream waits on the host)."""
+    if stream == int(cur.cuda_stream):
+        return
+    if stream == 0:
+        cur.synchronize()
+        return
+    torch.cuda.ExternalStream(stream, device=device).wait_stream(cur)
 
 
 class FrameShardedScene:
@@ -401,7 +413,12 @@ class ScenePipeline:
         s1.backproject(None, None, None, None, self.params, shape=(n, H, W),
                        device_ptrs=(depth.data_ptr(), seg.data_ptr(), K.data_ptr(), T.data_ptr()))
         col, lab, off = s1.bp_mask_index()
+        # pts comes from torch's caching allocator on torch's current stream, and the block may be one
+        # the consumer freed while its reads (the gather, a cat) are still queued there: the S1
+        # stream writes it only after torch's stream has drained up to this point
         pts = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=depth.device)
+        if depth.device.type == "cuda":
+            _stream_wait(int(s1.stream() or 0), torch.cuda.current_stream(depth.device), depth.device)
         s1.bp_points_to_device(pts.data_ptr())
         s1.synchronize()  # the ids are complete before another stream reads them
         return col, lab, off, pts
@@ -429,8 +446,13 @@ class ScenePipeline:
                             continue
                     if stop.is_set():
                         return
-            except BaseException as e:  # handed to the consumer, which raises it
-                q.put(e)
+            except BaseException as e:  # handed to the consumer, which raises it (dropped once it stopped)
+                while not stop.is_set():
+                    try:
+                        q.put(e, timeout=0.5)
+                        break
+                    except queue.Full:
+                        continue
 
         ths = [threading.Thread(target=produce, args=(i,), name=f"s1-producer-{i}", daemon=True) for i in range(NP)]
         for th in ths:
@@ -454,6 +476,9 @@ class ScenePipeline:
                     g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks)
                 sh.mask_index = (g_col, g_lab, g_off)
                 sh.pts = g_pts
+                # the graph context's stream reads the gathered ids (written on torch's stream) next
+                if g_pts.device.type == "cuda":
+                    sh._order_streams(torch_after_ctx=False, device=g_pts.device)
                 # set_masks copies the ids into the graph context and synchronises its stream before
                 # it returns (mc_scene_set_masks validates them on the host), so the producer's
                 # tensors, allocated on its thread's stream, are free to be reused afterwards

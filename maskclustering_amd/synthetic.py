@@ -83,6 +83,9 @@ SHAPES = {
     "tiny": dict(num_points=2_000, num_frames=24, num_objects=24, win=0.12),
     "c1": dict(num_points=20_000, num_frames=100, num_objects=240, win=0.05),
     "c2": dict(num_points=240_000, num_frames=250, num_objects=600, win=0.05),
+    # 2xC2 (SURVEY.md §8(d)(i)'s third point of the reference's T(M) fit): twice the frames, points
+    # and objects at the same masks per frame, so M doubles
+    "c2x2": dict(num_points=480_000, num_frames=500, num_objects=1200, win=0.025),
     "c3": dict(num_points=1_000_000, num_frames=1500, num_objects=2000, win=0.0133),
     "c4": dict(num_points=1_500_000, num_frames=2000, num_objects=3000, win=0.01),
 }

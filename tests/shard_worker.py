@@ -147,6 +147,9 @@ def main():
                 def synchronize(self):
                     pass
 
+                def stream(self):
+                    return 0
+
             run = OracleRun()
             owner = mode.startswith(("owner:", "owner2:"))
             producers = 2 if mode.startswith("owner2:") else 1  # S1 contexts (producer threads)
@@ -221,13 +224,22 @@ def main():
             sh.set_local_masks(col, lab, off, torch.from_numpy(pts).cuda())
             sh.step(**CFGS["scannet"])
             np.savez(out, **{k: np.asarray(v) for k, v in run.canonical(dense=False).items()})
-        elif mode == "gather":
+        elif mode in ("gather", "gather_dst", "gather_dst_nogather"):
+            # gather: every rank gets the global list; gather_dst: the point ids go to the last rank
+            # alone (dist.gather, the scene-owner path); gather_dst_nogather: the same as if the
+            # backend had no gather (the all-gather branch, every rank choosing it from the backend)
+            from maskclustering_amd import frame_shard
             from maskclustering_amd.synthetic import make_shape
+            if mode == "gather_dst_nogather":
+                frame_shard._GATHER_BACKENDS = ()
             s = make_shape("tiny", seed=4)
             lo, hi = frame_slice(s.num_frames, world, rank)
             col, lab, off, pts = local_masks(s, lo, hi)
-            g = gather_masks(col, lab, off, torch.from_numpy(pts), lo, max_masks=255 * (s.num_frames // world + 1))
-            np.savez(out, col=g[0], label=g[1], off=g[2], pts=g[3].numpy())
+            dst = None if mode == "gather" else world - 1
+            g = gather_masks(col, lab, off, torch.from_numpy(pts), lo, max_masks=255 * (s.num_frames // world + 1),
+                             dst=dst)
+            np.savez(out, col=g[0], label=g[1], off=g[2], pts=g[3].numpy() if g[3] is not None else np.zeros(0, np.int32),
+                     has_pts=np.array([g[3] is not None]))
         else:
             from maskclustering_amd.pipeline import GraphRun
             from maskclustering_amd.synthetic_frames import make_frames_shape

@@ -100,6 +100,86 @@ def test_gather_equals_global_mask_list(tmp_path, world):
         np.testing.assert_array_equal(z["pts"], s.mask_pts)
 
 
+@pytest.mark.parametrize("mode", ["gather_dst", "gather_dst_nogather"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_to_one_rank(tmp_path, world, mode):
+    """gather_masks(dst=last rank): every rank gets the global mask index, only dst the point ids, by
+    dist.gather or (a backend without gather, chosen alike on every rank) by the all-gather."""
+    from maskclustering_amd.synthetic import make_shape
+    s = make_shape("tiny", seed=4)
+    for r, out in enumerate(run_ranks(mode, world, tmp_path)):
+        z = np.load(out)
+        np.testing.assert_array_equal(z["col"], s.mask_col)
+        np.testing.assert_array_equal(z["label"], s.mask_label)
+        np.testing.assert_array_equal(z["off"], s.mask_off)
+        assert bool(z["has_pts"][0]) == (r == world - 1)
+        if r == world - 1:
+            np.testing.assert_array_equal(z["pts"], s.mask_pts)
+
+
+def test_scene_pipeline_producer_and_consumer_errors_do_not_hang():
+    """The consumer raises (on_scene) while a producer holds an exception for a full queue: run()
+    re-raises the consumer's error promptly instead of waiting on the producer forever."""
+    import threading
+
+    import torch
+    from maskclustering_amd.frame_shard import FrameShardedScene, ScenePipeline
+    failed = threading.Event()
+
+    class S1Ctx:
+        n = 0
+
+        def backproject(self, *a, **kw):
+            S1Ctx.n += 1
+            if S1Ctx.n == 3:
+                failed.set()
+                raise RuntimeError("producer failure")
+
+        def bp_mask_index(self):
+            return np.zeros(1, np.int32), np.ones(1, np.int32), np.array([0, 2], np.int64)
+
+        def bp_points_to_device(self, dst):
+            pass
+
+        def synchronize(self):
+            pass
+
+        def stream(self):
+            return 0
+
+    class Run:
+        ctx = None
+
+        def set_masks(self, *a, **kw):
+            pass
+
+        def step(self, *a):
+            pass
+
+    sh = FrameShardedScene(Run(), 10, 1, shard_graph=False)
+    z = torch.zeros((1, 1, 1))
+
+    def on_scene(k):
+        failed.wait(10)  # the producer's error is pending behind the queued scene 1
+        raise ValueError("consumer failure")
+
+    pipe = ScenePipeline(sh, S1Ctx(), z, z.to(torch.uint8), torch.zeros((1, 4), dtype=torch.float64),
+                         torch.zeros((1, 16), dtype=torch.float64))
+    err = []
+
+    def go():
+        try:
+            pipe.run(5, on_scene=on_scene, **KW["scannet"])
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+
+    th = threading.Thread(target=go, daemon=True)
+    th.start()
+    th.join(20)
+    assert not th.is_alive(), "ScenePipeline.run hung on the producer's pending exception"
+    assert len(err) == 1 and isinstance(err[0], ValueError)
+
+
 KW = {"scannet": dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
                       contained_threshold=0.8),
       "scannetpp": dict(mask_visible_threshold=0.4, undersegment_filter_threshold=0.2, view_consensus_threshold=1,

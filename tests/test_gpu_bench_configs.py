@@ -8,7 +8,7 @@ the C-ABI against the CPU oracle, bit for bit:
   mc_backproject against the oracle's S1, per candidate mask statistics and neighbour sets.
 * ``c3_e2e``: the full C3 scene as the bench runs it (1500 frames resident in HBM, S1 -> S6): every
   frame's S1 against the oracle's, then S2-S6 against the sparse oracle (oracle/graph_sparse.c) on
-  that mask set.
+  that mask set, under configs/scannetpp.json's thresholds (the bench's C3 line) and scannet's.
 * ``c4``: the Matterport-region-shaped scene (BASELINE configs[3]: 2000 frames of 1280x1024, depth in
   1/4000 m units, ~120k masks): the whole scene S1 -> S6 on the device, every frame's S1 against the
   oracle's (100 frames at a time), then S2-S6 against the sparse oracle on the device's mask set.
@@ -23,8 +23,9 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
-           contained_threshold=0.8)
+from maskclustering_amd.dataset_configs import graph_thresholds
+
+CFG = graph_thresholds("scannet")  # C2 = the ScanNet-shaped scene
 # oracle stats columns: id npix nvox ndbscan nsor ncand ncovered nneighbors kept
 # device stats columns: frame id npix nvox ndbscan nsor -1 ncovered nneighbors kept
 CMP_COLS = [(1, 0), (2, 1), (3, 2), (4, 3), (5, 4), (7, 6), (8, 7), (9, 8)]
@@ -132,17 +133,25 @@ def test_c3_e2e_matches_oracle():
     assert len(col) > 70_000
     run.P, run.F = len(t_scene), F
     run.mask_col, run.mask_label = col, lab
-    ctx.use_backprojection()
-    run.step(**CFG)
+    # S2-S6 under the ScanNet++ config the bench's C3 line runs (configs/scannetpp.json: ct = 1, whose
+    # edge rule needs S >= 2 at O = 1), then under configs/scannet.json, on the same resident masks
+    for ds in ("scannetpp", "scannet"):
+        cfg = graph_thresholds(ds)
+        ctx.use_backprojection()
+        run.step(**cfg)
+        _assert_graph_matches(run, len(t_scene), F, col, lab, off, pts, cfg, ds)
+
+
+def _assert_graph_matches(run, P, F, col, lab, off, pts, cfg, what):
     got = run.canonical(dense=False)
-    want = oracle.run_sparse(len(t_scene), F, col.astype(np.int32), lab.astype(np.int32), np.asarray(off, np.int64),
-                             np.asarray(pts, np.int32), **CFG)
+    want = oracle.run_sparse(P, F, col.astype(np.int32), lab.astype(np.int32), np.asarray(off, np.int64),
+                             np.asarray(pts, np.int32), **cfg)
     for k in ["gl_col", "gl_label", "boundary", "vf_bits", "c_row", "c_col", "undersegment", "node0_g", "thr_value",
               "thr_is_int", "num_iters", "level_sizes", "edge_counts", "obj_mask_off", "obj_mask_idx", "obj_pt_off",
               "obj_pt_idx", "obj_vf_bits", "obj_c_off", "obj_c_idx", "obj_node_info"]:
-        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=k)
+        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=f"{what}: {k}")
     for t in range(int(want["num_iters"])):
-        np.testing.assert_array_equal(got[f"part_{t}"], want[f"part_{t}"], err_msg=f"partition {t}")
+        np.testing.assert_array_equal(got[f"part_{t}"], want[f"part_{t}"], err_msg=f"{what}: partition {t}")
 
 
 def _c4_frames_window():
@@ -193,14 +202,7 @@ def test_c4_e2e_matches_oracle():
     assert len(col) > 100_000
     run.P, run.F = len(t_scene), F
     run.mask_col, run.mask_label = col, lab
+    cfg = graph_thresholds("matterport3d")  # configs/matterport3d.json
     ctx.use_backprojection()
-    run.step(**CFG)
-    got = run.canonical(dense=False)
-    want = oracle.run_sparse(len(t_scene), F, col.astype(np.int32), lab.astype(np.int32), np.asarray(off, np.int64),
-                             np.asarray(pts, np.int32), **CFG)
-    for k in ["gl_col", "gl_label", "boundary", "vf_bits", "c_row", "c_col", "undersegment", "node0_g", "thr_value",
-              "thr_is_int", "num_iters", "level_sizes", "edge_counts", "obj_mask_off", "obj_mask_idx", "obj_pt_off",
-              "obj_pt_idx", "obj_vf_bits", "obj_c_off", "obj_c_idx", "obj_node_info"]:
-        np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=k)
-    for t in range(int(want["num_iters"])):
-        np.testing.assert_array_equal(got[f"part_{t}"], want[f"part_{t}"], err_msg=f"partition {t}")
+    run.step(**cfg)
+    _assert_graph_matches(run, len(t_scene), F, col, lab, off, pts, cfg, "matterport3d")

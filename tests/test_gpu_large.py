@@ -1,5 +1,5 @@
-"""Parity at the large BASELINE configs on one GPU: C3 (ScanNet++-shaped, M ≈ 81k) and C4
-(Matterport-shaped stress, M ≈ 123k), the HIP path through the C-ABI against the sparse CPU
+"""Parity at the large BASELINE configs on one GPU: C3 (ScanNet++-shaped, M ≈ 81k, under
+configs/scannetpp.json and configs/scannet.json) and C4 (Matterport-shaped stress, M ≈ 123k), the HIP path through the C-ABI against the sparse CPU
 oracle (oracle/graph_sparse.c, pinned to the reference's own fixtures by
 tests/test_oracle_golden.py).  Every stage's canonical output is compared bit for bit except the
 dense point-in-mask / point-frame matrices (3 GB / 6 GB at these sizes; covered at C1/C2)."""
@@ -10,16 +10,18 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
-           contained_threshold=0.8)
+from maskclustering_amd.dataset_configs import graph_thresholds
 KEYS = ["gl_col", "gl_label", "boundary", "vf_bits", "c_row", "c_col", "undersegment", "node0_g", "observer_hist",
         "thr_value", "thr_is_int", "num_iters", "level_sizes", "edge_counts", "obj_mask_off", "obj_mask_idx",
         "obj_pt_off", "obj_pt_idx", "obj_vf_bits", "obj_c_off", "obj_c_idx", "obj_node_info", "obj_son_off",
         "obj_son_idx"]
 
 
-@pytest.mark.parametrize("shape", ["c3", "c4"])
-def test_large_scene_vs_sparse_oracle(shape):
+# each shape under its own dataset config (C3 ScanNet++ with ct = 1, C4 Matterport3D), and C3 also under
+# the ScanNet thresholds
+@pytest.mark.parametrize("shape,dataset", [("c3", "scannetpp"), ("c3", "scannet"), ("c4", "matterport3d")])
+def test_large_scene_vs_sparse_oracle(shape, dataset):
+    CFG = graph_thresholds(dataset)
     from maskclustering_amd.pipeline import GraphRun
     from maskclustering_amd.synthetic import make_shape
     s = make_shape(shape, seed=0)

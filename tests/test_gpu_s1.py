@@ -353,3 +353,42 @@ def test_two_contexts_share_a_device_under_budgets():
         np.testing.assert_array_equal(x, z)
     with pytest.raises(_native.McError):
         b.set_memory_budget(-1)
+
+
+def test_denser_scene_after_sparse_one_stays_within_budget():
+    """A stream of scenes on one context: the batches of a sparse scene are sized for its
+    small mask-pixel share, so a denser scene after it overflows the per-batch arrays; the redo must
+    take fewer frames per batch within the context's HBM budget (mc_ctx_set_memory_budget), not grow
+    the arrays to the whole batch's mask pixels, and give the masks of a context without a budget."""
+    from maskclustering_amd import _native
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    fr = make_frames_shape("small", seed=2)
+    F, H, W = fr.depth.shape
+    HW = H * W
+    sparse = fr.seg.copy()
+    for f in range(F):  # one mask per frame: the smallest id
+        ids = np.unique(sparse[f])
+        ids = ids[ids != 0]
+        if len(ids):
+            sparse[f][sparse[f] != ids[0]] = 0
+    valid = (fr.depth > 0) & (fr.depth <= 20)
+    dense_px = int(((fr.seg != 0) & valid).sum())
+    sparse_px = int(((sparse != 0) & valid).sum())
+    budget = max(int(0.5 * dense_px * 196), 250 * HW)
+    assert dense_px * 196 > budget and sparse_px * 196 * 4 < budget   # the case the redo must bound
+    ref = _native.Context(0)
+    want_sparse = _run(ref, fr.scene_points, fr.depth, sparse, fr.intrinsics, fr.poses)
+    want_dense = _run(ref, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    ctx = _native.Context(0)
+    ctx.set_memory_budget(budget)
+    got_sparse = _run(ctx, fr.scene_points, fr.depth, sparse, fr.intrinsics, fr.poses)
+    before = ctx.bp_batching()
+    got_dense = _run(ctx, fr.scene_points, fr.depth, fr.seg, fr.intrinsics, fr.poses)
+    after = ctx.bp_batching()
+    for x, y in zip(want_sparse, got_sparse):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(want_dense, got_dense):
+        np.testing.assert_array_equal(x, y)
+    assert after["redone"] > before["redone"], (before, after)
+    assert after["frames_per_batch"] < F, after
+    assert after["bytes_held"] <= budget + 196 * HW + 4 * F * HW + 196 * 2048, (budget, after)
