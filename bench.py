@@ -45,7 +45,7 @@ from maskclustering_amd.dataset_configs import DATASET_THRESHOLDS, shape_thresho
 CFG = shape_thresholds("c2")[1]
 G_GROUPS = ["s2_point_lists", "s3_masks", "s3_undo_s5", "s4_observer_hist", "s6_columns", "s6_pairs",
             "s6_components", "s6_merge", "s7_points"]
-BP_GROUPS = ["bp_pixels", "bp_voxel", "bp_denoise", "bp_query"]
+BP_GROUPS = ["bp_grid", "bp_pixels", "bp_voxel", "bp_denoise", "bp_query"]
 
 
 def log(*a):
@@ -317,6 +317,8 @@ class EndToEndStep:
                          f"S1-S6")
 
     def step(self):
+        # a new scene's points (mc_scene_set_points): its ball-query grid is built inside the step
+        self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=self.fr.num_points)
         self.ctx.backproject(None, None, None, None, self.prm, shape=self.shape,
                              device_ptrs=(self.t_depth.data_ptr(), self.t_seg.data_ptr(), self.t_K.data_ptr(),
                                           self.t_T.data_ptr()))
@@ -426,6 +428,8 @@ class ShardedEndToEndStep(EndToEndStep):
         self.scene_owner = pipelined and world > 1 and os.environ.get("MC_BENCH_SCENE_OWNER", "1") != "0"
         self.sh = FrameShardedScene(self.run, fr.num_points, F, costs=costs, native_comm=native,
                                     shard_graph=not self.scene_owner)
+        self.costs, self.native, self.local_dev = costs, native, local
+        self._lat = None
         assert (self.sh.lo, self.sh.hi) == (lo, hi)
         up = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.t_depth, self.t_seg = fr.depth, fr.seg
@@ -458,7 +462,8 @@ class ShardedEndToEndStep(EndToEndStep):
                 s1ctxs.append(c)
             self.s1ctx = s1ctxs[0]
             self.pipe = ScenePipeline(self.sh, s1ctxs if len(s1ctxs) > 1 else self.s1ctx, self.t_depth, self.t_seg,
-                                      self.t_K, self.t_T, self.prm, scene_owner=self.scene_owner)
+                                      self.t_K, self.t_T, self.prm, scene_owner=self.scene_owner,
+                                      scene_points=self.t_scene)
             self.timing_ctxs = [self.ctx] + s1ctxs
             self.pipe.warm()  # the other producers' first calls, outside the timed region
         log(f"rank {self.sh.rank}: frames [{lo}, {hi}) of {F} rendered in {time.perf_counter() - t0:.1f} s")
@@ -471,6 +476,7 @@ class ShardedEndToEndStep(EndToEndStep):
         if self.pipe is not None:
             self.pipe.run(1, first_owner=0, **self.cfg)
             return
+        self.ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=self.fr.num_points)
         self.sh.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm)
         self.sh.step(**self.cfg)
 
@@ -482,6 +488,26 @@ class ShardedEndToEndStep(EndToEndStep):
             return
         for _ in range(n):
             self.step()
+
+    def latency_steps(self, n):
+        """n scenes one at a time, every rank on each (the MC_BENCH_PIPELINE=0 path, strong scaling of
+        one scene's latency): S1 of this rank's slice on the pipeline's S1 context, the mask
+        all-gather, then S2-S6 row-block sharded over the ranks (graph_shard.ShardedGraph) on a graph
+        context of its own.  Collective on every rank."""
+        import torch
+        from maskclustering_amd.frame_shard import FrameShardedScene
+        from maskclustering_amd.pipeline import GraphRun
+        if self._lat is None:
+            run = GraphRun(self.local_dev)
+            run.ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+            self._lat = FrameShardedScene(run, self.fr.num_points, self.F_total, costs=self.costs,
+                                          native_comm=self.native, shard_graph=True)
+            assert (self._lat.lo, self._lat.hi) == (self.sh.lo, self.sh.hi)
+        for _ in range(n):
+            self.s1ctx.set_points(device_ptr=self.t_scene.data_ptr(), num_points=self.fr.num_points)
+            self._lat.backproject(self.t_depth, self.t_seg, self.t_K, self.t_T, self.prm, s1_ctx=self.s1ctx)
+            self._lat.step(**self.cfg)
+        return self._lat
 
     def work(self):
         F, H, W = self.shape
@@ -800,8 +826,7 @@ def run_sweep(a):
     seed + rank * pool + j).  value = wall time of all --scenes scenes (max over ranks)."""
     import torch
     import torch.distributed as dist
-    from maskclustering_amd import _native
-    from maskclustering_amd.pipeline import GraphRun
+    from maskclustering_amd.sweep import SceneSweep, scenes_of
     from maskclustering_amd.synthetic_frames import make_frames_shape
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -811,7 +836,7 @@ def run_sweep(a):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    mine = list(range(rank, a.scenes, world))
+    mine = scenes_of(rank, world, a.scenes)
     pool = []
     t0 = time.perf_counter()
     for j in range(min(a.pool, max(len(mine), 1))):
@@ -820,21 +845,12 @@ def run_sweep(a):
                      torch.from_numpy(np.ascontiguousarray(fr.intrinsics)).to(dev),
                      torch.from_numpy(np.ascontiguousarray(fr.poses.reshape(-1, 16))).to(dev)))
     log(f"rank {rank}: {len(mine)} scenes from a pool of {len(pool)} rendered in {time.perf_counter() - t0:.1f} s")
-    run = GraphRun(local)
-    ctx = run.ctx
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    prm = _native.bp_params()
+    sw = SceneSweep(local, shape_thresholds(a.shape)[1], stream=torch.cuda.current_stream().cuda_stream)
     objects = []
-    cfg = shape_thresholds(a.shape)[1]
 
     def scene(j):
         fr, pts, K, T = pool[j % len(pool)]
-        ctx.set_points(device_ptr=pts.data_ptr(), num_points=fr.num_points)
-        ctx.backproject(None, None, None, None, prm, shape=tuple(fr.depth.shape),
-                        device_ptrs=(fr.depth.data_ptr(), fr.seg.data_ptr(), K.data_ptr(), T.data_ptr()))
-        ctx.use_backprojection()
-        run.step(**cfg)
-        return int(ctx.cluster_info().num_objects)
+        return sw.run_scene(pts, fr.depth, fr.seg, K, T)
 
     for j in range(min(len(pool), max(a.warmup, 1))):
         scene(j)
@@ -887,6 +903,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 E2E / G record (N=1 only)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the one-scene-at-a-time latency record")
     ap.add_argument("--shard", choices=["scene", "frames"], default="frames",
                     help="frames: one scene, its frames split over the ranks, S2-S6 row-block sharded (strong "
                          "scaling; the north_star's ScanNet++-sized C3 by default); scene: every rank its own "
@@ -966,6 +983,9 @@ def main():
         c.reset_kernel_times()
         c.set_timing_filter(dominant)
         c.set_timing(True)
+    pipe = getattr(runner, "pipe", None)
+    if pipe is not None:
+        pipe.gather_s, pipe.gathers = 0.0, 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -982,11 +1002,29 @@ def main():
     for c in tctxs:
         c.set_timing(False)
     dom_ms, dom_n = ktime(dominant)
-    t = torch.tensor([elapsed], dtype=torch.float64,
+    gather_ms = 1e3 * pipe.gather_s / max(pipe.gathers, 1) if pipe is not None else 0.0
+    # the one-scene-at-a-time latency beside the pipelined throughput (frame-sharded e2e with the pipeline):
+    # the same barrier / synchronize discipline, max over ranks
+    lat_elapsed, lat_n = 0.0, 0
+    if pipe is not None and hasattr(runner, "latency_steps") and not args.no_latency:
+        lat_n = max(2, min(args.steps, 5))
+        runner.latency_steps(1)  # its graph context's first call
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tl = time.perf_counter()
+        runner.latency_steps(lat_n)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        lat_elapsed = time.perf_counter() - tl
+    from maskclustering_amd.frame_shard import rccl_comm_ranks
+    rccl_ranks = rccl_comm_ranks() if world > 1 else None
+    t = torch.tensor([elapsed, gather_ms, lat_elapsed], dtype=torch.float64,
                      device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, gather_ms, lat_elapsed = (float(x) for x in t.tolist())
     if not has_graph:
         dist.destroy_process_group()
         return
@@ -1027,6 +1065,7 @@ def main():
                     stages[g]["frac"] = stages[g].pop("alt_frac")
 
     cpu = None
+    ms_per_step_pre = elapsed / args.steps * 1e3
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = runner.cpu_baseline()
         ratio_path = os.path.join(REPO, "profiles", f"cpu_ratio_{args.shape}.json")
@@ -1044,6 +1083,21 @@ def main():
                         "installed in the build container or on the box, so only its S2-S6 was timed against the C port "
                         f"(profiles/cpu_ratio_c2.json: the reference over the port for S2-S6 on C2); S1 here is the "
                         "port's restatement (oracle/s1_oracle.c), timed on all host threads (value) and on one (single_thread)"}
+        fit_path = os.path.join(REPO, "profiles", "cpu_ref_fit.json")
+        if os.path.exists(fit_path) and args.variant in ("e2e", "g"):
+            # the reference's S2-S6 at this scene's M, EXTRAPOLATED from its T(M) fit over C1 / C2 / 2xC2 (it
+            # cannot run C3 / C4: dense M x M float32 matrices)
+            fit = json.load(open(fit_path))
+            M_run = int(ctx.graph_info().num_masks)
+            t_ref = fit["a"] * M_run ** fit["b"]
+            cpu.setdefault("reference_context", {})["reference_s2_s6_extrapolated"] = {
+                "seconds": round(t_ref, 1), "M": M_run, "fit": f"T(M) = {fit['a']:.4g} * M^{fit['b']}",
+                "points": [(p["shape"], p["M"], p["reference_s"]) for p in fit["points"]],
+                "label": "EXTRAPOLATED (not run): the reference's own S2-S6 timed on the 8-core build container at "
+                         "C1, C2 and 2xC2 under configs/scannet.json thresholds (scripts/cpu_ratio.py, "
+                         "scripts/cpu_ref_fit.py); S1 excluded (Open3D / pytorch3d absent)",
+                "source": os.path.relpath(fit_path, REPO),
+                "over_device_scene": round(t_ref * 1e3 / max(ms_per_step_pre, 1e-9), 1)}
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary and args.variant in ("e2e", "g"):
@@ -1097,6 +1151,20 @@ def main():
             "stage_roofline": stages,
             "cpu_baseline": cpu,
         }
+        if world > 1:
+            line["rccl_comm_ranks"] = rccl_ranks  # ncclCommCount on the job's communicator (None under gloo)
+            line["backend"] = dist.get_backend()
+        if pipe is not None:
+            line["gather_ms_per_scene"] = round(gather_ms, 4)
+            line["gather_note"] = ("host wall time per scene in gather_masks (mask metadata all-gather + point-id "
+                                   "gather to the scene's owner), max over ranks; it includes waiting for the slowest "
+                                   "rank's S1 of the scene" if world > 1 else "one process: no collective")
+        if lat_n:
+            line["latency"] = {
+                "ms_per_scene": round(1e3 * lat_elapsed / lat_n, 4), "scenes": lat_n,
+                "mode": "one scene at a time, every rank on it (MC_BENCH_PIPELINE=0 path): S1 of each rank's "
+                        "frame slice, mask all-gather, S2-S6 row-block sharded over the ranks; max over ranks",
+                "scene_ms_pipelined": round(ms_per_step, 4)}
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)

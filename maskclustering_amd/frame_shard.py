@@ -17,6 +17,8 @@ Exchanges per scene: the mask lists (C2 ≈ 15 MB of point ids, C3 ≈ 105 MB), 
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -222,6 +224,26 @@ def _check_same_on_all_ranks(costs: np.ndarray, group=None):
         raise ValueError("the ranks hold different frame cost vectors: their frame slices would disagree")
 
 
+def rccl_comm_ranks(group=None):
+    """The rank count RCCL's own communicator of the group reports (ncclCommCount on the communicator
+    torch's "nccl" backend made, from torch's librccl), or None: another backend, or no communicator
+    yet (it is made by the first collective on the device)."""
+    import ctypes
+    import os
+    if not dist.is_initialized() or dist.get_backend(group) != "nccl":
+        return None
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    try:
+        ptr = int(pg._get_backend(torch.device("cuda", torch.cuda.current_device()))._comm_ptr())
+    except (RuntimeError, AttributeError):
+        return None
+    if not ptr:
+        return None
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+    cnt = ctypes.c_int(0)
+    return int(cnt.value) if lib.ncclCommCount(ctypes.c_void_p(ptr), ctypes.byref(cnt)) == 0 else None
+
+
 def _stream_wait(stream: int, cur, device):
     """Make HIP stream `stream` (a library context's; 0 = the null stream) wait on torch stream
     `cur` on the device: an event, no host wait (the null stream waits on the host)."""
@@ -294,9 +316,10 @@ class FrameShardedScene:
         return g_col, g_lab, g_off
 
     def backproject(self, depth: torch.Tensor, seg: torch.Tensor, intrinsics: torch.Tensor,
-                    poses: torch.Tensor, params=None):
+                    poses: torch.Tensor, params=None, s1_ctx=None):
         """depth f32 [n,H,W], seg u8 [n,H,W], intrinsics f64 [n,4], poses f64 [n,16] on this
-        rank's GPU, n = hi - lo.  Leaves the global masks as the graph input."""
+        rank's GPU, n = hi - lo.  Leaves the global masks as the graph input.  s1_ctx (optional): the
+        context S1 runs on (its scene points set), instead of the graph context."""
         n = self.hi - self.lo
         if depth.shape[0] != n or seg.shape != depth.shape or intrinsics.shape[0] != n or poses.shape[0] != n:
             raise ValueError(f"rank {self.rank} owns {n} frames [{self.lo}, {self.hi})")
@@ -305,7 +328,8 @@ class FrameShardedScene:
             if t.dtype != dt or not t.is_contiguous() or t.device.type != "cuda":
                 raise ValueError("frame inputs must be contiguous device tensors (f32, u8, f64, f64)")
         _, H, W = depth.shape
-        if n and self.world == 1:  # one process: the back-projection result is the graph input as it is
+        c1 = self.ctx if s1_ctx is None else s1_ctx
+        if n and self.world == 1 and c1 is self.ctx:  # one process: the back-projection result is the graph input
             self.ctx.backproject(None, None, None, None, params, shape=(n, H, W),
                                  device_ptrs=(depth.data_ptr(), seg.data_ptr(), intrinsics.data_ptr(),
                                               poses.data_ptr()))
@@ -315,15 +339,16 @@ class FrameShardedScene:
             self.ctx.use_backprojection()
             return col, lab, off
         if n:
-            self.ctx.backproject(None, None, None, None, params, shape=(n, H, W),
-                                 device_ptrs=(depth.data_ptr(), seg.data_ptr(), intrinsics.data_ptr(),
-                                              poses.data_ptr()))
-            col, lab, off = self.ctx.bp_mask_index()
+            c1.backproject(None, None, None, None, params, shape=(n, H, W),
+                           device_ptrs=(depth.data_ptr(), seg.data_ptr(), intrinsics.data_ptr(), poses.data_ptr()))
+            col, lab, off = c1.bp_mask_index()
             local = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=depth.device)
-            # the copy of the point ids runs on the context's stream while the metadata block is
+            # the copy of the point ids runs on the S1 context's stream while the metadata block is
             # exchanged; torch's stream (the collectives') is ordered behind it without a host wait
-            self.ctx.bp_points_to_device(local.data_ptr())
-            ready = lambda: self._order_streams(torch_after_ctx=True, device=depth.device)
+            # (and the copy behind torch's stream: `local` may reuse a block torch's stream still reads)
+            _stream_wait(int(c1.stream() or 0), torch.cuda.current_stream(depth.device), depth.device)
+            c1.bp_points_to_device(local.data_ptr())
+            ready = lambda: self._order_streams(torch_after_ctx=True, device=depth.device, ctx=c1)  # noqa: E731
         else:  # more ranks than frames
             col, lab, off = np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64)
             local = torch.zeros(1, dtype=torch.int32, device=depth.device)
@@ -336,15 +361,17 @@ class FrameShardedScene:
         self.run.set_masks(self.P, self.F, g_col, g_lab, g_off, pts_device_ptr=self.pts.data_ptr())
         return g_col, g_lab, g_off
 
-    def _order_streams(self, torch_after_ctx: bool, device):
-        """Device-side ordering between the context's stream and torch's current stream (an event
-        recorded on one, waited on by the other); nothing when they are the same stream."""
+    def _order_streams(self, torch_after_ctx: bool, device, ctx=None):
+        """Device-side ordering between a context's stream (default: the graph context's) and
+        torch's current stream (an event recorded on one, waited on by the other); nothing when they
+        are the same stream."""
+        c = self.ctx if ctx is None else ctx
         cur = torch.cuda.current_stream(device)
-        s = int(self.ctx.stream() or 0)
+        s = int(c.stream() or 0)
         if s == int(cur.cuda_stream):
             return
         if s == 0:  # the context runs on the null stream: a host-side join is the safe order
-            (self.ctx.synchronize if torch_after_ctx else cur.synchronize)()
+            (c.synchronize if torch_after_ctx else cur.synchronize)()
             return
         ext = torch.cuda.ExternalStream(s, device=device)
         (cur.wait_stream(ext) if torch_after_ctx else ext.wait_stream(cur))
@@ -380,7 +407,8 @@ class ScenePipeline:
     """
 
     def __init__(self, sh: FrameShardedScene, s1_ctx, depth: torch.Tensor, seg: torch.Tensor,
-                 intrinsics: torch.Tensor, poses: torch.Tensor, params=None, scene_owner: bool = False):
+                 intrinsics: torch.Tensor, poses: torch.Tensor, params=None, scene_owner: bool = False,
+                 scene_points: torch.Tensor | None = None):
         n = sh.hi - sh.lo
         if depth.shape[0] != n:
             raise ValueError(f"rank {sh.rank} owns {n} frames [{sh.lo}, {sh.hi})")
@@ -393,8 +421,14 @@ class ScenePipeline:
         self.s1 = self.s1s[0]
         self.frames = (depth, seg, intrinsics, poses)
         self.params = params
+        # scene_points (float32 [P,3] on the device, optional): handed to the S1 context before every
+        # scene's back-projection, as each new scene's points are (mc_scene_set_points), so each scene
+        # rebuilds its ball-query grid inside its own S1 (graph/construction.py:37, per scene)
+        self.scene_points = scene_points
         self.scene_owner = bool(scene_owner) and sh.world > 1
         self.owned: list[int] = []
+        self.gather_s = 0.0   # host wall time in gather_masks (both collectives) over the scenes run
+        self.gathers = 0
 
     def warm(self):
         """One S1 call on every context but the first (a context's first call sizes its batches for
@@ -410,6 +444,8 @@ class ScenePipeline:
         if n == 0:
             return (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(1, np.int64),
                     torch.zeros(1, dtype=torch.int32, device=depth.device))
+        if self.scene_points is not None:
+            s1.set_points(device_ptr=self.scene_points.data_ptr(), num_points=len(self.scene_points))
         s1.backproject(None, None, None, None, self.params, shape=(n, H, W),
                        device_ptrs=(depth.data_ptr(), seg.data_ptr(), K.data_ptr(), T.data_ptr()))
         col, lab, off = s1.bp_mask_index()
@@ -468,12 +504,18 @@ class ScenePipeline:
                 if sh.world == 1:
                     g_col, g_lab, g_off, g_pts = col, lab, off, pts
                 elif self.scene_owner:
+                    tg = time.perf_counter()
                     g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks,
                                                               dst=owner)
+                    self.gather_s += time.perf_counter() - tg
+                    self.gathers += 1
                     if sh.rank != owner:
                         continue
                 else:
+                    tg = time.perf_counter()
                     g_col, g_lab, g_off, g_pts = gather_masks(col, lab, off, pts, sh.lo, sh.group, sh.max_masks)
+                    self.gather_s += time.perf_counter() - tg
+                    self.gathers += 1
                 sh.mask_index = (g_col, g_lab, g_off)
                 sh.pts = g_pts
                 # the graph context's stream reads the gathered ids (written on torch's stream) next

@@ -7,8 +7,11 @@ Without N GPUs this script runs what one rank's device does: S1 of the rank's co
 in a producer thread on its own context, and the graph stages over the WHOLE scene's masks (made
 once up front, handed to the graph context as the gather would) in the calling thread, scene after
 scene.  The graph stages run unsharded here (the bench shards S3 / S4 / S6 level 0 N ways): an
-upper bound on the rank's graph work.  Not included: the all-gather of the mask CSRs (issued by the
-consumer thread, under the producer's S1).  Prints one JSON line per N.
+upper bound on the rank's graph work.  The gather of the mask CSRs (issued by the consumer thread,
+under the producer's S1) is modelled in the consumer thread, per scene, before the graph stages: a device copy of the rank's share of the point ids (the bytes it sends; the owner
+receives N - 1 such shares, one per peer link, in parallel) plus a host wait of those bytes over one
+xGMI link at XGMI_LINK_GBS (64 GB/s, a conservative one-direction rate of a 153 GB/s link).  Prints
+one JSON line per N.
 
     python scripts/rank_proxy.py [shape] [scenes] [N ...]
 """
@@ -28,12 +31,14 @@ from maskclustering_amd.frame_shard import FrameShardedScene, balanced_frame_sli
 from maskclustering_amd.pipeline import GraphRun  # noqa: E402
 from maskclustering_amd.synthetic_frames import make_frames_shape  # noqa: E402
 
-CFG = dict(mask_visible_threshold=0.3, undersegment_filter_threshold=0.3, view_consensus_threshold=0.9,
-           contained_threshold=0.8)
+from maskclustering_amd.dataset_configs import shape_thresholds  # noqa: E402
+
+XGMI_LINK_GBS = float(os.environ.get("MC_PROXY_LINK_GBS", "64"))
 
 
 def main():
     shape = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    CFG = shape_thresholds(shape)[1]
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     Ns = [1] + [n for n in ([int(x) for x in sys.argv[3:]] or [8]) if n != 1]
     dev = torch.device("cuda", 0)
@@ -61,6 +66,7 @@ def main():
         s1b.set_memory_budget(int(free * 0.3))
 
     def s1_masks(lo, hi, s1=s1):
+        s1.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)  # per scene, as the bench
         s1.backproject(None, None, None, None, prm, shape=(hi - lo, fr.depth.shape[1], fr.depth.shape[2]),
                        device_ptrs=(fr.depth[lo:hi].data_ptr(), fr.seg[lo:hi].data_ptr(), K_t[lo:hi].data_ptr(),
                                     T_t[lo:hi].data_ptr()))
@@ -71,6 +77,20 @@ def main():
         return col, lab, off, pts
 
     full = s1_masks(0, F)  # the gathered masks every rank's graph stages read
+    nnz_all = int(full[2][-1])
+    scratch = torch.empty(max(nnz_all, 1), dtype=torch.int32, device=dev)
+
+    def gather_model(N):
+        """the rank's share of one scene's point-id gather: its slice's ids copied on the device, and
+        the host wait of those bytes over one link (the owner's N - 1 incoming shares arrive in parallel)"""
+        if N == 1:
+            return 0.0
+        share = max(1, nnz_all // N)
+        t = time.perf_counter()
+        scratch[:share].copy_(full[3][:share])
+        torch.cuda.current_stream().synchronize()
+        time.sleep(4.0 * share / (XGMI_LINK_GBS * 1e9))
+        return time.perf_counter() - t
 
     def graph():
         col, lab, off, pts = full
@@ -109,6 +129,7 @@ def main():
             th.start()
             for k in range(n):
                 q.get()
+                gather_model(N)
                 if k % every == 0:  # scene-owner mode: this rank's scenes only
                     graph()
             th.join()
@@ -140,6 +161,7 @@ def main():
                 th.start()
             for k in range(n):
                 qs[k % 2].get()
+                gather_model(N)
                 if k % every == 0:
                     graph()
             for th in ths:
@@ -164,11 +186,14 @@ def main():
             "rank_pipelined_scene_owner_ms": round(own_ms, 3), "scene_owner_scenes": Ko,
             "projected_speedup_scene_owner": round(base_pipe / own_ms, 2),
             "rank_two_producers_scene_owner_ms": own2_ms and round(own2_ms, 3),
+            "gather_model_ms": round(1e3 * gather_model(N), 3), "point_ids_per_scene": nnz_all,
+            "xgmi_link_gbs": XGMI_LINK_GBS,
             "projected_speedup_two_producers": own2_ms and round(base_pipe / own2_ms, 2),
             "note": "rank_pipelined_ms: S1 of the slowest slice beside the unsharded graph stages of the previous "
-                    "scene; projected_speedup: the N = 1 line's rank_pipelined_ms over this one; the mask all-gather "
-                    "is not included (issued under the next S1 by the consumer thread); scene_owner: the graph "
-                    "stages of every N-th scene only (the point ids gathered to that rank, not included either)"}),
+                    "scene; projected_speedup: the N = 1 line's rank_pipelined_ms over this one; every scene's share "
+                    "of the point-id gather is modelled in the consumer thread (gather_model_ms: a device copy of "
+                    "the rank's share + its bytes over one xGMI link); scene_owner: the graph stages of every N-th "
+                    "scene only"}),
               flush=True)
 
 

@@ -285,3 +285,14 @@ def test_scene_owner_pipeline_equals_single_process(tmp_path, world, shape, seed
             for name in want:
                 np.testing.assert_array_equal(got[f"{k}/{name}"], np.asarray(want[name]), err_msg=f"scene {k} {name}")
     assert sorted(seen) == list(range(nsc))
+
+
+def test_sweep_scene_assignment_covers_each_scene_once():
+    """run.py:33-50's split of the scene list over one process per GPU: scene i on rank i mod N."""
+    from maskclustering_amd.sweep import scenes_of
+    for world in (1, 2, 3, 8):
+        got = sorted(i for r in range(world) for i in scenes_of(r, world, 312))
+        assert got == list(range(312))
+        assert all(i % world == r for r in range(world) for i in scenes_of(r, world, 312))
+    with pytest.raises(ValueError):
+        scenes_of(2, 2, 10)
