@@ -2143,7 +2143,10 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         ctx->bp_stats.clear();
         ctx->bp_nnz = 0;
         const float rf = static_cast<float>(prm.ball_radius);
-        if (ctx->grid_radius != rf) bp_build_grid(ctx, rf, s);
+        if (ctx->grid_radius != rf) {  // a new scene (mc_scene_set_points) or radius: the 2r scene grid
+            TimedScope ts(ctx->timer, s, "bp_grid");
+            bp_build_grid(ctx, rf, s);
+        }
 
         const float *dep = depth;
         const uint8_t *sg = seg;

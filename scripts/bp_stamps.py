@@ -53,13 +53,11 @@ print("k-NN points deferred to the ring search", int(buf[30]), "(list overflow",
       int(buf[33]), ")", "near-tied keys redone exactly", int(buf[31]))
 print("knn points", int(buf[13]), "candidates/point", round(float(buf[29]) / max(int(buf[13]), 1), 1),
       "fallbacks", int(buf[31]))
-vt = [float(buf[k]) for k in (39, 36, 38, 40, 37, 41)]
+vt = [float(buf[k]) for k in (36, 38, 40, 37, 39)]
 vtot = max(sum(vt), 1.0)
-print("k_bp_voxel_runs workgroup-busy shares:", {n: f"{100 * v / vtot:.1f} %" for n, v in
-      zip(("slot set-up", "0 min bound", "1 runs", "2-3 ids + run buckets", "4 thread sums", "4 wave sums"), vt)},
+print("k_bp_voxel_lds workgroup-busy shares:", {n: f"{100 * v / vtot:.1f} %" for n, v in
+      zip(("0 min bound", "1a points+keys+probes", "1b masks+ids+sums", "1 exit", "2 means + slot set-up"), vt)},
       "total ms", round(vtot / 1e5, 2))
-print("voxel first tier: slots handed on", int(buf[42]), "with", int(buf[43]), "pixels; runs", int(buf[45]),
-      "; wave-summed voxels", int(buf[44]), "; second tier (k_bp_voxel_lds) workgroup-busy ms", round(float(buf[46]) / 1e5, 2))
 st = ctx.bp_candidates()
 for c, n in ((2, "npix"), (3, "nvox"), (4, "ndbscan"), (5, "nsor")):
     v = st[:, c]
