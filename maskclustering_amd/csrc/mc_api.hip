@@ -2260,6 +2260,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         mc::BpDev dv;
         dv.trunc = prm.depth_trunc;
         dv.vs = prm.voxel_size;
+        dv.rvs = 1.0 / prm.voxel_size;  // (IEEE division on the host: RN(1 / vs), div_rn's reciprocal)
         dv.eps2 = prm.dbscan_eps * prm.dbscan_eps;
         // k-NN pre-selection radii (fractions of eps, ascending, < 1): any choice gives the same
         // results (the smallest radius holding >= k kept points is used); MC_KNN_RADII="a,b,c" tunes

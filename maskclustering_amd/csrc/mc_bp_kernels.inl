@@ -33,6 +33,7 @@ constexpr int kCellBias = 1 << 20; // scene-grid cell coordinates in [-2^20, 2^2
 
 struct BpDev {
     double trunc, vs, eps2, ce, frac, std_ratio, cov;
+    double rvs;        // RN(1 / vs): the voxel index by div_rn
     double knn_r2[3];  // k-NN pre-selection radii^2 (0.6, 0.75, 0.9 eps)
     float r2, scene_inv;
     int minpts, knn, kball, few;
@@ -89,17 +90,36 @@ __device__ __forceinline__ int scene_cell(float v, float inv)
     return min(max(static_cast<int>(floorf(v * inv)), -kCellBias), kCellBias - 1) + kCellBias;
 }
 
+// a / b rounded to nearest, from rb = RN(1 / b) computed once per divisor (Markstein: q0 = RN(a rb),
+// r = a - b q0 is exact by FMA, and RN(q0 + r rb) is the correctly rounded quotient for normal operands
+// whose quotient neither overflows nor underflows): a multiply and two FMAs instead of the
+// division sequence (v_rcp_f64, scale, five FMAs, fixup), the same bits as a / b
+// (tests/test_div_rn_cpu.py checks the identity on operands of the ranges here).  S1's per-pixel
+// divisions are these: the unprojection by fx and fy, and the voxel index by the voxel size.
+__device__ __forceinline__ double div_rn(double a, double b, double rb)
+{
+    const double q0 = a * rb;
+    const double r = fma(-b, q0, a);
+    return fma(r, rb, q0);
+}
+
 // (a1, u1): Open3D create_from_depth_image + transform, in double, no FMA
-// floor(a / b) of the cell and voxel indices, the division rounded as Open3D's (a reciprocal multiply
-// with an exact fallback near integers measured no faster: the indices are not what the kernels wait on)
+// floor(a / b) of the cell indices (the denoise's grid; per voxel, not per pixel)
 __device__ __forceinline__ double floor_div(double a, double b) { return floor(a / b); }
 
+// the per-frame reciprocals of bp_world's divisors: rk[0] = RN(1 / fx), rk[1] = RN(1 / fy)
+__device__ __forceinline__ void bp_recip(const double *__restrict__ K, double rk[2])
+{
+    rk[0] = 1.0 / K[0];
+    rk[1] = 1.0 / K[1];
+}
+
 __device__ __forceinline__ void bp_world(const double *__restrict__ K, const double *__restrict__ T, int u, int v,
-                                         float d, double &ox, double &oy, double &oz)
+                                         float d, double &ox, double &oy, double &oz, const double *rk)
 {
     const double z = static_cast<double>(d);
-    const double x = ((static_cast<double>(u) - K[2]) * z) / K[0];
-    const double y = ((static_cast<double>(v) - K[3]) * z) / K[1];
+    const double x = div_rn((static_cast<double>(u) - K[2]) * z, K[0], rk[0]);
+    const double y = div_rn((static_cast<double>(v) - K[3]) * z, K[1], rk[1]);
     double r[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) r[k] = (((T[4 * k] * x) + (T[4 * k + 1] * y)) + (T[4 * k + 2] * z)) + T[4 * k + 3];
@@ -631,6 +651,8 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
         const double *Tp = pose + 16 * static_cast<size_t>(f);
         const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
         const unsigned *pl = pix_list + base;
+        double rk[2];
+        bp_recip(K, rk);
         for (int i = t; i < H; i += T) {
             hkey[i] = kVxEmpty;
             hval[i] = ~0u;
@@ -651,7 +673,7 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
             for (int u = 0; u < 4; u++) {
                 if (k0 + u * T < n) {
                     double p[3];
-                    bp_world(K, Tp, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2]);
+                    bp_world(K, Tp, static_cast<int>(iv[u] % W), static_cast<int>(iv[u] / W), dv[u], p[0], p[1], p[2], rk);
 #pragma unroll
                     for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
                 }
@@ -676,12 +698,12 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
             unsigned key = kVxEmpty;
             if (valid) {
                 double p[3];
-                bp_world(K, Tp, static_cast<int>(iv % W), static_cast<int>(iv / W), d, p[0], p[1], p[2]);
+                bp_world(K, Tp, static_cast<int>(iv % W), static_cast<int>(iv / W), d, p[0], p[1], p[2], rk);
                 unsigned kk = 0;
                 bool fits = true;
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    const double r = floor_div(p[c] - vmin[c], pr.vs);
+                    const double r = floor(div_rn(p[c] - vmin[c], pr.vs, pr.rvs));
                     fits = fits && r >= 0.0 && r < 1024.0;
                     kk = (kk << 10) | (fits ? static_cast<unsigned>(r) : 0u);
                 }
@@ -846,12 +868,14 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
         const double *T = pose + 16 * static_cast<size_t>(f);
         const float *dep = depth + static_cast<size_t>(f) * pr.H * W;
         const unsigned *pl = pix_list + base;
+        double rk[2];
+        bp_recip(K, rk);
         // min bound (order-free)
         double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
         for (int k = t; k < n; k += 256) {
             const unsigned i = pl[k];
             double p[3];
-            bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+            bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2], rk);
 #pragma unroll
             for (int c = 0; c < 3; c++) mn[c] = fmin(mn[c], p[c]);
         }
@@ -872,11 +896,11 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
             unsigned e = 0;
             if (valid) {
                 const unsigned i = pl[k];
-                bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2]);
+                bp_world(K, T, static_cast<int>(i % W), static_cast<int>(i / W), dep[i], p[0], p[1], p[2], rk);
                 long long ix[3];
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    ix[c] = static_cast<long long>(floor((p[c] - vmin[c]) / pr.vs));
+                    ix[c] = static_cast<long long>(floor(div_rn(p[c] - vmin[c], pr.vs, pr.rvs)));
                     if (ix[c] < 0 || ix[c] >= (1ll << 21)) {
                         atomicOr(errflag, 1);
                         ix[c] = ix[c] < 0 ? 0 : (1ll << 21) - 1;

@@ -2,7 +2,7 @@
 one batch holding every frame.
 
     MC_BP_BATCH_PIXELS=80000000 MCGRAPH_LIB=maskclustering_amd/libmcgraph_stamps.so \\
-        python scripts/bp_slot_times.py [shape]
+        python scripts/bp_slot_times.py [shape] [first frame] [frames]
 """
 import ctypes
 import os
@@ -15,7 +15,9 @@ from maskclustering_amd import _native  # noqa: E402
 from maskclustering_amd.synthetic_frames import make_frames_shape  # noqa: E402
 
 shape = sys.argv[1] if len(sys.argv) > 1 else "c2"
-fr = make_frames_shape(shape, seed=0, device="cuda")
+f0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+nf = int(sys.argv[3]) if len(sys.argv) > 3 else None
+fr = make_frames_shape(shape, seed=0, device="cuda", **({"frames": range(f0, f0 + nf)} if nf else {}))
 ctx = _native.Context(0)
 L = _native.load()
 L.mc_debug_bp_slot_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -36,7 +38,7 @@ order = np.argsort(-us)
 print("slowest slots: us nvox ndbscan nsor")
 for i in order[:15]:
     print(f"  {us[i]:9.1f} {nv[i]:6d} {nd[i]:6d} {nsor[i]:6d}")
-for lo, hi in ((0, 512), (512, 1024), (1024, 2048), (2048, 3072)):
+for lo, hi in ((0, 512), (512, 1024), (1024, 2048), (2048, 3072), (3072, 4096), (4096, 16384)):
     sel = (nv > lo) & (nv <= hi)
     if sel.any():
         print(f"class ({lo},{hi}]: n {int(sel.sum())} mean {us[sel].mean():8.1f} us  p50 {np.median(us[sel]):8.1f}"
