@@ -31,6 +31,7 @@ GROUPS = {
                       ["mc::k6_components", "mc::k6_compress"]),
     "s6_merge": (["mc::k6_merge"], ["mc::k6_merge"]),
     "s7_points": (["mc::k7"], ["mc::k7_words", "mc::k7_count"]),
+    "bp_grid": (["mc::k_grid_count", "mc::k_grid_scatter"], ["mc::k_grid_count"]),
     "bp_pixels": (["mc::k_bp_count", "mc::k_bp_frames", "mc::k_bp_slots", "mc::k_bp_compact"], ["mc::k_bp_count"]),
     "bp_voxel": (["mc::k_bp_voxel", "mc::k_bp_vox_order"], ["mc::k_bp_voxel_lds<256"]),
     "bp_denoise": (["mc::k_bp_denoise", "mc::k_bp_classify", "mc::k_bp_knn_ring", "mc::k_bp_vox_order"],
