@@ -137,10 +137,10 @@ def roofline_entry(w, avg_s, pmc_group=None):
     return e
 
 
-# the SQ counter passes of the benched build (scripts/gpu_r4final.sh); the round-3 file only as a fallback
-SQ_DENOISE = next((p for p in (os.path.join(REPO, "profiles", "r05", "denoise_sq_counters_c3.json"),
-                               os.path.join(REPO, "profiles", "r04", "denoise_sq_counters_c3.json"))
-                   if os.path.exists(p)), os.path.join(REPO, "profiles", "r05", "denoise_sq_counters_c3.json"))
+# the SQ counter passes of the benched build (scripts/gpu_final.sh PART=profiles); round 5's as a fallback
+SQ_DENOISE = next((p for p in (os.path.join(REPO, "profiles", "r06", "final", "denoise_sq_counters_c3.json"),
+                               os.path.join(REPO, "profiles", "r05", "denoise_sq_counters_c3.json"))
+                   if os.path.exists(p)), os.path.join(REPO, "profiles", "r06", "final", "denoise_sq_counters_c3.json"))
 SQ_DENOISE_FRAMES = 100     # the counter pass: C3 frames 600-699 (scripts/pmc_kernel.py over scripts/bp_profile.py)
 CLOCK_GHZ = 2.4             # MI355X engine clock (MI355X_MICROARCH.md)
 

@@ -60,7 +60,7 @@ def main():
     sh = FrameShardedScene(run, fr.num_points, F)
 
     s1b = None  # a second S1 context (two producers: one scene's kernel tails filled by the next's)
-    if os.environ.get("MC_PROXY_TWO_PRODUCERS", "1") != "0":
+    if os.environ.get("MC_PROXY_TWO_PRODUCERS", "0") != "0":  # (the bench's default is one producer)
         s1b = _native.Context(0)
         s1b.set_points(device_ptr=t_scene.data_ptr(), num_points=fr.num_points)
         s1b.set_memory_budget(int(free * 0.3))
@@ -113,6 +113,7 @@ def main():
     base_pipe = None
     costs = frame_costs(fr.depth, fr.seg, K_t).cpu().numpy()
     for N in Ns:
+        print(f"N = {N}", file=sys.stderr, flush=True)
         slices = balanced_frame_slices(costs, N)
         s1_ms = [timed(lambda: s1_masks(lo, hi), max(2, K // 2)) for lo, hi in slices]
         r = int(np.argmax(s1_ms))
@@ -122,13 +123,17 @@ def main():
             q: queue.Queue = queue.Queue(maxsize=1)
 
             def produce():
-                for _ in range(n):
-                    q.put(s1_masks(lo, hi))
+                try:
+                    for _ in range(n):
+                        q.put(s1_masks(lo, hi))
+                except BaseException as e:  # handed to the consumer, which raises it
+                    q.put(e)
 
             th = threading.Thread(target=produce, daemon=True)
             th.start()
             for k in range(n):
-                q.get()
+                if isinstance(q.get(), BaseException):
+                    raise RuntimeError("S1 producer failed")
                 gather_model(N)
                 if k % every == 0:  # scene-owner mode: this rank's scenes only
                     graph()
