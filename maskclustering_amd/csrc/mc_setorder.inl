@@ -30,6 +30,7 @@
 #include <mutex>
 #include <system_error>
 #include <thread>
+#include <pthread.h>
 #include <vector>
 
 #include <unistd.h>
@@ -347,28 +348,43 @@ class SharedPool {
     std::unique_ptr<Pool> pool_;
     int n_ = 0;
 };
-// One per process: a forked child inherits the parent's pool object (its n_ matching, its mutex
-// possibly held by a parent thread) but none of its worker threads, so a child that finds the
-// creating process's pid replaces it with a fresh pool and leaks the inherited one (joining threads
-// that do not exist, or waiting on a mutex no thread will release, would hang).
+// One per process.  A forked child inherits the parent's pool object (its n_ matching, its mutexes
+// possibly held by parent threads) but none of its worker threads, so the child must start from a new
+// pool: a pthread_atfork child handler (registered once, on first use) drops the inherited pool
+// (leaked: joining threads that do not exist, or waiting on a mutex no thread will release, would
+// hang) and re-initialises the creation mutex while the child still has only the forking thread.  The
+// pid check stays as a second guard.
+struct SharedPoolSlot {
+    std::atomic<SharedPool *> p{nullptr};
+    std::atomic<pid_t> owner{0};
+    std::mutex mk;
+};
+inline SharedPoolSlot &shared_pool_slot()
+{
+    static SharedPoolSlot slot;
+    return slot;
+}
+inline void shared_pool_atfork_child()
+{
+    SharedPoolSlot &sl = shared_pool_slot();
+    sl.p.store(nullptr, std::memory_order_relaxed);
+    sl.owner.store(0, std::memory_order_relaxed);
+    new (&sl.mk) std::mutex;  // (one thread in the child: the inherited state may be locked)
+}
 inline SharedPool &shared_pool()
 {
-    static std::atomic<SharedPool *> p{nullptr};
-    static std::atomic<pid_t> owner{0};
-    static std::mutex mk;
+    static const bool registered = (pthread_atfork(nullptr, nullptr, shared_pool_atfork_child), true);
+    (void)registered;
+    SharedPoolSlot &sl = shared_pool_slot();
     const pid_t me = getpid();
-    SharedPool *cur = p.load(std::memory_order_acquire);
-    if (cur && owner.load(std::memory_order_acquire) == me) return *cur;
-    // first use, or the first use in a forked child: only the forking thread runs in the child, so
-    // the inherited creation mutex may be held; a new one is taken instead of it
-    static std::mutex *mkp = &mk;
-    if (cur && owner.load() != me) mkp = new std::mutex;  // (leaked: the child's first use only)
-    std::lock_guard<std::mutex> g(*mkp);
-    cur = p.load(std::memory_order_acquire);
-    if (!cur || owner.load() != me) {
+    SharedPool *cur = sl.p.load(std::memory_order_acquire);
+    if (cur && sl.owner.load(std::memory_order_acquire) == me) return *cur;
+    std::lock_guard<std::mutex> g(sl.mk);
+    cur = sl.p.load(std::memory_order_acquire);
+    if (!cur || sl.owner.load(std::memory_order_acquire) != me) {
         cur = new SharedPool;  // never destroyed: idle workers end with the process
-        owner.store(me, std::memory_order_release);
-        p.store(cur, std::memory_order_release);
+        sl.owner.store(me, std::memory_order_release);
+        sl.p.store(cur, std::memory_order_release);
     }
     return *cur;
 }
