@@ -5,7 +5,7 @@ import warnings
 
 # S1's denoise runs its size classes side by side on their own HIP streams; HIP maps streams onto
 # GPU_MAX_HW_QUEUES hardware queues (default 4), and two classes that share a queue run one after
-# the other (C3 E2E 224 ms with 8 queues against 415 ms with 4).  Ask for 8 unless
+# the other (docs/experiments.md: C3 E2E 224 ms with 8 queues against 415 ms with 4).  Ask for 8 unless
 # more are set.  HIP reads the variable once, when the process first initialises the runtime, so
 # the setting does nothing if that already happened: warn then (torch.cuda initialised before this
 # import is the case that can be seen from here).

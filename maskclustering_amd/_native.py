@@ -362,7 +362,7 @@ class Context:
 
     def debug_counters(self, reset: bool = False):
         """(checks compiled in, failures per check kind): the in-kernel invariant checks of a
-        -DMC_DBG_CHECK=1 build; a normal build reports (False, zeros)."""
+        -DMC_DBG_CHECK=1 build (docs/experiments.md); a normal build reports (False, zeros)."""
         out = np.zeros(9, np.int64)
         self._check(self.L.mc_debug_counters(self.h, _ptr(out), 9, 1 if reset else 0))
         return bool(out[0]), out[1:]

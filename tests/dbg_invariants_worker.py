@@ -4,7 +4,7 @@ library is chosen per process by MCGRAPH_LIB).
     MCGRAPH_LIB=maskclustering_amd/libmcgraph_dbg.so python tests/dbg_invariants_worker.py
 
 With the -DMC_DBG_CHECK=1 build (built in-tree by __graft_entry__.build(), held to the spill-placement
-gate like every build, DESIGN.md §4): every size class (MC_BP_MIN_CLASS 0..5), lists full and capped
+gate like every build, DESIGN.md §9 round 5): every size class (MC_BP_MIN_CLASS 0..5), lists full and capped
 (MC_BP_NBCAP 64 / 8), on the dense S1 inputs.  In-kernel checks recompute every list, union and k-NN
 mean directly; their failure counters must stay zero, and the masks must equal the release build's
 (passed in as an npz by the test).  Prints one line per case; exit 1 on any failure."""

@@ -1,7 +1,7 @@
 """The S1 CPU restatement (oracle/s1_oracle.c) against fixtures made by running
 the reference's own utils/mask_backprojection.py (tests/golden/make_s1_golden.py),
 plus independent cross-checks of the restated library steps.  Parity of the
-Open3D / pytorch3d arithmetic itself is unpinned (DESIGN.md §5)."""
+Open3D / pytorch3d arithmetic itself is unpinned (DESIGN.md §2.2)."""
 import os
 
 import numpy as np

@@ -1,5 +1,5 @@
 """The gfx950 code of the S1 kernels (release and the MC_DBG_CHECK diagnostics build) holds no VGPR
-spill store placed where EXEC can be partial (scripts/spill_exec_check.py; DESIGN.md §4: the round-4
+spill store placed where EXEC can be partial (scripts/spill_exec_check.py; docs/experiments.md: the round-4
 diagnostics build lost the inactive lanes' values of such spills).  Cross-compiles on the CPU."""
 import os
 import subprocess
