@@ -1901,7 +1901,6 @@ void bp_build_grid(mc_ctx *ctx, float radius, hipStream_t s)
     ctx->grid_radius = radius;
 }
 
-constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 
 // one LDS size class of the denoise: as many workgroups as are resident at once, each taking the
 // class's slots from a ticket counter
@@ -1911,11 +1910,16 @@ constexpr int kBpGrid = 1024;  // persistent workgroups of the per-slot kernels
 // profiles/r04/r4e_tail_ab.jsonl)
 void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int ncap, int *st, const mc::BpDev &dv)
 {
-    hipLaunchKernelGGL(mc::k_bp_knn_ring, dim3(ctx->num_cu * 8), dim3(256), 0, s, st + BS_DQ,
-                       ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_slot_m.as<int>(), dv,
-                       ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
-                       ctx->d_slot_grid.as<double>(), ctx->d_avg.as<double>(), st + BS_DNERR);
-    hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * 4), dim3(256), 0, s,
+    auto ring = [&](auto kern, int wg_per_cu) {
+        hipLaunchKernelGGL(kern, dim3(ctx->num_cu * wg_per_cu), dim3(256), 0, s, st + BS_DQ,
+                           ctx->d_vx_pvid.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_slot_m.as<int>(), dv,
+                           ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
+                           ctx->d_slot_grid.as<double>(), ctx->d_avg.as<double>(), st + BS_DNERR);
+    };
+    ring(mc::k_bp_knn_ring<1>, 8);  // (at five or six waves per SIMD, spilling: no faster)
+    // a wave per slot whose ordered sums wait on latency: as many waves as its 45 VGPRs allow
+    const int tail_wg = getenv("MC_BP_TAILWG") ? atoi(getenv("MC_BP_TAILWG")) : 8;
+    hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * tail_wg), dim3(256), 0, s,
                        st + BS_CLS, ctx->d_cls_list.as<int>(), ncap, 0, mc::kBpClasses, ctx->d_slot_pix.as<int>(),
                        ctx->d_slot_m.as<int>(), dv, ctx->d_vpts.as<double>(), ctx->d_avg.as<double>(),
                        ctx->d_ssidx.as<int>(), ctx->d_qpts.as<float>(), ctx->d_slot_ns.as<int>(),
@@ -2249,10 +2253,11 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
         bp_reserve(ctx, FB, H, W, nbands, mask_cap(mfrac), s);
         double mfrac_seen = 0.0;
         const int PW = static_cast<int>((ctx->P_scene + 63) / 64) + 1;
-        if (ctx->d_bpbm.bytes < static_cast<size_t>(kBpGrid) * PW * 8) {
-            ctx->d_bpbm.reserve(static_cast<size_t>(kBpGrid) * PW * 8);
+        const int qgrid = ctx->num_cu * 6;  // one bitmap per query workgroup (its largest grid)
+        if (ctx->d_bpbm.bytes < static_cast<size_t>(qgrid) * PW * 8) {
+            ctx->d_bpbm.reserve(static_cast<size_t>(qgrid) * PW * 8);
             MC_HIP(hipMemsetAsync(ctx->d_bpbm.ptr, 0, ctx->d_bpbm.bytes, s));  // kept zero by k_bp_query
-            ctx->bp_bm_blocks = kBpGrid;
+            ctx->bp_bm_blocks = qgrid;
         }
         size_t tmp_cap = std::max<size_t>(ctx->d_tmp.bytes / 4, std::max<size_t>(1 << 20, ctx->bp_px_cap));
         ctx->d_tmp.reserve(tmp_cap * 4);
@@ -2365,16 +2370,23 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                 hipLaunchKernelGGL(mc::k_bp_vox_order, dim3(1), dim3(1024), 0, s, st + BS_NS, ctx->d_slot_np.as<int>(),
                                    ctx->d_vox_order.as<int>());
                 int *fb1 = ctx->d_vx_fb.as<int>(), *fb2 = fb1 + slots_cap(FB);
-                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxT, mc::kVxH, mc::kVxV>), dim3(ctx->num_cu * 4), dim3(mc::kVxT), 0, s,
-                                   st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
-                                   ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
-                                   KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(),
-                                   ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
-                hipLaunchKernelGGL((mc::k_bp_voxel_lds<mc::kVxT2, mc::kVxH2, mc::kVxV2>), dim3(ctx->num_cu), dim3(mc::kVxT2), 0, s,
-                                   st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
-                                   ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
-                                   ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2,
-                                   st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                auto tier1 = [&](auto kern, int wg_per_cu) {
+                    hipLaunchKernelGGL(kern, dim3(ctx->num_cu * wg_per_cu), dim3(mc::kVxT), 0, s,
+                                       st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
+                                       ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
+                                       KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(),
+                                       ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
+                };
+                auto tier2 = [&](auto kern) {
+                    hipLaunchKernelGGL(kern, dim3(ctx->num_cu), dim3(mc::kVxT2), 0, s,
+                                       st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
+                                       ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
+                                       ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2,
+                                       st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                };
+                // five workgroups per CU (32 KB of LDS, <= 96 VGPRs each) for the first tier
+                tier1(mc::k_bp_voxel_lds<mc::kVxT, mc::kVxH, mc::kVxV, 0, mc::kVxWpe>, mc::kVxWpe);
+                tier2(mc::k_bp_voxel_lds<mc::kVxT2, mc::kVxH2, mc::kVxV2, mc::kVxL2>);
                 hipLaunchKernelGGL(mc::k_bp_voxel, dim3(ctx->num_cu), dim3(256), 0, s, st + BS_VXFB2,
                                    fb2, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
@@ -2423,7 +2435,8 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
             }
             {
                 TimedScope ts(ctx->timer, s, "bp_query");
-                hipLaunchKernelGGL(mc::k_bp_query, dim3(kBpGrid), dim3(256), 0, s, st + BS_NS,
+                auto query = [&](auto kern, int grid) {
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, st + BS_NS,
                                    ctx->d_slot_pix.as<int>(), ctx->d_slot_ns.as<int>(), ctx->d_slot_box.as<float>(),
                                    ctx->d_qpts.as<float>(), dv, ctx->d_gpts.as<float4>(), ctx->d_gidx.as<int>(),
                                    ctx->d_gcell.as<unsigned long long>(), ctx->d_gstart.as<int>(), ctx->gnb,
@@ -2431,6 +2444,12 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    static_cast<int>(std::min<size_t>(tmp_cap, INT_MAX)), st + BS_TOP,
                                    ctx->d_slot_nn.as<int>(), ctx->d_slot_toff.as<int>(), ctx->d_slot_cov.as<int>(),
                                    st + BS_OVF, ctx->d_vox_order.as<int>());
+                };
+                // the query waits on dependent cell-range and point loads: as many waves as the
+                // registers allow (the 20-entry best list of ball_k <= 20: 76 VGPRs, six workgroups per
+                // CU, C3 query 8.4 -> 6.5 ms per scene; 32 entries: 89 VGPRs, five)
+                if (prm.ball_k <= 20) query(mc::k_bp_query<1, 20>, ctx->num_cu * 6);
+                else query(mc::k_bp_query<1, mc::kBpBallMax>, ctx->num_cu * 5);
                 bp_debug_sync(s, "k_bp_query");
                 hipLaunchKernelGGL(mc::k_bp_keepflags, grid_for(nslot), dim3(256), 0, s, st + BS_NS,
                                    ctx->d_slot_nn.as<int>(), ctx->d_kflag.as<int>(), ctx->d_ksize.as<int>());

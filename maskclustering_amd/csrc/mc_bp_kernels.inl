@@ -114,6 +114,14 @@ __device__ __forceinline__ void bp_recip(const double *__restrict__ K, double rk
     rk[1] = 1.0 / K[1];
 }
 
+// a value equal in every lane, moved to scalar registers (frees its VGPRs for the rest of the slot)
+__device__ __forceinline__ double uniform_d(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane(static_cast<int>(b & 0xFFFFFFFFll));
+    const int hi = __builtin_amdgcn_readfirstlane(static_cast<int>(b >> 32));
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
 __device__ __forceinline__ void bp_world(const double *__restrict__ K, const double *__restrict__ T, int u, int v,
                                          float d, double &ox, double &oy, double &oz, const double *rk)
 {
@@ -277,9 +285,11 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
           const int sids[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
           const float ds[4] = {dq[u].x, dq[u].y, dq[u].z, dq[u].w};
           unsigned vw = 0u;  // the four pixels' valid ids (k_bp_compact reads these instead of seg + depth)
+          int id[4];
+          unsigned pend = 0u;
 #pragma unroll
           for (int j = 0; j < 4; j++) {
-            int id = -1;
+            id[j] = -1;
             if (i < i1) {
                 const int sid = sids[j];
                 const float d = ds[j];
@@ -288,17 +298,30 @@ __global__ __launch_bounds__(256) void k_bp_count(const float *__restrict__ dept
                     lastp = sid;
                 }
                 if (static_cast<double>(d) == pr.trunc) trunc = 1;
-                if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id = sid;
+                if (sid != 0 && !skip && d > 0.0f && static_cast<double>(d) < pr.trunc) id[j] = sid;
             }
-            vw |= static_cast<unsigned>(id > 0 ? id : 0) << (8 * j);
-            unsigned long long act = __ballot(id >= 0);
-            while (act) {
-                const int leader = __ffsll(static_cast<long long>(act)) - 1;
-                const int k = __shfl(id, leader, 64);
-                const unsigned long long m = __ballot(id == k);
-                if (lane == leader) cnt[wv][k] += __popcll(m);
-                act &= ~m;
-            }
+            vw |= static_cast<unsigned>(id[j] > 0 ? id[j] : 0) << (8 * j);
+            if (id[j] >= 0) pend |= 1u << j;
+          }
+          // one LDS add per distinct id of the wave's 256 pixels: each lane's count of the id among
+          // its four pixels (0..4) summed over the wave from three ballots of the count's bits
+          while (true) {
+            const unsigned long long act = __ballot(pend != 0u);
+            if (!act) break;
+            const int L = __ffsll(static_cast<long long>(act)) - 1;
+            int mine = -1;
+#pragma unroll
+            for (int j = 3; j >= 0; j--)
+              if (pend & (1u << j)) mine = id[j];
+            const int k = __builtin_amdgcn_readlane(mine, L);
+            unsigned mb = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if ((pend & (1u << j)) && id[j] == k) mb |= 1u << j;
+            const int c = __popc(mb);
+            const int tot = __popcll(__ballot(c & 1)) + 2 * __popcll(__ballot(c & 2)) + 4 * __popcll(__ballot(c & 4));
+            if (lane == L) cnt[wv][k] += tot;
+            pend &= ~mb;
           }
           if (i < i1) *reinterpret_cast<unsigned *>(vid + fb + i) = vw;
         }
@@ -488,25 +511,23 @@ __global__ __launch_bounds__(256) void k_bp_compact(const unsigned char *__restr
 #pragma unroll
             for (int j = 3; j >= 0; j--)
               if (pend & (1u << j)) mine = id[j];
-            const int k = __shfl(mine, L, 64);
+            const int k = __builtin_amdgcn_readlane(mine, L);
             unsigned mb = 0u;
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if ((pend & (1u << j)) && id[j] == k) mb |= 1u << j;
             const int c = __popc(mb);
-            int incl = c;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-              const int y = __shfl_up(incl, d, 64);
-              if (lane >= d) incl += y;
-            }
-            const int tot = __shfl(incl, 63, 64);
+            // the lanes' exclusive prefix of c (0..4) and its total from three ballots of c's bits
+            const unsigned long long below = (1ull << lane) - 1ull;
+            const unsigned long long c0 = __ballot(c & 1), c1 = __ballot(c & 2), c2 = __ballot(c & 4);
+            const int excl = __popcll(c0 & below) + 2 * __popcll(c1 & below) + 4 * __popcll(c2 & below);
+            const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
             int b = 0;
             if (lane == L) {
               b = mycur[k];
               mycur[k] = b + tot;
             }
-            b = __shfl(b, L, 64) + incl - c;
+            b = __builtin_amdgcn_readlane(b, L) + excl;
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if (mb & (1u << j)) pos[j] = b + __popc(mb & ((1u << j) - 1u));
@@ -607,14 +628,19 @@ __global__ __launch_bounds__(1024) void k_bp_vox_order(const int *__restrict__ d
 }
 
 
-// tiers: <256, 3072, 2048> (32 KB of LDS, four workgroups per CU) for every slot; <512, 12288, 8192>
-// (140 KB, one per CU) for the slots the first tier lists; the global-hash kernel after that
-constexpr int kVxT = 256, kVxH = 3072, kVxV = 2048;    // first tier: threads (pixels per chunk), hash entries (load <= 2/3), voxels
-constexpr int kVxT2 = 512, kVxH2 = 12288, kVxV2 = 8192;  // second tier
+// tiers: <256, 2176, 2048> (31 KB of LDS, five workgroups per CU: the kernel waits on latency, and a
+// fifth workgroup hides more of it than the 3072-entry table's shorter probes at high load save:
+// C3 voxel 20.7 -> 19.8 ms per scene) for every slot; <512, 12288, 8192> (155 KB, one per CU; the
+// running sums of a slot's first 512 voxels in LDS) for the slots the first tier lists; the
+// global-hash kernel after that.  (Measured and not kept: the first 512 / 1408 voxels' running sums
+// in LDS in the first tier at three / two workgroups per CU: 23.9 / 30.8 ms.)
+constexpr int kVxT = 256, kVxH = 2176, kVxV = 2048;    // first tier: threads (pixels per chunk), hash entries, voxels
+constexpr int kVxWpe = 5;                              // its waves per SIMD (= workgroups per CU)
+constexpr int kVxT2 = 512, kVxH2 = 12288, kVxV2 = 8192, kVxL2 = 512;  // second tier (+ LDS running sums)
 constexpr unsigned kVxEmpty = ~0u;
 
-template <int T, int H, int V>
-__global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
+template <int T, int H, int V, int VL, int WPE = 1>
+__global__ __launch_bounds__(T, WPE) void k_bp_voxel_lds(const int *__restrict__ dNS, const int *__restrict__ order,
                                                     const int *__restrict__ slot_frame, const int *__restrict__ slot_np,
                                                     const int *__restrict__ slot_pix,
                                                     const unsigned *__restrict__ pix_list, const float *__restrict__ depth,
@@ -632,6 +658,10 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
     __shared__ double red[6 * NW];
     __shared__ int wsn[NW];
     __shared__ int s_flag;
+    // the running sums of the slot's first VL voxels stay in LDS (no global round trip per chunk for
+    // them); voxels numbered VL and up keep theirs at the slot's range of vpts / vcnt
+    __shared__ double lsx[VL > 0 ? VL : 1], lsy[VL > 0 ? VL : 1], lsz[VL > 0 ? VL : 1];
+    __shared__ int lcn[VL > 0 ? VL : 1];
     const int NS = *dNS;
     const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
     const int W = pr.W;
@@ -683,7 +713,7 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
         BP_STAMP(36);  // 0. min bound
         double vmin[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
+        for (int c = 0; c < 3; c++) vmin[c] = uniform_d(mn[c] - pr.vs * 0.5);  // (scalar registers)
         // 1. chunks in list order: voxel ids in first-occurrence order and the running sums
         int nv = 0;
         unsigned ivA = t < n ? pl[t] : 0u;              // this chunk's pixel
@@ -761,11 +791,18 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
             double ax = 0.0, ay = 0.0, az = 0.0;
             int cnt = 0;
             if (first && !isnew) {  // the running sum so far, loaded under the barrier
-                const double *o = vpts + 3 * (static_cast<size_t>(base) + v);
-                ax = o[0];
-                ay = o[1];
-                az = o[2];
-                cnt = vcnt[base + v];
+                if (v < static_cast<unsigned>(VL)) {
+                    ax = lsx[v];
+                    ay = lsy[v];
+                    az = lsz[v];
+                    cnt = lcn[v];
+                } else {
+                    const double *o = vpts + 3 * (static_cast<size_t>(base) + v);
+                    ax = o[0];
+                    ay = o[1];
+                    az = o[2];
+                    cnt = vcnt[base + v];
+                }
             }
             // the next chunk's depths and the one after's pixels, behind the sums' loads (a wave's
             // memory operations complete in issue order: the fold waits for the sums only).  The
@@ -809,11 +846,18 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
                         az = az + psz[i];
                     }
                 }
-                double *o = vpts + 3 * (static_cast<size_t>(base) + v);
-                o[0] = ax;
-                o[1] = ay;
-                o[2] = az;
-                vcnt[base + v] = cnt;
+                if (v < static_cast<unsigned>(VL)) {
+                    lsx[v] = ax;
+                    lsy[v] = ay;
+                    lsz[v] = az;
+                    lcn[v] = cnt;
+                } else {
+                    double *o = vpts + 3 * (static_cast<size_t>(base) + v);
+                    o[0] = ax;
+                    o[1] = ay;
+                    o[2] = az;
+                    vcnt[base + v] = cnt;
+                }
                 hval[h] = (v << 16) | 0xFFFFu;
             }
             nv += tot;
@@ -830,10 +874,17 @@ __global__ __launch_bounds__(T) void k_bp_voxel_lds(const int *__restrict__ dNS,
         // 2. means
         for (int v = t; v < nv; v += T) {
             double *o = vpts + 3 * (static_cast<size_t>(base) + v);
-            const double dn = static_cast<double>(vcnt[base + v]);
-            o[0] = o[0] / dn;
-            o[1] = o[1] / dn;
-            o[2] = o[2] / dn;
+            if (v < VL) {
+                const double dn = static_cast<double>(lcn[v]);
+                o[0] = lsx[v] / dn;
+                o[1] = lsy[v] / dn;
+                o[2] = lsz[v] / dn;
+            } else {
+                const double dn = static_cast<double>(vcnt[base + v]);
+                o[0] = o[0] / dn;
+                o[1] = o[1] / dn;
+                o[2] = o[2] / dn;
+            }
         }
         if (t == 0) slot_nv[s] = nv;
         __syncthreads();
@@ -2231,7 +2282,8 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 // could not serve them): a thread per queued point, over its slot's grid in global memory.  Grid rings up to R = 2 (cells whose nearest face is no nearer than the current k-th
 // distance skipped: a's offsets in its cell, gaps shrunk by 1e-9 ce so the bound stays below every
 // point's computed distance); a point the rings cannot settle (sparse) scans every kept point.
-__global__ __launch_bounds__(256) void k_bp_knn_ring(const int *__restrict__ dq_cnt, const int *__restrict__ dq,
+template <int WPE = 1>
+__global__ __launch_bounds__(256, WPE) void k_bp_knn_ring(const int *__restrict__ dq_cnt, const int *__restrict__ dq,
                                                      const int *__restrict__ slot_pix, const int *__restrict__ slot_m,
                                                      BpDev pr, const double4 *__restrict__ grec,
                                                      const int *__restrict__ gbs, const int *__restrict__ gitem,
@@ -2370,15 +2422,20 @@ __global__ __launch_bounds__(256) void k_bp_denoise_tail(const int *__restrict__
         const double *P = vpts + 3 * static_cast<size_t>(base);
         if constexpr (MC_DBG_CHECK) bp_dbg_knn_tail(P, gsx + base, av, m, min(pr.knn, m), s, base);
         double mean = 0.0, sq = 0.0;
+        // (each pass loads its next 64 values before the ordered chain of this 64 runs)
+        double an = lane < m ? av[lane] : 0.0;
         for (int r0 = 0; r0 < m; r0 += 64) {
             // values that are not > 0 become +0.0, whose add leaves the (non-negative) sum as it is:
             // the ordered chain is plain adds, the selects run lane-parallel before it
-            const double a = r0 + lane < m ? av[r0 + lane] : 0.0;
+            const double a = an;
+            an = r0 + 64 + lane < m ? av[r0 + 64 + lane] : 0.0;
             mean = seq_add64_pos<false>(mean, a > 0 ? a : 0.0);
         }
         mean = mean / static_cast<double>(m);
+        an = lane < m ? av[lane] : 0.0;
         for (int r0 = 0; r0 < m; r0 += 64) {
-            const double v = r0 + lane < m ? av[r0 + lane] : 0.0;
+            const double v = an;
+            an = r0 + 64 + lane < m ? av[r0 + 64 + lane] : 0.0;
             const double d = v > 0 ? (v - mean) * (v - mean) : 0.0;
             sq = seq_add64_pos<false>(sq, d > 0 ? d : 0.0);
         }
@@ -2686,7 +2743,8 @@ __global__ __launch_bounds__(256) void k_bp_denoise(
 // index order (= crop order, :38,123-128) are accepted.  Accepted ids are OR'ed into the block's
 // private bitmap over the scene; coverage = #q with an accepted neighbour / #q (:143); a kept mask
 // (:145) emits its set in ascending order through a bump allocator into tmp.
-__global__ __launch_bounds__(256) void k_bp_query(
+template <int WPE = 1, int KB = kBpBallMax>
+__global__ __launch_bounds__(256, WPE) void k_bp_query(
     const int *__restrict__ dNS, const int *__restrict__ slot_pix, const int *__restrict__ slot_ns,
     const float *__restrict__ slot_box, const float *__restrict__ qpts, BpDev pr, const float4 *__restrict__ gpts,
     const int *__restrict__ gidx, const unsigned long long *__restrict__ gcell, const int *__restrict__ gstart,
@@ -2729,9 +2787,9 @@ __global__ __launch_bounds__(256) void k_bp_query(
             const float qx = q[0], qy = q[1], qz = q[2];
             const int cx = scene_cell(qx, pr.scene_inv), cy = scene_cell(qy, pr.scene_inv),
                       cz = scene_cell(qz, pr.scene_inv);
-            int best[kBpBallMax];
+            int best[KB];  // (KB = 20 when ball_k <= 20: 12 VGPRs fewer, a sixth wave per SIMD)
 #pragma unroll
-            for (int x = 0; x < kBpBallMax; x++) best[x] = INT_MAX;
+            for (int x = 0; x < KB; x++) best[x] = INT_MAX;
             // the cells the ball can reach: a scene point with d2 < r^2 (float, as below) has
             // |dx|, |dy|, |dz| <= r, and the cells are 2r wide, so per axis the cells of
             // [q - r, q + r] widened by a rounding margin (0.01 cell + the float error of q * inv):
@@ -2779,7 +2837,7 @@ __global__ __launch_bounds__(256) void k_bp_query(
             }
             int got = 0;
 #pragma unroll
-            for (int x = 0; x < kBpBallMax; x++) {
+            for (int x = 0; x < KB; x++) {
                 if (x < pr.kball && best[x] != INT_MAX) {
                     const int id = best[x];
                     atomicOr(&mb[id >> 6], 1ull << (id & 63));

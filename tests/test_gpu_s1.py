@@ -22,22 +22,25 @@ def ctx():
     return _native.Context(0)
 
 
-def _run(ctx, scene, depth, seg, K, T):
+def _run(ctx, scene, depth, seg, K, T, **prm):
+    from maskclustering_amd import _native
     ctx.set_points(np.asarray(scene, np.float64).astype(np.float32))
-    ctx.backproject(depth, seg, K, T)
+    ctx.backproject(depth, seg, K, T, _native.bp_params(**prm) if prm else None)
     return ctx.bp_masks()
 
 
-def _check_against_oracle(ctx, fr, frames=None):
+def _check_against_oracle(ctx, fr, frames=None, **prm):
     from oracle import oracle
     idx = list(range(fr.num_frames)) if frames is None else frames
-    col, lab, off, pts = _run(ctx, fr.scene_points, fr.depth[idx], fr.seg[idx], fr.intrinsics[idx], fr.poses[idx])
+    col, lab, off, pts = _run(ctx, fr.scene_points, fr.depth[idx], fr.seg[idx], fr.intrinsics[idx], fr.poses[idx],
+                              **prm)
+    oprm = oracle.BpParams.default(**prm) if prm else None
     st = ctx.bp_candidates()
     scene = fr.scene_points.astype(np.float32)
     g = 0
     row = 0
     for c, f in enumerate(idx):
-        ol, oo, op, ost = oracle.s1_frame(scene, fr.depth[f], fr.seg[f], fr.intrinsics[f], fr.poses[f])
+        ol, oo, op, ost = oracle.s1_frame(scene, fr.depth[f], fr.seg[f], fr.intrinsics[f], fr.poses[f], oprm)
         big = ost[ost[:, 1] >= 25]
         dev = st[st[:, 0] == c]
         assert len(dev) == len(big), f"frame {f}: candidates {len(dev)} vs {len(big)}"
@@ -231,6 +234,23 @@ def test_voxel_kernels_match_oracle(ctx, monkeypatch, tier):
     (tier 1) or the second LDS tier (tier 2), against the oracle and the reference's glue fixture."""
     monkeypatch.setenv("MC_VX_GLOBAL", str(tier))
     _check_dense(ctx)
+
+
+@pytest.mark.parametrize("tier", [0, 2])
+def test_high_resolution_voxel_tiers_match_oracle(ctx, monkeypatch, tier):
+    """ScanNet++-resolution slots (thousands of voxels) through the first voxel tier and through the
+    second (every slot forced there: its first 512 voxels' running sums in LDS, the rest in HBM)."""
+    monkeypatch.setenv("MC_VX_GLOBAL", str(tier))
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    _check_against_oracle(ctx, make_frames_shape("tiny", seed=7, H=1440, W=1920, num_frames=1))
+
+
+@pytest.mark.parametrize("ball_k", [7, 21, 32])
+def test_ball_k_matches_oracle(ctx, ball_k):
+    """ball_k other than the reference's 20: the query's 32-entry best list (ball_k > 20; five
+    workgroups per CU) and the 20-entry one with fewer taken, against the CPU restatement."""
+    from maskclustering_amd.synthetic_frames import make_frames_shape
+    _check_against_oracle(ctx, make_frames_shape("tiny", seed=5, H=360, W=480, num_frames=3), ball_k=ball_k)
 
 
 def test_high_resolution_frame_matches_oracle(ctx):
