@@ -1916,7 +1916,7 @@ void bp_denoise_tail_launch(mc_ctx *ctx, hipStream_t s, int ncap, int *st, const
                            ctx->d_acc.as<double4>(), ctx->d_bstart.as<int>(), ctx->d_vx_list.as<int>(),
                            ctx->d_slot_grid.as<double>(), ctx->d_avg.as<double>(), st + BS_DNERR);
     };
-    ring(mc::k_bp_knn_ring<1>, 8);  // (at five or six waves per SIMD, spilling: no faster)
+    ring(mc::k_bp_knn_ring<4>, 8);  // (four waves per SIMD; at five or six, spilling: no faster)
     // a wave per slot whose ordered sums wait on latency: as many waves as its 45 VGPRs allow
     const int tail_wg = getenv("MC_BP_TAILWG") ? atoi(getenv("MC_BP_TAILWG")) : 8;
     hipLaunchKernelGGL(mc::k_bp_denoise_tail, dim3(ctx->num_cu * tail_wg), dim3(256), 0, s,

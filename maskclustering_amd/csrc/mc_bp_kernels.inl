@@ -2291,41 +2291,60 @@ __global__ __launch_bounds__(256, WPE) void k_bp_knn_ring(const int *__restrict_
                                                      int *__restrict__ err)
 {
     const int ne = *dq_cnt;
-    for (int f = blockIdx.x * 256 + threadIdx.x; f < ne; f += gridDim.x * 256) {
-        const int s = dq[f];
-        const int base = slot_pix[s];
+    const int lane = lane_id();
+    // wave-uniform loop (a wave's 64 points together), so that the whole wave can take a sparse
+    // point's whole-cloud scan (below)
+    const int nwv = gridDim.x * (256 / 64);
+    for (int f0 = ((blockIdx.x * 256 + threadIdx.x) >> 6) * 64; f0 < ne; f0 += nwv * 64) {
+        const int f = f0 + lane;
+        bool active = f < ne;
+        const int s = active ? dq[f] : 0;
+        const int base = active ? slot_pix[s] : 0;
         const double *gm = slot_grid + 8 * static_cast<size_t>(s);
-        const double mn[3] = {gm[0], gm[1], gm[2]};
+        double mn[3] = {0.0, 0.0, 0.0};
         BpLdsGrid g;
         g.pt = grec + base;
         g.bs = gbs + 2 * static_cast<size_t>(base) + s;
-        g.nb = static_cast<unsigned>(gm[6]);
-        const int n = static_cast<int>(gm[7]);
+        g.nb = 1u;
+        int n = 0;
+        if (active) {
 #pragma unroll
-        for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(gm[3 + c]);
-        {
+            for (int c = 0; c < 3; c++) mn[c] = gm[c];
+            g.nb = static_cast<unsigned>(gm[6]);
+            n = static_cast<int>(gm[7]);
+#pragma unroll
+            for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(gm[3 + c]);
+        }
+        int q = 0, r = 0;
+        if (active) {
             const int item = gitem[f];
-            const int q = item & 0x3FFF, r = item >> 14;
+            q = item & 0x3FFF;
+            r = item >> 14;
             // an entry outside its slot (a broken hand-off from the class kernel) is reported, not followed
             if (q >= n || r < 0 || r >= slot_m[s]) {
                 atomicOr(err, 1);
-                continue;
+                active = false;
             }
-            const double4 a = g.pt[q];
-            double best[kBpKnnMax];
+        }
+        double best[kBpKnnMax];
 #pragma unroll
-            for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-            int found = 0;
-            bool done = false;
-            int x, y, z;
+        for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
+        int found = 0;
+        bool done = false;
+        double4 a = make_double4(0.0, 0.0, 0.0, 0.0);
+        int x = 0, y = 0, z = 0;
+        const double ce = pr.ce, sl = 1e-9 * pr.ce;
+        double ox = 0.0, oy = 0.0, oz = 0.0;
+        if (active) {
+            a = g.pt[q];
             unpack3(static_cast<unsigned long long>(__double_as_longlong(a.w)) & ~kKeptBit, x, y, z);
             auto take = [&](int, double d2) {
                 sorted_insert(best, d2);
                 found++;
             };
-            const double ce = pr.ce, sl = 1e-9 * pr.ce;
-            const double ox = fmin(fmax(a.x - mn[0] - x * ce, 0.0), ce), oy = fmin(fmax(a.y - mn[1] - y * ce, 0.0), ce),
-                         oz = fmin(fmax(a.z - mn[2] - z * ce, 0.0), ce);
+            ox = fmin(fmax(a.x - mn[0] - x * ce, 0.0), ce);
+            oy = fmin(fmax(a.y - mn[1] - y * ce, 0.0), ce);
+            oz = fmin(fmax(a.z - mn[2] - z * ce, 0.0), ce);
             auto gap = [&](int d, double o) {
                 return d == 0 ? 0.0 : fmax(0.0, (d > 0 ? d * ce - o : -d * ce - (ce - o)) - sl);
             };
@@ -2343,16 +2362,13 @@ __global__ __launch_bounds__(256, WPE) void k_bp_knn_ring(const int *__restrict_
                 const double reach = static_cast<double>(R) * ce;
                 done = found >= kBpKnnMax && best[kBpKnnMax - 1] < reach * reach * (1.0 - 1e-9);
             }
-            if (!done) {  // sparse point: every kept point of the slot, in sorted order
-#pragma unroll
-                for (int k = 0; k < kBpKnnMax; k++) best[k] = DBL_MAX;
-                for (int q2 = 0; q2 < n; q2++) {
-                    const double4 p = g.pt[q2];
-                    if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
-                    const double ex = a.x - p.x, ey = a.y - p.y, ez = a.z - p.z;
-                    sorted_insert(best, ((ex * ex) + (ey * ey)) + (ez * ez));
-                }
-            }
+        }
+#ifdef MC_BP_RING_NOFB
+        done = true;  // timing-only diagnostics build: no whole-cloud fallback (wrong results)
+#endif
+        // the rings' k smallest -> the mean distance (the k-NN list's registers free for the scan below)
+        double sum = 0.0;
+        if (active && done) {
             if constexpr (MC_DBG_CHECK) {  // the ring result against every kept record of the slot's grid
                 double bf[kBpKnnMax];
                 for (int k = 0; k < kBpKnnMax; k++) bf[k] = DBL_MAX;
@@ -2383,9 +2399,49 @@ __global__ __launch_bounds__(256, WPE) void k_bp_knn_ring(const int *__restrict_
                     }
                 }
             }
-            double sum = 0.0;
 #pragma unroll
             for (int k = 0; k < kBpKnnMax; k++) sum = sum + sqrt(best[k]);
+        }
+        // sparse points (the rings could not settle them): every kept point of the slot, the whole
+        // wave scanning one such point's slot (a lane's k smallest over its stride, then the k
+        // smallest of the wave by k rounds of a wave minimum): the same k smallest values, in the
+        // same ascending order, as one thread's scan, without one lane's O(n) walk holding the wave
+        unsigned long long need = __ballot(active && !done);
+        while (need) {
+            const int L = __ffsll(static_cast<long long>(need)) - 1;
+            need &= need - 1ull;
+            auto bcast_d = [&](double v) {
+                const long long b = __double_as_longlong(v);
+                const int lo = __builtin_amdgcn_readlane(static_cast<int>(b & 0xFFFFFFFFll), L);
+                const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), L);
+                return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+            };
+            const double ax = bcast_d(a.x), ay = bcast_d(a.y), az = bcast_d(a.z);
+            const int nL = __builtin_amdgcn_readlane(n, L), baseL = __builtin_amdgcn_readlane(base, L);
+            const double4 *ptL = grec + baseL;
+            double bl[kBpKnnMax];
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) bl[k] = DBL_MAX;
+            for (int q2 = lane; q2 < nL; q2 += 64) {
+                const double4 p = ptL[q2];
+                if (!(static_cast<unsigned long long>(__double_as_longlong(p.w)) & kKeptBit)) continue;
+                const double ex = ax - p.x, ey = ay - p.y, ez = az - p.z;
+                sorted_insert(bl, ((ex * ex) + (ey * ey)) + (ez * ez));
+            }
+#pragma unroll
+            for (int k = 0; k < kBpKnnMax; k++) {
+                const double h = bl[0];
+                const double m = wave_min_d(h);
+                const unsigned long long w = __ballot(h == m);
+                if (lane == __ffsll(static_cast<long long>(w)) - 1) {  // the lane holding it moves on
+#pragma unroll
+                    for (int j = 0; j + 1 < kBpKnnMax; j++) bl[j] = bl[j + 1];
+                    bl[kBpKnnMax - 1] = DBL_MAX;
+                }
+                if (lane == L) sum = sum + sqrt(m);  // (k ascending, as the rings' sum above)
+            }
+        }
+        if (active) {
             gavg[base + r] = sum / static_cast<double>(kBpKnnMax);
             bp_dbg_path(static_cast<size_t>(base) + r, 4u | (static_cast<unsigned>(found > 0xFFFF ? 0xFFFF : found) << 4) |
                                                          (static_cast<unsigned>(done ? 1 : 0) << 20));
