@@ -1478,22 +1478,34 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 }
 
 // The same lists built from each unordered pair once (classes whose counts live in LDS): sorted
-// position q visits the points of its own cell at later positions and the 13 cells after its own in
-// (z, y, x) order; a pair within eps is appended to both lists, each at the slot an LDS atomic on its
-// counter returns (sflag[] holds the counts, self entries already in slot 0).  Half the candidate
-// records of lds_eps_list; the slot order within a list is arbitrary, which no consumer depends on
-// (the union and the border labels are order-free, the k-NN sorts).
+// position q visits half of its own bucket cyclically and the 13 cells after its own in (z, y, x)
+// order; a pair within eps is appended to both lists, each at the slot an LDS atomic on its counter
+// returns (sflag[] holds the counts, self entries already in slot 0).  Half the candidate records of
+// lds_eps_list; the slot order within a list is arbitrary, which no consumer depends on (the union
+// and the border labels are order-free, the k-NN sorts).  Own bucket [s, e) of c positions: q
+// visits the next h positions cyclically, h = (c - 1) / 2, plus the opposite one when c is even and
+// q is in the first half, so every pair of the bucket is visited once and each point's first list
+// entries (the union's first sampled link, step 6) mix earlier and later positions of its cell.
 template <int N>
 __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, int z, double ax, double ay, double az,
                                               const BpDev &pr, unsigned short *__restrict__ nbw, int q, int *sflag,
                                               int *farA, int *farB)
 {
+    const unsigned b0 = mod_mul(bp_hash3(x, y, z), g.nb);
+    const int s0 = g.bs[b0], e0 = g.bs[b0 + 1], c0 = e0 - s0;
+    const int h0 = (c0 - 1) / 2 + ((c0 % 2 == 0 && q - s0 < c0 / 2) ? 1 : 0);
+    const int f1 = min(q + 1 + h0, e0);               // forward part [q + 1, f1)
+    const int w1 = s0 + max(0, q + 1 + h0 - e0);      // wrapped part [s0, w1)
     auto range = [&](int d, unsigned long long &key) {
+        if (d <= 13) {  // 12: the own bucket's wrapped part, 13: its forward part
+            key = pack3(x, y, z);
+            return d == 12 ? make_int2(s0, w1) : make_int2(q + 1, f1);
+        }
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
         if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
-        return make_int2(d == 13 ? q + 1 : g.bs[b], g.bs[b + 1]);  // own cell: later positions only
+        return make_int2(g.bs[b], g.bs[b + 1]);
     };
     const double eps2 = pr.eps2;
     int fa = q, fb = q;
@@ -1512,9 +1524,9 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         }
     };
     unsigned long long nkey = 0;
-    int2 nr = range(13, nkey);
+    int2 nr = range(12, nkey);
 #pragma unroll 1
-    for (int d = 13; d < 27; d++) {
+    for (int d = 12; d < 27; d++) {
         const unsigned long long key = nkey;
         const int2 r = nr;
         if (d + 1 < 27) nr = range(d + 1, nkey);
