@@ -206,15 +206,21 @@ def s1_cpu_rate(scene_f32, frame_at, F, n_all=64, n_one=8):
     fr = [frame_at(int(i)) for i in idx]
     thr = oracle.default_threads()
 
+    crop = []
+
     def timed(sel, threads):
         t0 = time.perf_counter()
-        oracle.s1_frames(scene_f32, [fr[k][0] for k in sel], [fr[k][1] for k in sel],
-                         np.stack([fr[k][2] for k in sel]), np.stack([fr[k][3] for k in sel]), threads=threads)
-        return (time.perf_counter() - t0) / len(sel)
+        out = oracle.s1_frames(scene_f32, [fr[k][0] for k in sel], [fr[k][1] for k in sel],
+                               np.stack([fr[k][2] for k in sel]), np.stack([fr[k][3] for k in sel]), threads=threads)
+        dt = (time.perf_counter() - t0) / len(sel)
+        if not crop:  # the reference's crop (crop_scene_points, :59-66) per mask that reaches it: stats "ncand"
+            c = oracle.S1_STATS.index("ncand")
+            crop.append(sum(int(st[:, c].sum()) for _, _, _, st in out) / len(sel))
+        return dt
 
     one = list(range(0, len(idx), max(1, len(idx) // n_one)))[:n_one]
     return dict(all=timed(range(len(idx)), thr), one=timed(one, 1), threads=thr, n_all=len(idx), n_one=len(one),
-                frames=F)
+                frames=F, crop_candidates_per_frame=crop[0])
 
 
 def graph_cpu(P, F, col, lab, off, pts, threads, dense=False, cfg=None):
@@ -234,6 +240,7 @@ def e2e_cpu_baseline(s1, P, F, col, lab, off, pts, cfg):
     all_s, one_s = s1["all"] * F + g_all, s1["one"] * F + g_one
     pairs = tm["pairs"]
     return {"value": round(pairs / all_s, 1), "unit": "mask-pairs/s", "cores": s1["threads"], "kind": "port",
+            "s1_crop_candidates_per_frame": round(s1["crop_candidates_per_frame"], 1),
             "sample": f"S1 port (oracle/s1_oracle.c, OpenMP over frames, {s1['threads']} threads) timed on "
                       f"{s1['n_all']} frames spread over the {F} and scaled to {F} ({s1['all'] * F:.1f} s) + the "
                       f"S2-S6 port (oracle/graph_sparse.c, {s1['threads']} threads) on the full scene ({g_all:.2f} s)",
@@ -1098,6 +1105,23 @@ def main():
                          "scripts/cpu_ref_fit.py); S1 excluded (Open3D / pytorch3d absent)",
                 "source": os.path.relpath(fit_path, REPO),
                 "over_device_scene": round(t_ref * 1e3 / max(ms_per_step_pre, 1e-9), 1)}
+
+    if cpu and cpu.get("s1_crop_candidates_per_frame") and stages.get("bp_query"):
+        # SURVEY.md §8(d)'s S1 bytes count each mask's cropped candidates (12·c̄ per mask): the reference's
+        # crop (every scene point inside the mask's AABB) is never made on the device, so c̄ comes from
+        # the port's crop (oracle/s1_oracle.c, stats "ncand") on the cpu_baseline's sampled frames, scaled
+        # to the scene's frames; the query kernel reads only the 2r cells around each mask point
+        q = stages["bp_query"]
+        n_q = calib["bp_query"][1]  # launches per scene (the calibration step is one scene)
+        cand_b = 12.0 * cpu["s1_crop_candidates_per_frame"] * runner.shape[0] / max(n_q, 1)
+        with_c = work["bp_query"][1] + cand_b
+        avg_q = q["avg_launch_ms"] / 1e3
+        q["survey_model"] = "12·Σ mask points + 4·Σ neighbour ids + 12·Σ cropped candidates (c̄ sampled, see note)"
+        q["survey_frac"] = round(with_c / avg_q / 1e9 / HBM_PEAK_GBS, 4)
+        if pmc.get("bp_query"):
+            q["traffic_over_survey_model"] = round(float(pmc["bp_query"]["bytes_per_launch"]) / with_c, 2)
+        q["survey_note"] = (f"c̄: {cpu['s1_crop_candidates_per_frame']:.0f} cropped scene points per frame (summed over its "
+                            "masks) in the S1 port's crop on the cpu_baseline frames, scaled to the scene")
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary and args.variant in ("e2e", "g"):
