@@ -1422,7 +1422,11 @@ __device__ __forceinline__ int nb_cnt(int f) { return f & kNbCnt; }
 template <int N>
 __device__ __forceinline__ void nb_put(unsigned short *__restrict__ nbw, int q, int k, unsigned e)
 {
-    nbw[(static_cast<size_t>(k >> 3) * N + q) * 8 + (k & 7)] = static_cast<unsigned short>(e);
+    // 32-bit offset (< 8 * 64 * N <= 2^23): a store with the workgroup's region base in SGPRs and one
+    // VGPR offset, no 64-bit address arithmetic per store
+    const unsigned off = ((static_cast<unsigned>(k) >> 3) * static_cast<unsigned>(N) + static_cast<unsigned>(q)) * 8u +
+                         (static_cast<unsigned>(k) & 7u);
+    *reinterpret_cast<unsigned short *>(reinterpret_cast<char *>(nbw) + (off << 1)) = static_cast<unsigned short>(e);
 }
 __device__ __forceinline__ unsigned nb_class(double d2, const BpDev &pr)
 {
@@ -1514,9 +1518,12 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
         if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
             const unsigned c = nb_class(d2, pr) << 14;
+            // entries past the cap overwrite the last slot (as lds_eps_list): every slot still holds a
+            // neighbour, and a list past the cap is not read (its point walks the cells), so the
+            // stores need no branch
             const int o1 = atomicAdd(&sflag[q], 1), o2 = atomicAdd(&sflag[q2], 1);
-            if (o1 < kBpNbCap) nb_put<N>(nbw, q, o1, static_cast<unsigned>(q2) | c);
-            if (o2 < kBpNbCap) nb_put<N>(nbw, q2, o2, static_cast<unsigned>(q) | c);
+            nb_put<N>(nbw, q, min(o1, kBpNbCap - 1), static_cast<unsigned>(q2) | c);
+            nb_put<N>(nbw, q2, min(o2, kBpNbCap - 1), static_cast<unsigned>(q) | c);
             // far neighbours of this point's forward walk (radius classes 3 and 2): the union's sampled
             // links (step 6), stored once after the walk
             fa = c == (3u << 14) ? q2 : fa;
@@ -2181,7 +2188,10 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
             const int found = __popcll(mall);
             unsigned long long pm = __popcll(m1) >= kk ? m1 : __popcll(m2) >= kk ? m2 : __popcll(m3) >= kk ? m3 : mall;
             if (found >= kk) {
-                const unsigned short *lst = nbw + static_cast<size_t>(q) * 8;  // slot k: lst[(k / 8) * 8 * N + k % 8]
+                // slot k of q: byte (((k / 8) * N + q) * 8 + k % 8) * 2 of the region (32-bit offsets
+                // from the workgroup's base, as nb_put)
+                const char *lstb = reinterpret_cast<const char *>(nbw);
+                const unsigned qb = static_cast<unsigned>(q) * 16u;
                 // the selected entries' positions are reloaded from the list (a lane-varying slot index
                 // cannot read the register copy), kBpKnnBatch at a time, the next batch's loads in flight
                 // while this batch's points are inserted: the lists live past the L2 (one region per
@@ -2191,7 +2201,9 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
                     for (int u = 0; u < kBpKnnBatch; u++) {
                         const int b = pm ? __ffsll(static_cast<long long>(pm)) - 1 : -1;
                         pm &= pm - 1;
-                        e[u] = b >= 0 ? static_cast<int>(lst[static_cast<size_t>(b >> 3) * 8 * N + (b & 7)]) : -1;
+                        const unsigned ob = (static_cast<unsigned>(b) >> 3) * (16u * static_cast<unsigned>(N)) + qb +
+                                            ((static_cast<unsigned>(b) & 7u) << 1);
+                        e[u] = b >= 0 ? static_cast<int>(*reinterpret_cast<const unsigned short *>(lstb + ob)) : -1;
                     }
                 };
                 int en[kBpKnnBatch];
