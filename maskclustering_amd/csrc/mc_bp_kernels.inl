@@ -1517,17 +1517,18 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
         if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
-            const unsigned c = nb_class(d2, pr) << 14;
-            // entries past the cap overwrite the last slot (as lds_eps_list): every slot still holds a
-            // neighbour, and a list past the cap is not read (its point walks the cells), so the
-            // stores need no branch
+            // both slots' atomics in flight together; the radius class and the far links (radius
+            // classes 3 and 2 of this point's forward walk: the union's sampled links, step 6, stored
+            // once after the walk) computed under them; one wait before the stores.  Entries past
+            // the cap overwrite the last slot (as lds_eps_list): every slot still holds a neighbour,
+            // and a list past the cap is not read (its point walks the cells), so no branch
             const int o1 = atomicAdd(&sflag[q], 1), o2 = atomicAdd(&sflag[q2], 1);
-            nb_put<N>(nbw, q, min(o1, kBpNbCap - 1), static_cast<unsigned>(q2) | c);
-            nb_put<N>(nbw, q2, min(o2, kBpNbCap - 1), static_cast<unsigned>(q) | c);
-            // far neighbours of this point's forward walk (radius classes 3 and 2): the union's sampled
-            // links (step 6), stored once after the walk
+            const unsigned c = nb_class(d2, pr) << 14;
             fa = c == (3u << 14) ? q2 : fa;
             fb = c == (2u << 14) ? q2 : fb;
+            asm volatile("" ::"v"(o1), "v"(o2), "v"(c));
+            nb_put<N>(nbw, q, min(o1, kBpNbCap - 1), static_cast<unsigned>(q2) | c);
+            nb_put<N>(nbw, q2, min(o2, kBpNbCap - 1), static_cast<unsigned>(q) | c);
         }
     };
     unsigned long long nkey = 0;
