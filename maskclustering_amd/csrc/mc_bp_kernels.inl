@@ -1454,7 +1454,7 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
     auto visit = [&](const double4 &p, int q2, unsigned long long key) {
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
-        if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
+        if (static_cast<unsigned long long>(__double_as_longlong(p.w)) == key && d2 < eps2) {  // (no kept bits yet)
             const unsigned c = nb_class(d2, pr);
             nb_put<N>(nbw, q, min(cnt, kBpNbCap - 1), static_cast<unsigned>(q2) | (c << 14));
             if (c == 3u) farA = q2;  // far neighbours: the sampled links of the union (step 6)
@@ -1516,7 +1516,8 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
     auto visit = [&](const double4 &p, int q2, unsigned long long key) {
         const double dx = ax - p.x, dy = ay - p.y, dz = az - p.z;
         const double d2 = ((dx * dx) + (dy * dy)) + (dz * dz);
-        if ((static_cast<unsigned long long>(__double_as_longlong(p.w)) & ~kKeptBit) == key && d2 < eps2) {
+        // (no record carries the kept bit yet: the class filter sets it after the lists are built)
+        if (static_cast<unsigned long long>(__double_as_longlong(p.w)) == key && d2 < eps2) {
             // both slots' atomics in flight together; the radius class and the far links (radius
             // classes 3 and 2 of this point's forward walk: the union's sampled links, step 6, stored
             // once after the walk) computed under them; one wait before the stores.  Entries past
