@@ -230,7 +230,8 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const float *__restrict__ 
     for (int j = blockIdx.x * 256 + threadIdx.x; j < P; j += gridDim.x * 256) {
         const unsigned b = bkt[j];
         const int pos = start[b] + atomicSub(&cnt[b], 1) - 1;
-        gpts[pos] = make_float4(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], 0.f);
+        // w: the scene index's bits (the query reads point and id in one 16-byte load)
+        gpts[pos] = make_float4(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], __int_as_float(j));
         gidx[pos] = j;
         gcell[pos] = cellk[j];
     }
@@ -2907,14 +2908,23 @@ __global__ __launch_bounds__(256, WPE) void k_bp_query(
                 const unsigned long long key = nkey;
                 const int2 rng = nrng;
                 if (d + 1 < ncell) nrng = cell_range(d + 1, nkey);
-                for (int k = rng.x; k < rng.y; k++) {
-                    if (gcell[k] != key) continue;
-                    const float4 p = gpts[k];
+                // two records per step, each one's cell key and point + id (w) loaded together
+                // (independent loads: one memory round trip per step instead of up to three dependent
+                // ones); a step past the range re-reads its last record and ignores it
+                auto take = [&](unsigned long long ck, const float4 &p) {
+                    if (ck != key) return;
                     if (!(p.x > lo[0] && p.x < hi[0] && p.y > lo[1] && p.y < hi[1] && p.z > lo[2] && p.z < hi[2]))
-                        continue;
+                        return;
                     const float ex = qx - p.x, ey = qy - p.y, ez = qz - p.z;
                     const float d2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, __fmul_rn(ex, ex)));
-                    if (d2 < pr.r2) sorted_insert(best, gidx[k]);
+                    if (d2 < pr.r2) sorted_insert(best, __float_as_int(p.w));
+                };
+                for (int k = rng.x; k < rng.y; k += 2) {
+                    const int k1 = min(k + 1, rng.y - 1);
+                    const unsigned long long c0 = gcell[k], c1 = gcell[k1];
+                    const float4 p0 = gpts[k], p1 = gpts[k1];
+                    take(c0, p0);
+                    if (k + 1 < rng.y) take(c1, p1);
                 }
             }
             int got = 0;
