@@ -832,20 +832,32 @@ __global__ __launch_bounds__(T, WPE) void k_bp_voxel_lds(const int *__restrict__
                 if (v >= static_cast<unsigned>(V)) s_flag = 1;
             }
             if (first && v < static_cast<unsigned>(V)) {
-                // this chunk's pixels of voxel v, in pixel order
+                // this chunk's pixels of voxel v, in pixel order, each pixel's staged point loaded one
+                // pixel ahead of the adds (the same sums in the same order, the LDS latency under the
+                // previous pixel's adds)
 #pragma unroll
                 for (int w = 0; w < NW; w++) {
                     unsigned long long m = msk[t][w];
                     if (!m) continue;
                     msk[t][w] = 0ull;
                     cnt += __popcll(m);
+                    int i = 64 * w + static_cast<int>(__builtin_ctzll(m));
+                    m &= m - 1ull;
+                    double cx = psx[i], cy = psy[i], cz = psz[i];
                     while (m) {
-                        const int i = 64 * w + __ffsll(static_cast<long long>(m)) - 1;
+                        i = 64 * w + static_cast<int>(__builtin_ctzll(m));
                         m &= m - 1ull;
-                        ax = ax + psx[i];
-                        ay = ay + psy[i];
-                        az = az + psz[i];
+                        const double nx = psx[i], ny = psy[i], nz = psz[i];
+                        ax = ax + cx;
+                        ay = ay + cy;
+                        az = az + cz;
+                        cx = nx;
+                        cy = ny;
+                        cz = nz;
                     }
+                    ax = ax + cx;
+                    ay = ay + cy;
+                    az = az + cz;
                 }
                 if (v < static_cast<unsigned>(VL)) {
                     lsx[v] = ax;
