@@ -835,9 +835,11 @@ __global__ __launch_bounds__(T, WPE) void k_bp_voxel_lds(const int *__restrict__
                 // this chunk's pixels of voxel v, in pixel order, each pixel's staged point loaded one
                 // pixel ahead of the adds (the same sums in the same order, the LDS latency under the
                 // previous pixel's adds)
+                unsigned long long mnext = msk[t][0];
 #pragma unroll
                 for (int w = 0; w < NW; w++) {
-                    unsigned long long m = msk[t][w];
+                    unsigned long long m = mnext;
+                    if (w + 1 < NW) mnext = msk[t][w + 1];  // the next wave's word under this one's adds
                     if (!m) continue;
                     msk[t][w] = 0ull;
                     cnt += __popcll(m);
