@@ -2375,14 +2375,15 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                        st + BS_NS, ctx->d_vox_order.as<int>(), ctx->d_slot_frame.as<int>(),
                                        ctx->d_slot_np.as<int>(), ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB,
                                        KB, TB, dv, ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(),
-                                       ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0);
+                                       ctx->d_slot_nv.as<int>(), fb1, st + BS_VXFB, vx_global >= 1 ? 1 : 0,
+                                       ctx->d_slot_grid.as<double>());
                 };
                 auto tier2 = [&](auto kern) {
                     hipLaunchKernelGGL(kern, dim3(ctx->num_cu), dim3(mc::kVxT2), 0, s,
                                        st + BS_VXFB, fb1, ctx->d_slot_frame.as<int>(), ctx->d_slot_np.as<int>(),
                                        ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
                                        ctx->d_vx_pvid.as<int>(), ctx->d_vpts.as<double>(), ctx->d_slot_nv.as<int>(), fb2,
-                                       st + BS_VXFB2, vx_global == 1 ? 1 : 0);
+                                       st + BS_VXFB2, vx_global == 1 ? 1 : 0, ctx->d_slot_grid.as<double>());
                 };
                 // five workgroups per CU (32 KB of LDS, <= 96 VGPRs each) for the first tier
                 tier1(mc::k_bp_voxel_lds<mc::kVxT, mc::kVxH, mc::kVxV, 0, mc::kVxWpe>, mc::kVxWpe);
@@ -2392,7 +2393,7 @@ int mc_backproject(mc_ctx *ctx, int32_t num_frames, int32_t height, int32_t widt
                                    ctx->d_slot_pix.as<int>(), ctx->d_pix_list.as<unsigned>(), dB, KB, TB, dv,
                                    ctx->d_hkey.as<unsigned long long>(), ctx->d_hvid.as<int>(), ctx->d_hfirst.as<int>(),
                                    ctx->d_vox_entry.as<int>(), ctx->d_acc.as<double>(), ctx->d_vpts.as<double>(),
-                                   ctx->d_slot_nv.as<int>(), st + BS_VOXERR);
+                                   ctx->d_slot_nv.as<int>(), st + BS_VOXERR, ctx->d_slot_grid.as<double>());
                 bp_debug_sync(s, "bp_voxel");
             }
             {

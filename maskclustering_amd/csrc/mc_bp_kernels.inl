@@ -648,7 +648,7 @@ __global__ __launch_bounds__(T, WPE) void k_bp_voxel_lds(const int *__restrict__
                                                     const double *__restrict__ intr, const double *__restrict__ pose,
                                                     BpDev pr, int *__restrict__ vcnt, double *__restrict__ vpts,
                                                     int *__restrict__ slot_nv, int *__restrict__ fb_list,
-                                                    int *__restrict__ fb_cnt, int force_fb)
+                                                    int *__restrict__ fb_cnt, int force_fb, double *__restrict__ slot_grid)
 {
     static_assert(T % 64 == 0 && T <= 1024 && V <= 0xFFFF, "chunk-first thread ids and voxel ids share 16 bits");
     constexpr int NW = T / 64;
@@ -715,6 +715,10 @@ __global__ __launch_bounds__(T, WPE) void k_bp_voxel_lds(const int *__restrict__
         double vmin[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) vmin[c] = uniform_d(mn[c] - pr.vs * 0.5);  // (scalar registers)
+        // the slot's denoise grid origin (below every voxel mean: a mean of points >= the min bound)
+        if (t == 0)
+#pragma unroll
+            for (int c = 0; c < 3; c++) slot_grid[8 * static_cast<size_t>(s) + c] = vmin[c];
         // 1. chunks in list order: voxel ids in first-occurrence order and the running sums
         int nv = 0;
         unsigned ivA = t < n ? pl[t] : 0u;              // this chunk's pixel
@@ -919,7 +923,8 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
                                                   unsigned long long *__restrict__ hkey, int *__restrict__ hvid,
                                                   int *__restrict__ hfirst, int *__restrict__ vox_entry,
                                                   double *__restrict__ acc, double *__restrict__ vpts,
-                                                  int *__restrict__ slot_nv, int *__restrict__ errflag)
+                                                  int *__restrict__ slot_nv, int *__restrict__ errflag,
+                                                  double *__restrict__ slot_grid)
 {
     __shared__ double sp[256 * 3];
     __shared__ double red[24];
@@ -949,6 +954,9 @@ __global__ __launch_bounds__(256) void k_bp_voxel(const int *__restrict__ dNS, c
         double vmin[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) vmin[c] = mn[c] - pr.vs * 0.5;
+        if (t == 0)  // the slot's denoise grid origin (as k_bp_voxel_lds)
+#pragma unroll
+            for (int c = 0; c < 3; c++) slot_grid[8 * static_cast<size_t>(s) + c] = vmin[c];
         const unsigned C = 2u * static_cast<unsigned>(n);
         unsigned long long *hk = hkey + 2 * static_cast<size_t>(base);
         int *hv = hvid + 2 * static_cast<size_t>(base);
@@ -1345,6 +1353,7 @@ struct BpLdsGrid {
 };
 
 constexpr unsigned long long kKeptBit = 1ull << 63;
+constexpr int kBpCellMax = (1 << 21) - 2;  // denoise grid cells per axis: pack3's 21 bits, a neighbour's + 1 included
 constexpr int kLdsCellUnroll = 2;  // records in flight per cell scan (VGPR budget: 128 at 4 waves/SIMD)
 
 // fn(q, d2) for every sorted position q of cell (x, y, z) whose key (with `with` bits set) matches;
@@ -1859,30 +1868,26 @@ __global__ __launch_bounds__(BpLdsClass<N>::T, BpLdsClass<N>::kWgPerCu * BpLdsCl
 #endif
         BP_STAMP(16);
         const double *P = vpts + 3 * static_cast<size_t>(base);
-        // 1. bounding box -> grid origin and cell range
-        double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-        for (int i = t; i < n; i += T)
+        // 1. grid origin: the voxel kernel's min bound of the slot (slot_grid[0..2], below every
+        //    voxel mean), so no bounding-box pass; the grid is this kernel's own search structure (any
+        //    origin below the points gives the same neighbour sets), and cells beyond the points are
+        //    empty buckets, so the extent bound is just the key range
+        double mn[3];
+        {
+            const double *gm0 = slot_grid + 8 * static_cast<size_t>(s);
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                mn[c] = fmin(mn[c], P[3 * i + c]);
-                mx[c] = fmax(mx[c], P[3 * i + c]);
-            }
-        block_minmax3_nw<NW>(mn, mx, red);
+            for (int c = 0; c < 3; c++) mn[c] = uniform_d(gm0[c]);
+        }
         BpLdsGrid g;
         g.pt = spt;
         g.bs = sA;
         g.nb = static_cast<unsigned>(NBK * n);
 #pragma unroll
-        for (int c = 0; c < 3; c++) g.cmax[c] = static_cast<int>(floor((mx[c] - mn[c]) / pr.ce));
-        if (t == 0) {  // the grid's origin, extent and size for k_bp_knn_ring, written while they are fresh
-            // (read back at the end of the slot, thread 0's origin was seen to differ from the one the
-            // cell keys were made with, in one build: DESIGN.md §4, "S1 race investigation")
+        for (int c = 0; c < 3; c++) g.cmax[c] = kBpCellMax;
+        if (t == 0) {  // the grid's extent and size for k_bp_knn_ring (the origin is in place)
             double *gm = slot_grid + 8 * static_cast<size_t>(s);
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                gm[c] = mn[c];
-                gm[3 + c] = static_cast<double>(g.cmax[c]);
-            }
+            for (int c = 0; c < 3; c++) gm[3 + c] = static_cast<double>(kBpCellMax);
             gm[6] = static_cast<double>(g.nb);
             gm[7] = static_cast<double>(n);
         }
