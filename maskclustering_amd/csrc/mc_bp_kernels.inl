@@ -60,15 +60,14 @@ __device__ unsigned g_bp_slot_time[1 << 16];  // per-slot busy time (10 ns ticks
 #define BP_STAMP(k) do { } while (0)
 #endif
 
+// cell hash for the hashed grids (bucket = mod_mul(hash, buckets), i.e. the hash's high bits): a
+// linear form with odd golden-ratio-like multipliers (three multiply-adds; the walks hash up to 27
+// cells per point, so the hash is on their critical path); the buckets only need cells spread out,
+// the key test separates the cells a bucket shares
 __device__ __forceinline__ unsigned bp_hash3(int x, int y, int z)
 {
-    unsigned h = static_cast<unsigned>(x) * 0x9E3779B1u;
-    h ^= static_cast<unsigned>(y) * 0x85EBCA77u + (h << 6) + (h >> 2);
-    h ^= static_cast<unsigned>(z) * 0xC2B2AE3Du + (h << 6) + (h >> 2);
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    h ^= h >> 12;
-    return h;
+    return static_cast<unsigned>(x) * 0x9E3779B1u + static_cast<unsigned>(y) * 0x85EBCA77u +
+           static_cast<unsigned>(z) * 0xC2B2AE3Du;
 }
 __device__ __forceinline__ unsigned bp_hash64(unsigned long long k)
 {
