@@ -1361,7 +1361,8 @@ template <typename Fn>
 __device__ __forceinline__ void lds_cell(const BpLdsGrid &g, int x, int y, int z, unsigned long long with, double ax,
                                          double ay, double az, Fn &&fn)
 {
-    if (x < 0 || y < 0 || z < 0 || x > g.cmax[0] || y > g.cmax[1] || z > g.cmax[2]) return;
+    // (no bounds test: coordinates are >= -2 (the origin lies below every point) and far below
+    // kBpCellMax; a negative one makes a key with its top bits set, which no record has)
     const unsigned long long key = pack3(x, y, z) | with;
     const unsigned long long mask = ~0ull ^ (with ? 0ull : kKeptBit);
     const unsigned b = mod_mul(bp_hash3(x, y, z), g.nb);
@@ -1395,7 +1396,8 @@ __device__ __forceinline__ void lds_cells27(const BpLdsGrid &g, int x, int y, in
     const unsigned long long mask = ~0ull ^ (with ? 0ull : kKeptBit);
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
-        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        // (no bounds test: coordinates are >= -2 (the origin lies below every point) and far below
+        // kBpCellMax; a negative one makes a key with its top bits set, which no record has)
         key = pack3(cx, cy, cz) | with;
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(g.bs[b], g.bs[b + 1]);
@@ -1467,7 +1469,8 @@ __device__ __forceinline__ int lds_eps_list(const BpLdsGrid &g, int x, int y, in
 {
     auto range = [&](int d, unsigned long long &key) {
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
-        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        // (no bounds test: coordinates are >= -2 (the origin lies below every point) and far below
+        // kBpCellMax; a negative one makes a key with its top bits set, which no record has)
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(g.bs[b], g.bs[b + 1]);
@@ -1529,7 +1532,8 @@ __device__ __forceinline__ void lds_eps_pairs(const BpLdsGrid &g, int x, int y, 
             return d == 12 ? make_int2(s0, w1) : make_int2(q + 1, f1);
         }
         const int cx = x + d % 3 - 1, cy = y + (d / 3) % 3 - 1, cz = z + d / 9 - 1;
-        if (cx < 0 || cy < 0 || cz < 0 || cx > g.cmax[0] || cy > g.cmax[1] || cz > g.cmax[2]) return make_int2(0, 0);
+        // (no bounds test: coordinates are >= -2 (the origin lies below every point) and far below
+        // kBpCellMax; a negative one makes a key with its top bits set, which no record has)
         key = pack3(cx, cy, cz);
         const unsigned b = mod_mul(bp_hash3(cx, cy, cz), g.nb);
         return make_int2(g.bs[b], g.bs[b + 1]);
