@@ -145,7 +145,7 @@ SQ_DENOISE_FRAMES = 100     # the counter pass: C3 frames 600-699 (scripts/pmc_k
 CLOCK_GHZ = 2.4             # MI355X engine clock (MI355X_MICROARCH.md)
 
 
-def denoise_valu(frames, launches, avg_s):
+def denoise_valu(frames, launches, avg_s, voxels=None):
     """The denoise's second bound: VALU issue.  The committed SQ pass gives the size classes' VALU
     instructions per frame; times the frames of one launch (a batch), x 4 cycles per wave64
     instruction (a SIMD is 16 lanes wide), over the SIMDs' cycles in the live launch time."""
@@ -173,6 +173,9 @@ def denoise_valu(frames, launches, avg_s):
             per[k.replace("mc::", "")] = e
     if per:
         out["per_kernel"] = per
+    if voxels:  # the scene's voxels (denoise inputs) per launch
+        out["insts_per_voxel"] = round(per_launch / (voxels / max(launches, 1)), 1)
+        out["insts_per_voxel_note"] = "wave64 VALU instructions per input voxel (the SQ pass's frames scaled to the launch)"
     return out
 
 
@@ -1051,7 +1054,9 @@ def main():
     roof["kernel"] = dominant
     roof["launches_timed"] = int(dom_n)
     if dominant == "bp_denoise":
-        roof["valu"] = denoise_valu(runner.shape[0], calib[dominant][1], dom_ms / max(dom_n, 1) / 1e3)
+        s1c = getattr(runner, "s1ctx", None) or getattr(runner, "ctx", None)
+        nvox = int(s1c.bp_candidates()[:, 3].sum()) if s1c is not None else None
+        roof["valu"] = denoise_valu(runner.shape[0], calib[dominant][1], dom_ms / max(dom_n, 1) / 1e3, nvox)
     if pmc.get(dominant):
         roof["traffic_source"] = os.path.relpath(pmc_path, REPO)
     stages = {}
